@@ -1,0 +1,44 @@
+# Builds libdwpa22000.so (HIP for gfx950 + host C++) in-tree, and the CPU parity oracle (test infrastructure).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-function
+SRC := dwpa_amd/csrc
+OBJ := build/obj
+LIB := dwpa_amd/lib/libdwpa22000.so
+HDRS := $(wildcard $(SRC)/*.hpp) include/dwpa22000.h
+OBJS := $(OBJ)/kernels.o $(OBJ)/rules_dev.o $(OBJ)/engine.o $(OBJ)/m22000_host.o $(OBJ)/crack.o $(OBJ)/rules.o
+
+all: $(LIB) oracle
+
+$(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(OBJ)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p dwpa_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -lz -lpthread
+
+oracle:
+	$(MAKE) -s -C oracle
+
+asm: $(SRC)/kernels.hip $(HDRS)
+	@mkdir -p build/asm
+	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o build/asm/kernels.o -save-temps=obj -Rpass-analysis=kernel-resource-usage
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean asm
+
+tools: tools/bin/valu_peak
+
+tools/bin/valu_peak: tools/valu_peak.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+.PHONY: tools

@@ -1,0 +1,230 @@
+"""bench.py -- PMK/s (PBKDF2-HMAC-SHA1 x4096) of the m22000 engine on MI355X, BASELINE.json configs[1] (C2).
+
+Workload (per GPU): one ESSID, one EAPOL keyver-2 hashline (message_pair 0x80, planted nonce correction +3 LE,
+PHP nonce window nc=8 -> 21 attempts), a 100M-word synthetic dictionary resident in HBM (uint64 offsets +
+bytes, lengths geometric around 10 clipped to [8, 63]; the true PSK is word 99,999,000).  A step = one batch
+of the dictionary through the hot path: candidates -> HMAC midstates -> PBKDF2 -> verify.  Rank r of N scans
+batches r, r+N, ... (static keyspace shards, no collective on the data path): weak scaling.
+
+The JSON line carries the PBKDF2 kernel's roofline (integer VALU bound) from HIP events recorded around each
+launch on the stream it runs on, and the CPU baseline (the OpenSSL restatement of check_key_m22000 from
+oracle/, timed on this host's cores on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "PMK/s (PBKDF2-HMAC-SHA1 x4096) per GPU and per 8×MI355X node, m22000"
+DICT_WORDS = 100_000_000
+PLANT_INDEX = 99_999_000
+NC = 8
+# Algorithmic work per PMK: 16,388 SHA-1 compressions (north_star), each priced at the minimal gfx950 VALU
+# instruction count of the HMAC inner-loop compression (DESIGN.md "roofline"): 78 rounds x 5 + rounds 0-1 in
+# 3 (midstate invariants) + 176 schedule ops (constant-folded padding) + 5 digest adds + 2.5 for T ^= U.
+COMPRESSIONS_PER_PMK = 16388
+OPS_PER_COMPRESSION = 576.5
+# gfx950: 256 CUs x 4 SIMD-32 (a wave64 VALU op issues over 2 cycles) = 128 int32 lane-ops / clk / CU, 2.4 GHz.
+PEAK_LANE_OPS = 256 * 128 * 2.4e9
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1 << 22, help="candidates per step per GPU")
+    ap.add_argument("--dict-words", type=int, default=DICT_WORDS)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def make_dictionary(torch, n, dev, seed=2):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    lens = torch.empty(n, dtype=torch.float32, device=dev).geometric_(0.3, generator=g).add_(7).clamp_(8, 63)
+    lens = lens.to(torch.int64)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(lens, 0, out=off[1:])
+    total = int(off[-1].item())
+    data = torch.randint(0x21, 0x7F, (total + 64,), dtype=torch.uint8, device=dev, generator=g)
+    return off, data, lens
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import dwpa_amd
+    from dwpa_amd import synth as S
+
+    n = args.dict_words
+    plant = min(PLANT_INDEX, n - 1)
+    off, data, lens = make_dictionary(torch, n, dev)
+    b0, b1 = int(off[plant].item()), int(off[plant + 1].item())
+    psk = data[b0:b1].cpu().numpy().tobytes()
+    import random
+    rng = random.Random(1)
+    essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
+    line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rng)
+
+    B = (args.batch + 63) & ~63
+    nbatches = (n + B - 1) // B
+    stream = torch.cuda.Stream(device=dev)
+    hs = stream.cuda_stream
+    sc = dwpa_amd.Scan([line], device=local, nc=NC, nc_mode=0, batch=B)
+
+    def batch_range(i):
+        first = (i % nbatches) * B
+        return first, min(B, n - first)
+
+    def step(i, ev=None):
+        first, cnt = batch_range(i)
+        sc.load_dict(off.data_ptr(), data.data_ptr(), first, cnt, 8, 63, hs)
+        if ev is not None:
+            ev[0].record(stream)
+        sc.pbkdf2(0, hs)
+        if ev is not None:
+            ev[1].record(stream)
+        sc.verify(0, hs)
+        return cnt
+
+    torch.cuda.synchronize()
+    for w in range(args.warmup):
+        step(rank + w * world)
+    stream.synchronize()
+    sc.hits(hs)  # drop warmup hits
+
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    counts = []
+    for s in range(args.steps):
+        counts.append(step(rank + (args.warmup + s) * world, kev[s]))
+        done += counts[-1]
+    stream.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms = [a.elapsed_time(b) for a, b in kev]
+    kernel_ms = sum(kms) / len(kms)
+
+    t = torch.tensor([elapsed, float(done)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tm = t[:1].clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        td = t[1:].clone()
+        dist.all_reduce(td, op=dist.ReduceOp.SUM)
+        elapsed, total = float(tm.item()), float(td.item())
+    else:
+        total = float(done)
+
+    # correctness: the batch holding the planted PSK must report it with nc +3 LE and the right PMK (untimed)
+    pi = plant // B
+    step(pi)
+    hits = sc.hits(hs)
+    verified = any(h["cand"] == plant and h["nc"] == 3 and h["endian"] == "LE" and h["pmk"] == S.pmk(psk, essid)
+                   for h in hits)
+
+    pmk_per_launch = sum(counts) / len(counts)
+    achieved = sum(counts) * COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION / (sum(kms) * 1e-3)
+    result = None
+    if rank == 0:
+        value = total / elapsed
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(line, data, off, lens, plant, args.cpu_seconds)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "PMK/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {
+                "workload": "C2: one ESSID, one EAPOL keyver-2 line (mp 0x80, planted NC +3 LE), 100M-word "
+                            "synthetic dictionary resident in HBM, PHP nonce window nc=8 (21 attempts)",
+                "dict_words": n,
+                "batch_per_step": B,
+                "parallelism": f"keyspace shards x{world}, no collective on the data path",
+            },
+            "roofline": {
+                "bound": "valu",
+                "kernel": "k_pbkdf2",
+                "achieved": round(achieved / 1e12, 3),
+                "peak": round(PEAK_LANE_OPS / 1e12, 3),
+                "unit": "TOP/s (int32 VALU lane-ops)",
+                "frac": round(achieved / PEAK_LANE_OPS, 4),
+                "traffic": None,
+                "kernel_ms": round(kernel_ms, 3),
+                "pmk_per_launch": pmk_per_launch,
+                "ops_per_pmk": COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION,
+                "roofline_pmk_per_s": round(PEAK_LANE_OPS / (COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION), 1),
+            },
+            "cpu_baseline": cpu,
+            "hits_verified": bool(verified),
+        }
+        print(json.dumps(result), flush=True)
+    sc.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0 and not verified:
+        sys.exit(3)
+
+
+def cpu_baseline(line, data, off, lens, plant, seconds):
+    """The PHP CPU path: check_key_m22000(line, [word]) per word (one PHP request per key, as put_work does),
+    restated in C on OpenSSL (oracle/), on this host's cores; bounded sample ending at the planted PSK."""
+    from oracle import oracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+
+    def words(lo, hi):
+        o = off[lo:hi + 1].cpu().tolist()
+        raw = data[o[0]:o[-1]].cpu().numpy().tobytes()
+        return [raw[o[i] - o[0]:o[i + 1] - o[0]] for i in range(hi - lo)]
+
+    probe = words(plant - 64 * threads + 1, plant + 1)
+    t0 = time.perf_counter()
+    idx, res = O.c_check_many(line, probe, NC, threads)
+    dt = time.perf_counter() - t0
+    rate = len(probe) / dt
+    m = int(max(len(probe), min(400_000, rate * seconds)))
+    sample = words(plant - m + 1, plant + 1)
+    t0 = time.perf_counter()
+    idx, res = O.c_check_many(line, sample, NC, threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+            "sample": f"{len(sample)} dictionary words ending at the planted PSK, check_key_m22000 per word "
+                      f"(OpenSSL PKCS5_PBKDF2_HMAC + 21 NC attempts), {dt:.1f} s",
+            "found_planted": idx == len(sample) - 1}
+
+
+if __name__ == "__main__":
+    main()

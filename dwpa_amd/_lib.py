@@ -1,0 +1,120 @@
+"""ctypes binding of libdwpa22000.so (include/dwpa22000.h).
+
+There is no CPU fallback: importing works anywhere (so the CPU test suite can check exports), but every compute
+entry point returns DWPA_E_NODEV without a gfx950 device and the wrappers raise ``DwpaError`` -- loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DWPA_LIB", os.path.join(HERE, "lib", "libdwpa22000.so"))
+HEADER = os.path.join(os.path.dirname(HERE), "include", "dwpa22000.h")
+
+DWPA_MISS, DWPA_HIT = 0, 1
+DWPA_E_FORMAT, DWPA_E_HEX, DWPA_E_TYPE, DWPA_E_KEYVER = -1, -2, -3, -4
+DWPA_E_NODEV, DWPA_E_HIP, DWPA_E_ARG, DWPA_E_NOMEM, DWPA_E_IO, DWPA_E_OVERFLOW, DWPA_E_RULE = -10, -11, -12, -13, -14, -15, -16
+DWPA_RC_CRACKED, DWPA_RC_EXHAUSTED, DWPA_RC_ERROR = 0, 1, -1
+DWPA_NC_PHP, DWPA_NC_HASHCAT = 0, 1
+
+
+class DwpaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"dwpa error {code}: {msg}")
+        self.code = code
+
+
+class Bytes(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("key_index", ctypes.c_int32), ("nc", ctypes.c_int32), ("endian", ctypes.c_int8),
+                ("nc_valid", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2), ("pmk", ctypes.c_uint8 * 32)]
+
+
+class Job(ctypes.Structure):
+    _fields_ = [("line", ctypes.c_char_p), ("line_len", ctypes.c_size_t), ("keys", ctypes.POINTER(Bytes)),
+                ("nkeys", ctypes.c_size_t), ("pmk", ctypes.c_char_p), ("nc", ctypes.c_int32)]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device_mask", ctypes.c_uint32), ("batch", ctypes.c_uint32),
+                ("nc_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+
+
+class Hit(ctypes.Structure):
+    _fields_ = [("cand", ctypes.c_uint64), ("line", ctypes.c_uint32), ("nc", ctypes.c_int32), ("endian", ctypes.c_int8),
+                ("nc_valid", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2), ("pmk", ctypes.c_uint8 * 32)]
+
+
+_P = ctypes.c_void_p
+SIGNATURES = {
+    "dwpa_abi_version": ([], ctypes.c_int),
+    "dwpa_init": ([ctypes.POINTER(Config)], ctypes.c_int),
+    "dwpa_device_count": ([], ctypes.c_int),
+    "dwpa_strerror": ([ctypes.c_int], ctypes.c_char_p),
+    "dwpa_shutdown": ([], None),
+    "dwpa_check_m22000": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Bytes), ctypes.c_size_t, ctypes.c_char_p,
+                           ctypes.c_int, ctypes.POINTER(Result)], ctypes.c_int),
+    "dwpa_check_batch": ([ctypes.POINTER(Job), ctypes.c_size_t, ctypes.POINTER(Result), ctypes.POINTER(ctypes.c_int)],
+                         ctypes.c_int),
+    "dwpa_pbkdf2_pmk": ([ctypes.POINTER(Bytes), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),
+    "dwpa_hc_unhex": ([ctypes.c_char_p, ctypes.c_size_t, _P, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    "dwpa_hash_m22000": ([ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),
+    "dwpa_crack_files": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
+                          ctypes.c_char_p, ctypes.POINTER(Config)], ctypes.c_int),
+    "dwpa_rules_expand": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Bytes), ctypes.c_size_t, _P, _P,
+                           ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "dwpa_scan_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
+                          ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_P)], ctypes.c_int),
+    "dwpa_scan_num_groups": ([_P], ctypes.c_int),
+    "dwpa_scan_line_status": ([_P, ctypes.c_size_t], ctypes.c_int),
+    "dwpa_scan_load_dict": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P],
+                            ctypes.c_int),
+    "dwpa_scan_load_numeric": ([_P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P], ctypes.c_int),
+    "dwpa_scan_pbkdf2": ([_P, ctypes.c_int, _P], ctypes.c_int),
+    "dwpa_scan_verify": ([_P, ctypes.c_int, _P], ctypes.c_int),
+    "dwpa_scan_hits": ([_P, ctypes.POINTER(Hit), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), _P], ctypes.c_int),
+    "dwpa_scan_loaded": ([_P, ctypes.POINTER(ctypes.c_uint32), _P], ctypes.c_int),
+    "dwpa_scan_destroy": ([_P], None),
+}
+
+_lib = None
+
+
+def load():
+    """Load the shared library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DwpaError(DWPA_E_NODEV, f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = "") -> int:
+    if rc < 0 and rc not in (DWPA_E_FORMAT, DWPA_E_HEX, DWPA_E_TYPE, DWPA_E_KEYVER):
+        raise DwpaError(rc, (what + ": " if what else "") + load().dwpa_strerror(rc).decode(errors="replace"))
+    return rc
+
+
+def bytes_array(items):
+    """Python sequence of bytes/None -> (ctypes array of Bytes, keep-alive list)."""
+    arr = (Bytes * max(1, len(items)))()
+    keep = []
+    for i, k in enumerate(items):
+        if k is None:
+            arr[i].ptr, arr[i].len = None, 0
+        else:
+            k = bytes(k)
+            b = ctypes.create_string_buffer(k, len(k) + 1)
+            keep.append(b)
+            arr[i].ptr, arr[i].len = ctypes.cast(b, ctypes.c_void_p), len(k)
+    return arr, keep

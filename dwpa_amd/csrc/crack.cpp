@@ -1,0 +1,350 @@
+// crack.cpp -- dwpa_crack_files(): the in-process replacement of help_crack.py's hashcat subprocess
+// (run_cracker, help_crack/help_crack.py:765-802; command line :773; rc handling :776-786; outfile parsed by
+// get_key :804-879).
+//
+// Work distribution: the dictionary stream is cut into chunks; each chunk is split into contiguous, equal
+// shards, one per active device, and every device thread scans its shard in batches (load -> per-ESSID PBKDF2 ->
+// verify).  There is no device-to-device traffic: hits (a few bytes) are gathered on the host, where the first
+// hit of each hashline is written to the outfile and the line is retired on every device (hashcat reports each
+// hash once).  Rules (hashcat -r, help_crack.py:445-447,931-933) are applied on the GPU (rules.cpp).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "dwpa22000.h"
+#include "engine.hpp"
+#include "m22000_host.hpp"
+#include "rules.hpp"
+
+namespace dwpa {
+
+struct Chunk {
+    std::vector<uint64_t> off;  // words+1 offsets
+    std::string bytes;          // concatenated words (decoded)
+    size_t words() const { return off.empty() ? 0 : off.size() - 1; }
+};
+
+// Dictionary reader: plain or gzip (zlib reads both), one word per line, "\n" or "\r\n", $HEX[] decoded.
+class DictReader {
+  public:
+    explicit DictReader(const std::vector<std::string>& paths) : paths_(paths) {}
+    // Returns false at the end of all files; sets err on I/O failure.
+    bool next(Chunk& c, size_t max_words, size_t max_bytes, bool& err) {
+        c.off.clear();
+        c.bytes.clear();
+        c.off.push_back(0);
+        while (c.words() < max_words && c.bytes.size() < max_bytes) {
+            if (!gz_) {
+                if (idx_ >= paths_.size()) break;
+                gz_ = gzopen(paths_[idx_].c_str(), "rb");
+                if (!gz_) { err = true; return false; }
+                gzbuffer(gz_, 1 << 20);
+            }
+            std::string line;
+            if (!getline(line)) {
+                gzclose(gz_);
+                gz_ = nullptr;
+                idx_++;
+                continue;
+            }
+            if (starts_hex((const uint8_t*)line.data(), line.size())) line = hc_unhex(line);
+            c.bytes += line;
+            c.off.push_back(c.bytes.size());
+        }
+        return c.words() > 0;
+    }
+    ~DictReader() {
+        if (gz_) gzclose(gz_);
+    }
+
+  private:
+    bool getline(std::string& out) {
+        out.clear();
+        for (;;) {
+            if (pos_ >= len_) {
+                int r = gzread(gz_, buf_, sizeof(buf_));
+                if (r <= 0) {
+                    if (out.empty() && !pending_) return false;
+                    pending_ = false;
+                    break;
+                }
+                len_ = (size_t)r;
+                pos_ = 0;
+            }
+            const char* b = buf_ + pos_;
+            const void* nl = memchr(b, '\n', len_ - pos_);
+            if (nl) {
+                size_t k = (const char*)nl - b;
+                out.append(b, k);
+                pos_ += k + 1;
+                pending_ = false;
+                break;
+            }
+            out.append(b, len_ - pos_);
+            pending_ = true;
+            pos_ = len_;
+        }
+        if (!out.empty() && out.back() == '\r') out.pop_back();
+        return true;
+    }
+    std::vector<std::string> paths_;
+    size_t idx_ = 0;
+    gzFile gz_ = nullptr;
+    char buf_[1 << 16];
+    size_t pos_ = 0, len_ = 0;
+    bool pending_ = false;
+};
+
+struct CrackShared {
+    std::mutex mu;
+    std::vector<uint8_t> cracked;         // per input line
+    std::vector<ParsedLine> parsed;
+    FILE* out = nullptr;
+    size_t valid = 0, ncracked = 0;
+    int error = 0;
+};
+
+static std::string outfile_record(const ParsedLine& p, const std::string& psk) {
+    const std::string& target = p.kind == LINE_PMKID ? p.pmkid : p.keymic;
+    return hex_lower(target.substr(0, 16)) + ":" + hex_lower(p.mac_ap) + ":" + hex_lower(p.mac_sta) + ":" +
+           hashcat_plain(p.essid) + ":" + hashcat_plain(psk) + "\n";
+}
+
+struct DevWork {
+    int device;
+    dwpa_scan* scan = nullptr;
+    DevBuf off, bytes;
+    hipStream_t stream = nullptr;
+};
+
+static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, size_t e, const RuleSet* rules,
+                      DevRules* drules) {
+    if (e <= b) return 0;
+    if (hipSetDevice(w.device) != hipSuccess) return DWPA_E_HIP;
+    // upload shard (offsets rebased to the shard)
+    std::vector<uint64_t> off(e - b + 1);
+    for (size_t i = b; i <= e; i++) off[i - b] = c.off[i] - c.off[b];
+    const size_t nbytes = c.off[e] - c.off[b];
+    if (w.off.ensure(off.size() * 8) || w.bytes.ensure(nbytes + 64)) return DWPA_E_NOMEM;
+    if (hipMemcpyAsync(w.off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, w.stream) != hipSuccess ||
+        hipMemcpyAsync(w.bytes.p, c.bytes.data() + c.off[b], nbytes, hipMemcpyHostToDevice, w.stream) != hipSuccess)
+        return DWPA_E_HIP;
+    const uint32_t cap = scan_batch_cap(w.scan);
+    const int ngroups = dwpa_scan_num_groups(w.scan);
+    const size_t words = e - b;
+    const uint64_t nrules = rules ? rules->size() : 1;
+    const uint64_t total = words * nrules;
+    // candidate id = word * nrules + rule; batches walk the candidate space in order
+    const uint32_t words_per_batch = rules ? std::max<uint32_t>(1, cap / (uint32_t)nrules) : cap;
+    for (size_t wb = 0; wb < words; wb += words_per_batch) {
+        const uint32_t nw = (uint32_t)std::min<size_t>(words_per_batch, words - wb);
+        int r;
+        if (rules)
+            r = rules_load(w.scan, drules, (const uint64_t*)w.off.p, (const uint8_t*)w.bytes.p, wb, nw, w.stream);
+        else
+            r = scan_load_dict(w.scan, (const uint64_t*)w.off.p, (const uint8_t*)w.bytes.p, wb, nw, 8, 63, w.stream);
+        if (r < 0) return r;
+        for (int g = 0; g < ngroups; g++) {
+            if ((r = scan_pbkdf2(w.scan, g, w.stream)) < 0) return r;
+            if ((r = scan_verify(w.scan, g, w.stream)) < 0) return r;
+        }
+        std::vector<HitDev> hits;
+        if ((r = scan_hits_raw(w.scan, hits, w.stream)) < 0) return r;
+        if (hits.empty()) continue;
+        std::sort(hits.begin(), hits.end(), [](const HitDev& x, const HitDev& y) { return x.cand < y.cand; });
+        std::lock_guard<std::mutex> lk(sh.mu);
+        for (const HitDev& h : hits) {
+            dwpa_hit ph;
+            hit_to_public(w.scan, h, ph);
+            if (sh.cracked[ph.line]) continue;
+            const uint64_t word = h.cand / nrules, rule = h.cand % nrules;
+            std::string plain(c.bytes.data() + c.off[b + word], c.off[b + word + 1] - c.off[b + word]);
+            if (rules) plain = rules->apply_host((size_t)rule, plain);
+            sh.cracked[ph.line] = 1;
+            sh.ncracked++;
+            const std::string rec = outfile_record(sh.parsed[ph.line], plain);
+            fwrite(rec.data(), 1, rec.size(), sh.out);
+            fflush(sh.out);
+        }
+        (void)total;
+    }
+    return 0;
+}
+
+static int crack_impl(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file, int nec,
+                      const char* out_file, const dwpa_config* cfg) {
+    if (!hash_file || !out_file || (!dicts && ndicts)) return DWPA_RC_ERROR;
+    if (cfg && dwpa_init(cfg) < 0) return DWPA_RC_ERROR;
+    if (engine_init() < 0) return DWPA_RC_ERROR;
+    std::vector<int> devs = engine_devices();
+    if (devs.empty()) return DWPA_RC_ERROR;
+    const int nc_mode = cfg ? cfg->nc_mode : DWPA_NC_HASHCAT;
+
+    // hash file
+    std::vector<std::string> lines;
+    {
+        FILE* f = fopen(hash_file, "rb");
+        if (!f) return DWPA_RC_ERROR;
+        std::string cur;
+        int ch;
+        while ((ch = fgetc(f)) != EOF) {
+            if (ch == '\n') {
+                if (!cur.empty() && cur.back() == '\r') cur.pop_back();
+                if (!cur.empty()) lines.push_back(cur);
+                cur.clear();
+            } else cur.push_back((char)ch);
+        }
+        if (!cur.empty() && cur.back() == '\r') cur.pop_back();
+        if (!cur.empty()) lines.push_back(cur);
+        fclose(f);
+    }
+    CrackShared sh;
+    sh.parsed.resize(lines.size());
+    sh.cracked.assign(lines.size(), 0);
+    for (size_t i = 0; i < lines.size(); i++) {
+        sh.parsed[i] = parse_m22000(lines[i].data(), lines[i].size());
+        if (sh.parsed[i].status) sh.cracked[i] = 1;  // rejected by the parser (hashcat: token exception)
+        else sh.valid++;
+    }
+    if (sh.valid == 0) return DWPA_RC_ERROR;  // hashcat: "No hashes loaded"
+
+    RuleSet rules;
+    const RuleSet* rp = nullptr;
+    if (rules_file) {
+        if (rules.load_file(rules_file) < 0) return DWPA_RC_ERROR;
+        if (!rules.all_noop()) rp = &rules;
+    }
+
+    sh.out = fopen(out_file, "ab");
+    if (!sh.out) return DWPA_RC_ERROR;
+
+    std::vector<const char*> lp(lines.size());
+    std::vector<size_t> ll(lines.size());
+    for (size_t i = 0; i < lines.size(); i++) { lp[i] = lines[i].data(); ll[i] = lines[i].size(); }
+    const uint32_t batch = cfg && cfg->batch ? cfg->batch : engine_batch();
+    std::vector<DevWork> work(devs.size());
+    std::vector<DevRules> drules(devs.size());
+    int rc = 0;
+    for (size_t k = 0; k < devs.size() && rc >= 0; k++) {
+        work[k].device = devs[k];
+        hipSetDevice(devs[k]);
+        if (hipStreamCreateWithFlags(&work[k].stream, hipStreamNonBlocking) != hipSuccess) rc = DWPA_E_HIP;
+        if (rc >= 0) rc = scan_create(devs[k], lp.data(), ll.data(), lines.size(), nec, nc_mode, batch, &work[k].scan);
+        if (rc >= 0 && rp) rc = rules_upload(devs[k], rules, &drules[k]);
+    }
+
+    std::vector<std::string> dpaths;
+    for (size_t i = 0; i < ndicts; i++) dpaths.push_back(dicts[i]);
+    DictReader reader(dpaths);
+    Chunk chunk;
+    bool ioerr = false;
+    const size_t chunk_words = (size_t)batch * devs.size() * 8;
+    while (rc >= 0 && sh.ncracked < sh.valid && reader.next(chunk, chunk_words, (size_t)1 << 31, ioerr)) {
+        // retire lines cracked so far on every device
+        {
+            std::lock_guard<std::mutex> lk(sh.mu);
+            for (size_t k = 0; k < work.size(); k++)
+                for (size_t i = 0; i < lines.size(); i++)
+                    if (sh.cracked[i]) scan_mark_cracked(work[k].scan, (uint32_t)i);
+        }
+        const size_t W = chunk.words(), G = work.size();
+        std::vector<std::thread> th;
+        std::vector<int> rcs(G, 0);
+        for (size_t k = 0; k < G; k++) {
+            const size_t b = W * k / G, e = W * (k + 1) / G;
+            th.emplace_back([&, k, b, e] { rcs[k] = scan_shard(work[k], sh, chunk, b, e, rp, &drules[k]); });
+        }
+        for (auto& t : th) t.join();
+        for (int r : rcs)
+            if (r < 0) rc = r;
+    }
+    for (size_t k = 0; k < work.size(); k++) {
+        if (work[k].scan) scan_destroy(work[k].scan);
+        hipSetDevice(work[k].device);
+        work[k].off.release();
+        work[k].bytes.release();
+        rules_release(&drules[k]);
+        if (work[k].stream) hipStreamDestroy(work[k].stream);
+    }
+    fclose(sh.out);
+    if (rc < 0 || ioerr) return DWPA_RC_ERROR;
+    return sh.ncracked == sh.valid ? DWPA_RC_CRACKED : DWPA_RC_EXHAUSTED;
+}
+
+}  // namespace dwpa
+
+extern "C" {
+
+int dwpa_crack_files(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,
+                     int nonce_error_corrections, const char* out_file, const dwpa_config* cfg) {
+    return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg);
+}
+
+// md5 over fields 1..7 of the hashline (web/common.php:310-315); a tiny host MD5 keeps this dependency-free.
+static void md5_host(const uint8_t* msg, size_t len, uint8_t out[16]) {
+    static const uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+    static const int S[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+    std::string b((const char*)msg, len);
+    b.push_back((char)0x80);
+    while (b.size() % 64 != 56) b.push_back('\0');
+    const uint64_t bits = (uint64_t)len * 8;
+    for (int i = 0; i < 8; i++) b.push_back((char)(bits >> (8 * i)));
+    uint32_t h[4] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476};
+    for (size_t o = 0; o < b.size(); o += 64) {
+        uint32_t m[16];
+        for (int j = 0; j < 16; j++)
+            m[j] = (uint32_t)(uint8_t)b[o + 4 * j] | (uint32_t)(uint8_t)b[o + 4 * j + 1] << 8 |
+                   (uint32_t)(uint8_t)b[o + 4 * j + 2] << 16 | (uint32_t)(uint8_t)b[o + 4 * j + 3] << 24;
+        uint32_t a = h[0], bb = h[1], c = h[2], d = h[3];
+        for (int i = 0; i < 64; i++) {
+            uint32_t f;
+            int g;
+            if (i < 16) { f = (bb & c) | (~bb & d); g = i; }
+            else if (i < 32) { f = (d & bb) | (~d & c); g = (5 * i + 1) & 15; }
+            else if (i < 48) { f = bb ^ c ^ d; g = (3 * i + 5) & 15; }
+            else { f = c ^ (bb | ~d); g = (7 * i) & 15; }
+            uint32_t t = d;
+            d = c;
+            c = bb;
+            uint32_t x = a + f + K[i] + m[g];
+            int s = S[i >> 4][i & 3];
+            bb = bb + ((x << s) | (x >> (32 - s)));
+            a = t;
+        }
+        h[0] += a; h[1] += bb; h[2] += c; h[3] += d;
+    }
+    for (int k = 0; k < 4; k++)
+        for (int i = 0; i < 4; i++) out[4 * k + i] = (uint8_t)(h[k] >> (8 * i));
+}
+
+int dwpa_hash_m22000(const char* line, size_t line_len, uint8_t out[16]) {
+    if (!line || !out) return DWPA_E_ARG;
+    const char* f[9];
+    size_t fl[9], cnt = 0, st = 0;
+    for (size_t i = 0; i < line_len && cnt < 8; i++)
+        if (line[i] == '*') { f[cnt] = line + st; fl[cnt] = i - st; cnt++; st = i + 1; }
+    f[cnt] = line + st; fl[cnt] = line_len - st; cnt++;
+    if (cnt != 9) return DWPA_E_FORMAT;
+    std::string cat;
+    for (int i = 1; i <= 7; i++) cat.append(f[i], fl[i]);
+    md5_host((const uint8_t*)cat.data(), cat.size(), out);
+    return 0;
+}
+
+}  // extern "C"

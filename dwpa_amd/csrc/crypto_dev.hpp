@@ -1,0 +1,385 @@
+// crypto_dev.hpp -- gfx950 device primitives for the m22000 path (integer VALU only, no MFMA).
+//
+// SHA-1 is the hot primitive: PBKDF2-HMAC-SHA1 x4096 (web/common.php:178-180,246-248) is ~99 % of all work.
+// Rotates lower to v_alignbit_b32, Ch/Maj/Parity to v_bfi_b32 / v_bitop3_b32 / v_xor3_b32, and sums of three
+// to v_add3_u32.  MD5 (keyver 1 MIC, common.php:262-265), SHA-256 (keyver 3 KDF, :270-273) and AES-128
+// (CMAC, :56-112) are the verifier-side primitives; they run once per nonce-correction attempt, not 4096x.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+namespace dwpa {
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, 32u - n); }
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// ------------------------------------------------------------------------------------------------
+// SHA-1
+// ------------------------------------------------------------------------------------------------
+#define DWPA_SHA1_CH(b, c, d) ((((c) ^ (d)) & (b)) ^ (d))
+#define DWPA_SHA1_PAR(b, c, d) ((b) ^ (c) ^ (d))
+#define DWPA_SHA1_MAJ(b, c, d) (((b) & (c)) | (((b) | (c)) & (d)))
+
+constexpr uint32_t SHA1_K0 = 0x5a827999u, SHA1_K1 = 0x6ed9eba1u, SHA1_K2 = 0x8f1bbcdcu, SHA1_K3 = 0xca62c1d6u;
+constexpr uint32_t SHA1_IV0 = 0x67452301u, SHA1_IV1 = 0xefcdab89u, SHA1_IV2 = 0x98badcfeu, SHA1_IV3 = 0x10325476u,
+                   SHA1_IV4 = 0xc3d2e1f0u;
+
+template <int T>
+__device__ __forceinline__ uint32_t sha1_f(uint32_t b, uint32_t c, uint32_t d) {
+    if constexpr (T < 20) return DWPA_SHA1_CH(b, c, d);
+    else if constexpr (T < 40) return DWPA_SHA1_PAR(b, c, d);
+    else if constexpr (T < 60) return DWPA_SHA1_MAJ(b, c, d);
+    else return DWPA_SHA1_PAR(b, c, d);
+}
+template <int T>
+__device__ __forceinline__ constexpr uint32_t sha1_k() {
+    return T < 20 ? SHA1_K0 : T < 40 ? SHA1_K1 : T < 60 ? SHA1_K2 : SHA1_K3;
+}
+
+// Generic compression: st <- SHA1_compress(st, m[0..15]) (big-endian message words).
+__device__ __forceinline__ void sha1_compress(uint32_t st[5], const uint32_t m[16]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = m[i];
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
+#define DWPA_SHA1_STEP(T)                                                                                   \
+    {                                                                                                       \
+        uint32_t wt;                                                                                        \
+        if constexpr ((T) < 16) wt = w[(T)];                                                                \
+        else {                                                                                              \
+            wt = rotl(w[((T) - 3) & 15] ^ w[((T) - 8) & 15] ^ w[((T) - 14) & 15] ^ w[(T) & 15], 1);          \
+            w[(T) & 15] = wt;                                                                               \
+        }                                                                                                   \
+        uint32_t t = rotl(a, 5) + sha1_f<(T)>(b, c, d) + e + sha1_k<(T)>() + wt;                            \
+        e = d; d = c; c = rotl(b, 30); b = a; a = t;                                                        \
+    }
+#define DWPA_SHA1_STEP4(T) DWPA_SHA1_STEP(T) DWPA_SHA1_STEP(T + 1) DWPA_SHA1_STEP(T + 2) DWPA_SHA1_STEP(T + 3)
+#define DWPA_SHA1_STEP20(T) DWPA_SHA1_STEP4(T) DWPA_SHA1_STEP4(T + 4) DWPA_SHA1_STEP4(T + 8) DWPA_SHA1_STEP4(T + 12) DWPA_SHA1_STEP4(T + 16)
+    DWPA_SHA1_STEP20(0)
+    DWPA_SHA1_STEP20(20)
+    DWPA_SHA1_STEP20(40)
+    DWPA_SHA1_STEP20(60)
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
+}
+
+// HMAC-SHA1 key midstate with the per-midstate invariants of rounds 0-1 folded out of the 4096-iteration loop.
+// For a fixed state H the first two rounds only depend on H and the first two message words:
+//   round 0: a1 = rotl(H0,5) + Ch(H1,H2,H3) + H4 + K + W0            = c0 + W0
+//   round 1: a2 = rotl(a1,5) + Ch(H0,rotl(H1,30),H2) + H3 + K + W1     = rotl(a1,5) + c1 + W1
+// leaving (a2, a1, rotl(H0,30), rotl(H1,30), H2) as the state entering round 2.
+struct Sha1Mid {
+    uint32_t h0, h1, h2, h3, h4;
+    uint32_t c0, c1, r0, r1;
+};
+
+__device__ __forceinline__ Sha1Mid sha1_mid(const uint32_t h[5]) {
+    Sha1Mid m;
+    m.h0 = h[0]; m.h1 = h[1]; m.h2 = h[2]; m.h3 = h[3]; m.h4 = h[4];
+    m.r0 = rotl(h[0], 30);
+    m.r1 = rotl(h[1], 30);
+    m.c0 = rotl(h[0], 5) + DWPA_SHA1_CH(h[1], h[2], h[3]) + h[4] + SHA1_K0;
+    m.c1 = DWPA_SHA1_CH(h[0], m.r1, h[2]) + h[3] + SHA1_K0;
+    return m;
+}
+
+// 3-input XOR in one VALU op: v_bitop3_b32 with truth table 0x96 (gfx950).  LLVM selects bitop3 for Ch/Maj but
+// splits XOR3 into two v_xor_b32, which costs ~100 extra ops per compression in the schedule and parity rounds.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// Majority in one op (bitop3 truth table 0xE8); left to itself LLVM emits v_xor + v_bfi for it.
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// a ^ b ^ K with a wave-uniform constant K in an SGPR (VOP3 on gfx9 takes no literal operand).
+__device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
+// Message words of the 84-byte HMAC inner/outer message: W0..W4 variable, W5 = 0x80000000, W6..W14 = 0, W15 = 672.
+constexpr bool w84_var(int s) { return s >= 16 || s <= 4; }
+constexpr uint32_t w84_const(int s) { return s == 5 ? 0x80000000u : s == 15 ? 672u : 0u; }
+
+// W[T] before the rotate: XOR of the variable sources plus the folded constant, fewest VALU ops.
+template <int T>
+__device__ __forceinline__ uint32_t sched84(const uint32_t w[16]) {
+    constexpr int s0 = T - 3, s1 = T - 8, s2 = T - 14, s3 = T - 16;
+    constexpr uint32_t K = (w84_var(s0) ? 0u : w84_const(s0)) ^ (w84_var(s1) ? 0u : w84_const(s1)) ^
+                           (w84_var(s2) ? 0u : w84_const(s2)) ^ (w84_var(s3) ? 0u : w84_const(s3));
+    constexpr int nv = (int)w84_var(s0) + (int)w84_var(s1) + (int)w84_var(s2) + (int)w84_var(s3);
+    uint32_t v[4] = {0, 0, 0, 0};
+    int n = 0;
+    if constexpr (w84_var(s0)) v[n++] = w[s0 & 15];
+    if constexpr (w84_var(s1)) v[n++] = w[s1 & 15];
+    if constexpr (w84_var(s2)) v[n++] = w[s2 & 15];
+    if constexpr (w84_var(s3)) v[n++] = w[s3 & 15];
+    if constexpr (nv == 4) return xor3(v[0], v[1], v[2]) ^ v[3];
+    else if constexpr (nv == 3) {
+        if constexpr (K == 0) return xor3(v[0], v[1], v[2]);
+        else return xor3(v[0], v[1], v[2]) ^ K;
+    } else if constexpr (nv == 2) {
+        if constexpr (K == 0) return v[0] ^ v[1];
+        else return xor3s(v[0], v[1], K);
+    } else if constexpr (nv == 1) {
+        if constexpr (K == 0) return v[0];
+        else return v[0] ^ K;
+    } else {
+        return K;
+    }
+}
+
+template <int T>
+__device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[16]) {
+    uint32_t f;
+    if constexpr (T < 20) f = DWPA_SHA1_CH(b, c, d);
+    else if constexpr (T < 40) f = xor3(b, c, d);
+    else if constexpr (T < 60) f = maj3(b, c, d);
+    else f = xor3(b, c, d);
+    uint32_t t;
+    if constexpr (T < 16 && !w84_var(T)) {
+        t = rotl(a, 5) + f + e + (sha1_k<T>() + w84_const(T));
+    } else {
+        uint32_t wt;
+        if constexpr (T < 16) wt = w[T];
+        else {
+            wt = rotl(sched84<T>(w), 1);
+            w[T & 15] = wt;
+        }
+        t = rotl(a, 5) + f + e + sha1_k<T>() + wt;
+    }
+    e = d; d = c; c = rotl(b, 30); b = a; a = t;
+}
+
+template <int T0, int... Ts>
+__device__ __forceinline__ void steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[16],
+                                        std::integer_sequence<int, T0, Ts...>) {
+    step84<T0>(a, b, c, d, e, w);
+    if constexpr (sizeof...(Ts) > 0) steps84(a, b, c, d, e, w, std::integer_sequence<int, Ts...>{});
+}
+template <int Lo, int... Is>
+__device__ __forceinline__ void run_steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
+                                            uint32_t w[16], std::integer_sequence<int, Is...>) {
+    steps84(a, b, c, d, e, w, std::integer_sequence<int, (Lo + Is)...>{});
+}
+
+// out <- SHA1_compress(M, in[0..4] || 0x80 || 0.. || bitlen(64+20)): the PBKDF2/HMAC inner-loop compression
+// (a 20-byte digest hashed after a 64-byte key pad block).  Rounds 0-1 come from the folded midstate invariants,
+// rounds 2-79 use the constant-folded message schedule above.
+__device__ __forceinline__ void sha1_84(const Sha1Mid& M, const uint32_t in[5], uint32_t out[5]) {
+    uint32_t w[16];
+    w[0] = in[0]; w[1] = in[1]; w[2] = in[2]; w[3] = in[3]; w[4] = in[4];
+#pragma unroll
+    for (int i = 5; i < 16; i++) w[i] = w84_const(i);
+    uint32_t a1 = M.c0 + w[0];
+    uint32_t a2 = rotl(a1, 5) + M.c1 + w[1];
+    uint32_t a = a2, b = a1, c = M.r0, d = M.r1, e = M.h2;
+    run_steps84<2>(a, b, c, d, e, w, std::make_integer_sequence<int, 78>{});
+    out[0] = M.h0 + a; out[1] = M.h1 + b; out[2] = M.h2 + c; out[3] = M.h3 + d; out[4] = M.h4 + e;
+}
+
+__device__ __forceinline__ void sha1_iv(uint32_t st[5]) {
+    st[0] = SHA1_IV0; st[1] = SHA1_IV1; st[2] = SHA1_IV2; st[3] = SHA1_IV3; st[4] = SHA1_IV4;
+}
+
+// HMAC-SHA1 key block (<= 64 bytes, big-endian words, zero padded) -> ipad / opad midstates.
+__device__ __forceinline__ void sha1_hmac_mid(const uint32_t kb[16], uint32_t ipad[5], uint32_t opad[5]) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = kb[i] ^ 0x36363636u;
+    sha1_iv(ipad);
+    sha1_compress(ipad, blk);
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = kb[i] ^ 0x5c5c5c5cu;
+    sha1_iv(opad);
+    sha1_compress(opad, blk);
+}
+
+// ------------------------------------------------------------------------------------------------
+// SHA-256 (keyver 3 KDF: HMAC-SHA256(PMK, "\1\0Pairwise key expansion" || m || n || "\x80\1"))
+// ------------------------------------------------------------------------------------------------
+__constant__ static const uint32_t SHA256_K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+__device__ __forceinline__ void sha256_iv(uint32_t st[8]) {
+    st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
+    st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
+}
+
+__device__ __forceinline__ void sha256_compress(uint32_t st[8], const uint32_t m[16]) {
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = m[i];
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+        uint32_t wt;
+        if (t < 16) wt = w[t];
+        else {
+            uint32_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
+            uint32_t s0 = rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3);
+            uint32_t s1 = rotr(y, 17) ^ rotr(y, 19) ^ (y >> 10);
+            wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+            w[t & 15] = wt;
+        }
+        uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        uint32_t ch = ((f ^ g) & e) ^ g;
+        uint32_t t1 = h + S1 + ch + SHA256_K[t] + wt;
+        uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        uint32_t mj = (a & b) | ((a | b) & c);
+        uint32_t t2 = S0 + mj;
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+__device__ __forceinline__ void sha256_hmac_mid(const uint32_t kb[16], uint32_t ipad[8], uint32_t opad[8]) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = kb[i] ^ 0x36363636u;
+    sha256_iv(ipad);
+    sha256_compress(ipad, blk);
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = kb[i] ^ 0x5c5c5c5cu;
+    sha256_iv(opad);
+    sha256_compress(opad, blk);
+}
+
+// ------------------------------------------------------------------------------------------------
+// MD5 (keyver 1 MIC: HMAC-MD5(KCK, EAPOL)); little-endian message words
+// ------------------------------------------------------------------------------------------------
+__constant__ static const uint32_t MD5_K[64] = {
+    0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u, 0xfd469501u,
+    0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u,
+    0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du, 0x02441453u, 0xd8a1e681u, 0xe7d3fbc8u,
+    0x21e1cde6u, 0xc33707d6u, 0xf4d50d87u, 0x455a14edu, 0xa9e3e905u, 0xfcefa3f8u, 0x676f02d9u, 0x8d2a4c8au,
+    0xfffa3942u, 0x8771f681u, 0x6d9d6122u, 0xfde5380cu, 0xa4beea44u, 0x4bdecfa9u, 0xf6bb4b60u, 0xbebfbc70u,
+    0x289b7ec6u, 0xeaa127fau, 0xd4ef3085u, 0x04881d05u, 0xd9d4d039u, 0xe6db99e5u, 0x1fa27cf8u, 0xc4ac5665u,
+    0xf4292244u, 0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
+    0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu, 0xeb86d391u};
+
+__device__ __forceinline__ void md5_iv(uint32_t st[4]) {
+    st[0] = 0x67452301u; st[1] = 0xefcdab89u; st[2] = 0x98badcfeu; st[3] = 0x10325476u;
+}
+
+__device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16]) {
+    constexpr int S[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t f;
+        int g;
+        if (i < 16) { f = ((c ^ d) & b) ^ d; g = i; }
+        else if (i < 32) { f = ((b ^ c) & d) ^ c; g = (5 * i + 1) & 15; }
+        else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) & 15; }
+        else { f = c ^ (b | ~d); g = (7 * i) & 15; }
+        uint32_t t = d;
+        d = c;
+        c = b;
+        b = b + rotl(a + f + MD5_K[i] + m[g], S[i >> 4][i & 3]);
+        a = t;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+}
+
+__device__ __forceinline__ void md5_hmac_mid(const uint32_t kb[16], uint32_t ipad[4], uint32_t opad[4]) {
+    uint32_t blk[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = kb[i] ^ 0x36363636u;
+    md5_iv(ipad);
+    md5_compress(ipad, blk);
+#pragma unroll
+    for (int i = 0; i < 16; i++) blk[i] = kb[i] ^ 0x5c5c5c5cu;
+    md5_iv(opad);
+    md5_compress(opad, blk);
+}
+
+// ------------------------------------------------------------------------------------------------
+// AES-128 encryption (keyver 3 MIC = AES-128-CMAC(KCK, EAPOL)), T-table in LDS.
+// Te0[x] = (2s, s, s, 3s) big-endian bytes of s = S(x); Te1..3 are byte rotations; the S-box is byte 1 of Te0.
+// The table is built at compile time from GF(2^8) arithmetic (no table copied from anywhere).
+// ------------------------------------------------------------------------------------------------
+struct AesTables {
+    uint32_t te0[256];
+};
+constexpr uint8_t gf_xt(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+constexpr AesTables make_aes_tables() {
+    // multiplicative inverses via exp/log tables over the generator 0x03, then the FIPS-197 affine map
+    uint8_t ex[256] = {}, lg[256] = {};
+    uint8_t x = 1;
+    for (int i = 0; i < 255; i++) {
+        ex[i] = x;
+        lg[x] = (uint8_t)i;
+        x = (uint8_t)(x ^ gf_xt(x));
+    }
+    AesTables t{};
+    for (int a = 0; a < 256; a++) {
+        uint8_t inv = a ? ex[(255 - lg[a]) % 255] : 0;
+        uint8_t s = inv;
+        for (int k = 1; k < 5; k++) s ^= (uint8_t)((inv << k) | (inv >> (8 - k)));
+        s ^= 0x63;
+        t.te0[a] = ((uint32_t)gf_xt(s) << 24) | ((uint32_t)s << 16) | ((uint32_t)s << 8) | (uint32_t)(gf_xt(s) ^ s);
+    }
+    return t;
+}
+__constant__ static const AesTables AES_TABLES = make_aes_tables();
+
+__device__ __forceinline__ uint32_t aes_sb(const uint32_t* te, uint32_t x) { return (te[x & 0xff] >> 8) & 0xff; }
+
+// rk[44] from a 16-byte key given as 4 big-endian words
+__device__ __forceinline__ void aes128_expand(const uint32_t* te, const uint32_t key[4], uint32_t rk[44]) {
+    rk[0] = key[0]; rk[1] = key[1]; rk[2] = key[2]; rk[3] = key[3];
+    uint32_t rcon = 0x01;
+#pragma unroll
+    for (int i = 4; i < 44; i++) {
+        uint32_t t = rk[i - 1];
+        if ((i & 3) == 0) {
+            t = (aes_sb(te, t >> 16) << 24) | (aes_sb(te, t >> 8) << 16) | (aes_sb(te, t) << 8) | aes_sb(te, t >> 24);
+            t ^= rcon << 24;
+            rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x11b : 0);
+        }
+        rk[i] = rk[i - 4] ^ t;
+    }
+}
+
+__device__ __forceinline__ void aes128_encrypt(const uint32_t* te, const uint32_t rk[44], uint32_t s[4]) {
+    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        uint32_t t0 = te[s0 >> 24] ^ rotr(te[(s1 >> 16) & 0xff], 8) ^ rotr(te[(s2 >> 8) & 0xff], 16) ^ rotr(te[s3 & 0xff], 24) ^ rk[4 * r];
+        uint32_t t1 = te[s1 >> 24] ^ rotr(te[(s2 >> 16) & 0xff], 8) ^ rotr(te[(s3 >> 8) & 0xff], 16) ^ rotr(te[s0 & 0xff], 24) ^ rk[4 * r + 1];
+        uint32_t t2 = te[s2 >> 24] ^ rotr(te[(s3 >> 16) & 0xff], 8) ^ rotr(te[(s0 >> 8) & 0xff], 16) ^ rotr(te[s1 & 0xff], 24) ^ rk[4 * r + 2];
+        uint32_t t3 = te[s3 >> 24] ^ rotr(te[(s0 >> 16) & 0xff], 8) ^ rotr(te[(s1 >> 8) & 0xff], 16) ^ rotr(te[s2 & 0xff], 24) ^ rk[4 * r + 3];
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    s[0] = (aes_sb(te, s0 >> 24) << 24 | aes_sb(te, s1 >> 16) << 16 | aes_sb(te, s2 >> 8) << 8 | aes_sb(te, s3)) ^ rk[40];
+    s[1] = (aes_sb(te, s1 >> 24) << 24 | aes_sb(te, s2 >> 16) << 16 | aes_sb(te, s3 >> 8) << 8 | aes_sb(te, s0)) ^ rk[41];
+    s[2] = (aes_sb(te, s2 >> 24) << 24 | aes_sb(te, s3 >> 16) << 16 | aes_sb(te, s0 >> 8) << 8 | aes_sb(te, s1)) ^ rk[42];
+    s[3] = (aes_sb(te, s3 >> 24) << 24 | aes_sb(te, s0 >> 16) << 16 | aes_sb(te, s1 >> 8) << 8 | aes_sb(te, s2)) ^ rk[43];
+}
+
+// CMAC subkey doubling on a 128-bit big-endian value held in 4 words
+__device__ __forceinline__ void cmac_dbl(const uint32_t in[4], uint32_t out[4]) {
+    uint32_t msb = in[0] >> 31;
+    out[0] = (in[0] << 1) | (in[1] >> 31);
+    out[1] = (in[1] << 1) | (in[2] >> 31);
+    out[2] = (in[2] << 1) | (in[3] >> 31);
+    out[3] = (in[3] << 1) ^ (msb ? 0x87u : 0u);
+}
+
+}  // namespace dwpa

@@ -1,0 +1,708 @@
+// engine.cpp -- libdwpa22000.so: device contexts, the server-side check path, the device-resident scan API and
+// the C-ABI exports declared in include/dwpa22000.h.
+//
+// Process model: one process may drive every visible MI355X (crack_files: one host thread per device, static
+// contiguous keyspace shards, no collective -- shards never exchange data; hits are gathered on the host).
+// bench.py instead runs one process per GPU (torch.distributed launch) and uses the scan API on its own device.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "dwpa22000.h"
+#include "engine.hpp"
+#include "kernels.hpp"
+#include "m22000_host.hpp"
+
+namespace dwpa {
+
+static thread_local hipError_t t_last_hip = hipSuccess;
+
+#define HIPCHK(x)                                                                                            \
+    do {                                                                                                     \
+        hipError_t e_ = (x);                                                                                 \
+        if (e_ != hipSuccess) {                                                                              \
+            t_last_hip = e_;                                                                                 \
+            return DWPA_E_HIP;                                                                               \
+        }                                                                                                    \
+    } while (0)
+#define RCHK(x)                    \
+    do {                           \
+        int r_ = (x);              \
+        if (r_ < 0) return r_;     \
+    } while (0)
+
+int DevBuf::ensure(size_t bytes) {
+    if (n >= bytes && p) return 0;
+    if (p) hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc(&p, bytes) != hipSuccess) return DWPA_E_NOMEM;
+    n = bytes;
+    return 0;
+}
+void DevBuf::release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    n = 0;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// global state
+// ---------------------------------------------------------------------------------------------------------
+struct Device {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    Batch batch;
+    DevBuf lines, atts, pool, segs, salt, koff, kbytes, idsup;
+};
+
+static std::mutex g_mu;
+static bool g_init = false;
+static int g_ndev = 0;
+static uint32_t g_mask = 0;
+static uint32_t g_batch = 0;
+static std::vector<std::unique_ptr<Device>> g_dev;
+static std::atomic<uint32_t> g_rr{0};
+
+static uint32_t default_batch() { return g_batch ? g_batch : (1u << 20); }
+
+static int init_locked(const dwpa_config* cfg) {
+    if (cfg) {
+        g_mask = cfg->device_mask;
+        g_batch = cfg->batch;
+    }
+    if (g_init) return 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DWPA_E_NODEV;
+    g_ndev = n;
+    g_dev.clear();
+    for (int d = 0; d < n; d++) {
+        auto dev = std::make_unique<Device>();
+        dev->id = d;
+        g_dev.push_back(std::move(dev));
+    }
+    g_init = true;
+    return 0;
+}
+
+static int ensure_init() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_locked(nullptr);
+}
+
+static std::vector<int> active_devices() {
+    std::vector<int> v;
+    for (int d = 0; d < g_ndev; d++)
+        if (!g_mask || (g_mask >> d & 1u)) v.push_back(d);
+    return v;
+}
+
+static int device_stream(Device& d) {
+    if (!d.stream) {
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    }
+    return 0;
+}
+
+int Batch::reserve(uint32_t want_cap, uint32_t want_hitcap) {
+    if (cap < want_cap) {
+        RCHK(mid.ensure((size_t)MID_WORDS * want_cap * 4));
+        RCHK(pmk.ensure((size_t)PMK_WORDS * want_cap * 4));
+        RCHK(ids.ensure((size_t)want_cap * 8));
+        cap = want_cap;
+    }
+    if (hitcap < want_hitcap) {
+        RCHK(hits.ensure((size_t)want_hitcap * sizeof(HitDev)));
+        hitcap = want_hitcap;
+    }
+    RCHK(counters.ensure(16));
+    return 0;
+}
+
+template <typename T>
+static int upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+    RCHK(b.ensure(std::max<size_t>(v.size() * sizeof(T), 16)));
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    return 0;
+}
+
+static void pmk_bytes(const uint32_t w[8], uint8_t out[32]) {
+    for (int k = 0; k < 8; k++) {
+        out[4 * k] = (uint8_t)(w[k] >> 24);
+        out[4 * k + 1] = (uint8_t)(w[k] >> 16);
+        out[4 * k + 2] = (uint8_t)(w[k] >> 8);
+        out[4 * k + 3] = (uint8_t)w[k];
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// explicit keys -> slots (server-side check path and dwpa_pbkdf2_pmk)
+// ---------------------------------------------------------------------------------------------------------
+struct Slot {
+    const std::string* key;   // bytes hashed (after hc_unhex)
+    uint32_t job;
+    uint32_t ordinal;         // index among the job's non-null keys
+    const std::string* essid;
+    bool pbkdf2;              // false: PMK supplied by the caller
+};
+
+// Materialise, derive and (optionally) verify a list of slots sorted by (essid, !pbkdf2).
+// On return hits[] holds every hit of this chunk.
+static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
+                     const std::vector<const uint8_t*>& job_pmk, const std::vector<uint32_t>& job_line,
+                     const TableBuilder* tb, bool verify, std::vector<HitDev>& hits_out, uint8_t* pmk_out) {
+    hipStream_t s = d.stream;
+    const uint32_t n = (uint32_t)(e - b);
+    RCHK(d.batch.reserve(n, n));
+    // keys -> offsets/bytes (packed back to back: k_prep_dict derives len = off[i+1] - off[i])
+    std::vector<uint64_t> off(n + 1);
+    std::string bytes;
+    for (uint32_t i = 0; i < n; i++) {
+        off[i] = bytes.size();
+        bytes += *slots[b + i].key;
+    }
+    off[n] = bytes.size();
+    bytes.append(8, '\0');
+    std::vector<uint8_t> bv(bytes.begin(), bytes.end());
+    RCHK(upload(d.koff, off, s));
+    RCHK(upload(d.kbytes, bv, s));
+    HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, n, 0, 0xffffffffu,
+                            (uint32_t*)d.batch.mid.p, nullptr, nullptr, d.batch.cap, false, s));
+    // ids = key ordinals (selects the PHP attempt list of each key)
+    std::vector<uint64_t> ids(n);
+    for (uint32_t i = 0; i < n; i++) ids[i] = slots[b + i].ordinal;
+    HIPCHK(hipMemcpyAsync(d.batch.ids.p, ids.data(), n * 8, hipMemcpyHostToDevice, s));
+
+    // PBKDF2 per ESSID run
+    std::vector<uint32_t> salts;
+    struct Run { uint32_t b, e, salt_off, nsalt; };
+    std::vector<Run> runs;
+    for (uint32_t i = 0; i < n;) {
+        uint32_t j = i;
+        while (j < n && *slots[b + j].essid == *slots[b + i].essid && slots[b + j].pbkdf2) j++;
+        if (j > i) {
+            std::vector<uint32_t> sb;
+            uint32_t nb = build_salt_blocks(*slots[b + i].essid, sb);
+            runs.push_back({i, j, (uint32_t)salts.size(), nb});
+            salts.insert(salts.end(), sb.begin(), sb.end());
+            i = j;
+        } else {
+            i++;  // caller-supplied PMK
+        }
+    }
+    RCHK(upload(d.salt, salts, s));
+    for (const Run& r : runs)
+        HIPCHK(launch_pbkdf2((const uint32_t*)d.batch.mid.p, d.batch.cap, r.b, r.e - r.b, nullptr,
+                             (const uint32_t*)d.salt.p + r.salt_off, r.nsalt, (uint32_t*)d.batch.pmk.p, s));
+    for (uint32_t i = 0; i < n; i++)
+        if (!slots[b + i].pbkdf2) {
+            const uint8_t* p = job_pmk[slots[b + i].job];
+            uint32_t w[8];
+            for (int k = 0; k < 8; k++)
+                w[k] = (uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 | (uint32_t)p[4 * k + 2] << 8 | p[4 * k + 3];
+            HIPCHK(launch_set_pmk((uint32_t*)d.batch.pmk.p, d.batch.cap, i, w, s));
+        }
+
+    if (pmk_out) {
+        std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
+        HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (uint32_t i = 0; i < n; i++) {
+            uint32_t pw[8];
+            for (int k = 0; k < 8; k++) pw[k] = w[(size_t)k * d.batch.cap + i];
+            pmk_bytes(pw, pmk_out + 32 * (size_t)(b + i));
+        }
+    }
+    if (!verify) {
+        HIPCHK(hipStreamSynchronize(s));  // host staging vectors die with this frame
+        return 0;
+    }
+
+    // segments: runs of consecutive slots of one job, <= 64 each
+    std::vector<SegDev> segs;
+    for (uint32_t i = 0; i < n;) {
+        uint32_t j = i;
+        const uint32_t job = slots[b + i].job;
+        while (j < n && slots[b + j].job == job && j - i < 64) j++;
+        if (!tb->never[job_line[job]]) segs.push_back({job_line[job], i, j - i, 0});
+        i = j;
+    }
+    if (segs.empty()) {
+        HIPCHK(hipStreamSynchronize(s));
+        return 0;
+    }
+    RCHK(upload(d.segs, segs, s));
+    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
+    uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
+    HIPCHK(launch_verify((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, nullptr,
+                         (const SegDev*)d.segs.p, (uint32_t)segs.size(), 0, 1, (const LineDev*)d.lines.p,
+                         (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt,
+                         d.batch.hitcap, tb->any_aes, s));
+    uint32_t nh = 0;
+    HIPCHK(hipMemcpyAsync(&nh, hitcnt, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nh > d.batch.hitcap) return DWPA_E_OVERFLOW;
+    size_t old = hits_out.size();
+    hits_out.resize(old + nh);
+    if (nh) HIPCHK(hipMemcpy(hits_out.data() + old, d.batch.hits.p, nh * sizeof(HitDev), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+static Device* pick_device() {
+    std::vector<int> act = active_devices();
+    if (act.empty()) return nullptr;
+    // prefer an idle device, else round-robin
+    for (size_t k = 0; k < act.size(); k++) {
+        Device* d = g_dev[act[(g_rr + k) % act.size()]].get();
+        if (d->mu.try_lock()) {
+            g_rr++;
+            return d;
+        }
+    }
+    Device* d = g_dev[act[g_rr++ % act.size()]].get();
+    d->mu.lock();
+    return d;
+}
+
+static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs) {
+    RCHK(ensure_init());
+    Device* dp = pick_device();
+    if (!dp) return DWPA_E_NODEV;
+    std::lock_guard<std::mutex> lk(dp->mu, std::adopt_lock);
+    Device& d = *dp;
+    HIPCHK(hipSetDevice(d.id));
+    RCHK(device_stream(d));
+
+    TableBuilder tb;
+    std::vector<ParsedLine> parsed(njobs);
+    std::vector<uint32_t> job_line(njobs, 0);
+    std::vector<const uint8_t*> job_pmk(njobs, nullptr);
+    std::vector<std::vector<std::string>> keys(njobs);
+    std::vector<std::vector<uint32_t>> key_index(njobs);
+    std::vector<Slot> slots;
+    for (size_t j = 0; j < njobs; j++) {
+        out[j].key_index = -1;
+        out[j].nc = 0;
+        out[j].endian = 0;
+        out[j].nc_valid = 0;
+        memset(out[j].pmk, 0, 32);
+        parsed[j] = parse_m22000(jobs[j].line, jobs[j].line_len);
+        rcs[j] = parsed[j].status;
+        if (parsed[j].status) continue;
+        for (size_t k = 0; k < jobs[j].nkeys; k++) {
+            const dwpa_bytes& kb = jobs[j].keys[k];
+            if (!kb.ptr) continue;  // is_null($key): skipped (common.php:172,240)
+            std::string key((const char*)kb.ptr, kb.len);
+            if (starts_hex(kb.ptr, kb.len)) key = hc_unhex(key);
+            keys[j].push_back(std::move(key));
+            key_index[j].push_back((uint32_t)k);
+        }
+        rcs[j] = DWPA_MISS;
+        if (keys[j].empty()) continue;
+        job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
+        job_pmk[j] = jobs[j].pmk;
+        if (tb.never[job_line[j]]) continue;
+    }
+    for (size_t j = 0; j < njobs; j++) {
+        if (rcs[j] != DWPA_MISS || keys[j].empty() || tb.never[job_line[j]]) continue;
+        for (uint32_t o = 0; o < keys[j].size(); o++)
+            slots.push_back({&keys[j][o], (uint32_t)j, o, &parsed[j].essid, !(o == 0 && job_pmk[j])});
+    }
+    if (slots.empty()) return 0;
+    std::stable_sort(slots.begin(), slots.end(), [](const Slot& a, const Slot& b) {
+        int c = a.essid->compare(*b.essid);
+        if (c) return c < 0;
+        return a.pbkdf2 > b.pbkdf2;
+    });
+    hipStream_t s = d.stream;
+    RCHK(upload(d.lines, tb.lines, s));
+    RCHK(upload(d.atts, tb.atts, s));
+    RCHK(upload(d.pool, tb.pool, s));
+
+    std::vector<HitDev> hits;
+    const size_t chunk = default_batch();
+    for (size_t b = 0; b < slots.size(); b += chunk)
+        RCHK(run_slots(d, slots, b, std::min(slots.size(), b + chunk), job_pmk, job_line, &tb, true, hits, nullptr));
+
+    // first key in input order wins, then the first attempt in PHP order (common.php:186,280-289)
+    std::map<uint32_t, size_t> line_job;
+    for (size_t j = 0; j < njobs; j++)
+        if (rcs[j] == DWPA_MISS && !keys[j].empty()) line_job[job_line[j]] = j;
+    std::vector<int64_t> best(njobs, -1);
+    std::vector<uint32_t> best_att(njobs, 0);
+    std::vector<const HitDev*> best_hit(njobs, nullptr);
+    for (const HitDev& h : hits) {
+        auto it = line_job.find(h.line);
+        if (it == line_job.end()) continue;
+        const size_t j = it->second;
+        if (best[j] < 0 || (int64_t)h.cand < best[j] || ((int64_t)h.cand == best[j] && h.attempt < best_att[j])) {
+            best[j] = (int64_t)h.cand;
+            best_att[j] = h.attempt;
+            best_hit[j] = &h;
+        }
+    }
+    for (size_t j = 0; j < njobs; j++) {
+        if (best[j] < 0) continue;
+        const LineDev& L = tb.lines[job_line[j]];
+        rcs[j] = DWPA_HIT;
+        out[j].key_index = (int32_t)key_index[j][(size_t)best[j]];
+        pmk_bytes(best_hit[j]->pmk, out[j].pmk);
+        if (L.kind == LINE_PMKID) {
+            out[j].nc_valid = 0;
+        } else {
+            const uint32_t list = (uint32_t)std::min<int64_t>(best[j], (int64_t)L.nlists - 1);
+            const AttDev& at = tb.atts[L.list_off + list * L.natt + best_att[j]];
+            out[j].nc_valid = 1;
+            out[j].nc = at.nc;
+            out[j].endian = (int8_t)at.endian;
+        }
+    }
+    return 0;
+}
+
+static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out) {
+    RCHK(ensure_init());
+    Device* dp = pick_device();
+    if (!dp) return DWPA_E_NODEV;
+    std::lock_guard<std::mutex> lk(dp->mu, std::adopt_lock);
+    Device& d = *dp;
+    HIPCHK(hipSetDevice(d.id));
+    RCHK(device_stream(d));
+    std::string es((const char*)essid, essid_len);
+    std::vector<std::string> ks(nkeys);
+    std::vector<Slot> slots(nkeys);
+    for (size_t i = 0; i < nkeys; i++) {
+        if (keys[i].ptr) ks[i].assign((const char*)keys[i].ptr, keys[i].len);
+        slots[i] = {&ks[i], 0, (uint32_t)i, &es, true};
+    }
+    std::vector<HitDev> hits;
+    const size_t chunk = default_batch();
+    std::vector<const uint8_t*> jp(1, nullptr);
+    std::vector<uint32_t> jl(1, 0);
+    for (size_t b = 0; b < nkeys; b += chunk)
+        RCHK(run_slots(d, slots, b, std::min(nkeys, b + chunk), jp, jl, nullptr, false, hits, out));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// scan API
+// ---------------------------------------------------------------------------------------------------------
+struct ScanGroup {
+    std::string essid;
+    uint32_t line_begin = 0, line_end = 0;  // contiguous in the line table
+    uint32_t salt_off = 0, nsalt = 0;
+};
+
+}  // namespace dwpa
+
+struct dwpa_scan {
+    int device = 0;
+    int nc_mode = 0;
+    dwpa::TableBuilder tb;
+    std::vector<int> status;              // per input line
+    std::vector<uint32_t> line_of;        // input line -> table line (valid when status == 0)
+    std::vector<uint32_t> input_of;       // table line -> input line
+    std::vector<dwpa::ScanGroup> groups;
+    std::vector<uint8_t> cracked;         // per table line (crack_files stops re-checking cracked lines)
+    dwpa::DevBuf lines, atts, pool, salt, segs;
+    dwpa::Batch batch;
+    uint32_t batch_cap = 0;
+};
+
+namespace dwpa {
+
+static hipStream_t as_stream(void* s) { return (hipStream_t)s; }
+
+int scan_create(int device, const char* const* lines, const size_t* lens, size_t nlines, int nc, int nc_mode,
+                uint32_t batch, dwpa_scan** out) {
+    RCHK(ensure_init());
+    if (device < 0 || device >= g_ndev || !out || batch == 0) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(device));
+    auto sc = std::make_unique<dwpa_scan>();
+    sc->device = device;
+    sc->nc_mode = nc_mode;
+    sc->status.resize(nlines);
+    sc->line_of.assign(nlines, 0);
+    std::vector<ParsedLine> parsed(nlines);
+    std::map<std::string, std::vector<size_t>> by_essid;
+    for (size_t i = 0; i < nlines; i++) {
+        parsed[i] = parse_m22000(lines[i], lens[i]);
+        sc->status[i] = parsed[i].status;
+        if (!parsed[i].status) by_essid[parsed[i].essid].push_back(i);
+    }
+    std::vector<uint32_t> salts;
+    for (auto& kv : by_essid) {
+        ScanGroup g;
+        g.essid = kv.first;
+        g.line_begin = (uint32_t)sc->tb.lines.size();
+        for (size_t i : kv.second) {
+            sc->line_of[i] = sc->tb.add_line(parsed[i], nc, nc_mode, nc);
+            sc->input_of.push_back((uint32_t)i);
+        }
+        g.line_end = (uint32_t)sc->tb.lines.size();
+        std::vector<uint32_t> sb;
+        g.nsalt = build_salt_blocks(g.essid, sb);
+        g.salt_off = (uint32_t)salts.size();
+        salts.insert(salts.end(), sb.begin(), sb.end());
+        sc->groups.push_back(g);
+    }
+    sc->cracked.assign(sc->tb.lines.size(), 0);
+    for (size_t l = 0; l < sc->tb.never.size(); l++)
+        if (sc->tb.never[l]) sc->cracked[l] = 1;  // can never match: never verified
+    RCHK(upload(sc->lines, sc->tb.lines, nullptr));
+    RCHK(upload(sc->atts, sc->tb.atts, nullptr));
+    RCHK(upload(sc->pool, sc->tb.pool, nullptr));
+    RCHK(upload(sc->salt, salts, nullptr));
+    batch = (batch + 63) & ~63u;
+    RCHK(sc->batch.reserve(batch, std::max<uint32_t>(batch, 1u << 16)));
+    sc->batch_cap = batch;
+    HIPCHK(hipMemset(sc->batch.counters.p, 0, 16));
+    HIPCHK(hipDeviceSynchronize());
+    *out = sc.release();
+    return 0;
+}
+
+void scan_destroy(dwpa_scan* sc) {
+    if (!sc) return;
+    hipSetDevice(sc->device);
+    hipDeviceSynchronize();
+    sc->lines.release(); sc->atts.release(); sc->pool.release(); sc->salt.release(); sc->segs.release();
+    sc->batch.mid.release(); sc->batch.pmk.release(); sc->batch.ids.release(); sc->batch.hits.release();
+    sc->batch.counters.release();
+    delete sc;
+}
+
+int scan_load_dict(dwpa_scan* sc, const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t count,
+                   uint32_t minlen, uint32_t maxlen, void* stream) {
+    if (!sc || count > sc->batch_cap) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(sc->device));
+    hipStream_t s = as_stream(stream);
+    HIPCHK(hipMemsetAsync(sc->batch.counters.p, 0, 4, s));
+    HIPCHK(launch_prep_dict(off, bytes, first, count, minlen, maxlen, (uint32_t*)sc->batch.mid.p,
+                            (uint64_t*)sc->batch.ids.p, (uint32_t*)sc->batch.counters.p, sc->batch_cap, true, s));
+    return 0;
+}
+
+int scan_load_numeric(dwpa_scan* sc, uint64_t first, uint32_t count, uint32_t digits, void* stream) {
+    if (!sc || count > sc->batch_cap || digits == 0 || digits > 20) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(sc->device));
+    hipStream_t s = as_stream(stream);
+    HIPCHK(hipMemcpyAsync(sc->batch.counters.p, &count, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_prep_numeric(first, count, digits, (uint32_t*)sc->batch.mid.p, (uint64_t*)sc->batch.ids.p,
+                               sc->batch_cap, s));
+    HIPCHK(hipStreamSynchronize(s));  // `count` lives on this host stack frame
+    return 0;
+}
+
+int scan_pbkdf2(dwpa_scan* sc, int group, void* stream) {
+    if (!sc || group < 0 || group >= (int)sc->groups.size()) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(sc->device));
+    const ScanGroup& g = sc->groups[group];
+    bool any = false;
+    for (uint32_t l = g.line_begin; l < g.line_end; l++) any |= !sc->cracked[l];
+    if (!any) return 0;
+    HIPCHK(launch_pbkdf2((const uint32_t*)sc->batch.mid.p, sc->batch_cap, 0, sc->batch_cap,
+                         (const uint32_t*)sc->batch.counters.p, (const uint32_t*)sc->salt.p + g.salt_off, g.nsalt,
+                         (uint32_t*)sc->batch.pmk.p, as_stream(stream)));
+    return 0;
+}
+
+int scan_verify(dwpa_scan* sc, int group, void* stream) {
+    if (!sc || group < 0 || group >= (int)sc->groups.size()) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(sc->device));
+    const ScanGroup& g = sc->groups[group];
+    const uint32_t nsegs = sc->batch_cap / 64;
+    // contiguous runs of uncracked lines -> implicit-segment launches
+    for (uint32_t l = g.line_begin; l < g.line_end;) {
+        if (sc->cracked[l]) { l++; continue; }
+        uint32_t e = l;
+        while (e < g.line_end && !sc->cracked[e]) e++;
+        HIPCHK(launch_verify((const uint32_t*)sc->batch.pmk.p, sc->batch_cap, (const uint64_t*)sc->batch.ids.p,
+                             (const uint32_t*)sc->batch.counters.p, nullptr, nsegs, l, e - l,
+                             (const LineDev*)sc->lines.p, (const uint32_t*)sc->pool.p, (const AttDev*)sc->atts.p,
+                             (HitDev*)sc->batch.hits.p, (uint32_t*)sc->batch.counters.p + 1, sc->batch.hitcap,
+                             sc->tb.any_aes, as_stream(stream)));
+        l = e;
+    }
+    return 0;
+}
+
+int scan_hits_raw(dwpa_scan* sc, std::vector<HitDev>& out, void* stream) {
+    HIPCHK(hipSetDevice(sc->device));
+    hipStream_t s = as_stream(stream);
+    uint32_t nh = 0;
+    HIPCHK(hipMemcpyAsync(&nh, (uint32_t*)sc->batch.counters.p + 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (nh > sc->batch.hitcap) return DWPA_E_OVERFLOW;
+    out.resize(nh);
+    if (nh) HIPCHK(hipMemcpyAsync(out.data(), sc->batch.hits.p, nh * sizeof(HitDev), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemsetAsync((uint32_t*)sc->batch.counters.p + 1, 0, 4, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+void hit_to_public(const dwpa_scan* sc, const HitDev& h, dwpa_hit& o) {
+    const LineDev& L = sc->tb.lines[h.line];
+    memset(&o, 0, sizeof(o));
+    o.cand = h.cand;
+    o.line = sc->input_of[h.line];
+    pmk_bytes(h.pmk, o.pmk);
+    if (L.kind == LINE_EAPOL) {
+        const uint32_t list = (uint32_t)std::min<uint64_t>(h.cand, (uint64_t)L.nlists - 1);
+        const AttDev& at = sc->tb.atts[L.list_off + list * L.natt + h.attempt];
+        o.nc_valid = 1;
+        o.nc = at.nc;
+        o.endian = (int8_t)at.endian;
+    }
+}
+
+void scan_mark_cracked(dwpa_scan* sc, uint32_t input_line) {
+    if (input_line < sc->status.size() && sc->status[input_line] == 0) sc->cracked[sc->line_of[input_line]] = 1;
+}
+uint32_t scan_batch_cap(const dwpa_scan* sc) { return sc->batch_cap; }
+Batch& scan_batch_ref(dwpa_scan* sc) { return sc->batch; }
+
+// ---------------------------------------------------------------------------------------------------------
+// helpers for crack.cpp
+// ---------------------------------------------------------------------------------------------------------
+int engine_init() { return ensure_init(); }
+std::vector<int> engine_devices() { return active_devices(); }
+uint32_t engine_batch() { return default_batch(); }
+
+}  // namespace dwpa
+
+// =========================================================================================================
+// C ABI
+// =========================================================================================================
+using namespace dwpa;
+
+extern "C" {
+
+int dwpa_abi_version(void) { return DWPA_ABI_VERSION; }
+
+int dwpa_init(const dwpa_config* cfg) {
+    if (cfg && cfg->struct_size && cfg->struct_size < sizeof(uint32_t) * 3) return DWPA_E_ARG;
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_locked(cfg);
+}
+
+int dwpa_device_count(void) {
+    int r = ensure_init();
+    return r < 0 ? r : g_ndev;
+}
+
+const char* dwpa_strerror(int code) {
+    switch (code) {
+    case DWPA_MISS: return "no match";
+    case DWPA_HIT: return "match";
+    case DWPA_E_FORMAT: return "malformed hashline (need 9 '*'-separated fields starting with WPA)";
+    case DWPA_E_HEX: return "hashline field is not valid hex";
+    case DWPA_E_TYPE: return "hashline type is neither 01 (PMKID) nor 02 (EAPOL)";
+    case DWPA_E_KEYVER: return "unsupported EAPOL key version";
+    case DWPA_E_NODEV: return "no usable gfx950 device";
+    case DWPA_E_HIP: return hipGetErrorString(t_last_hip);
+    case DWPA_E_ARG: return "invalid argument";
+    case DWPA_E_NOMEM: return "out of memory";
+    case DWPA_E_IO: return "I/O error";
+    case DWPA_E_OVERFLOW: return "hit buffer overflow";
+    case DWPA_E_RULE: return "unsupported or malformed rule";
+    default: return "unknown error";
+    }
+}
+
+void dwpa_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& d : g_dev) {
+        std::lock_guard<std::mutex> dl(d->mu);
+        hipSetDevice(d->id);
+        hipDeviceSynchronize();
+        for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->salt, &d->koff, &d->kbytes, &d->idsup,
+                          &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
+            b->release();
+        d->batch.cap = d->batch.hitcap = 0;
+        if (d->stream) hipStreamDestroy(d->stream);
+        d->stream = nullptr;
+    }
+    g_dev.clear();
+    g_init = false;
+}
+
+int dwpa_check_m22000(const char* line, size_t line_len, const dwpa_bytes* keys, size_t nkeys, const uint8_t* pmk,
+                      int nc, dwpa_result* out) {
+    if (!line || (!keys && nkeys) || !out) return DWPA_E_ARG;
+    dwpa_job j{line, line_len, keys, nkeys, pmk, nc};
+    int rc = 0;
+    int r = check_batch_impl(&j, 1, out, &rc);
+    return r < 0 ? r : rc;
+}
+
+int dwpa_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs) {
+    if ((!jobs || !out || !rcs) && njobs) return DWPA_E_ARG;
+    if (njobs == 0) return 0;
+    return check_batch_impl(jobs, njobs, out, rcs);
+}
+
+int dwpa_pbkdf2_pmk(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* pmks_out) {
+    if ((!keys && nkeys) || (!essid && essid_len) || (!pmks_out && nkeys)) return DWPA_E_ARG;
+    if (nkeys == 0) return 0;
+    return pbkdf2_impl(keys, nkeys, essid, essid_len, pmks_out);
+}
+
+int dwpa_hc_unhex(const uint8_t* in, size_t in_len, uint8_t* out, size_t* out_len) {
+    if ((!in && in_len) || !out || !out_len) return DWPA_E_ARG;
+    std::string r = hc_unhex(std::string((const char*)in, in_len));
+    memcpy(out, r.data(), r.size());
+    *out_len = r.size();
+    return 0;
+}
+
+int dwpa_scan_create(int device, const char* const* lines, const size_t* line_lens, size_t nlines, int nc,
+                     int nc_mode, uint32_t batch, dwpa_scan** out) {
+    if ((!lines || !line_lens) && nlines) return DWPA_E_ARG;
+    return scan_create(device, lines, line_lens, nlines, nc, nc_mode, batch, out);
+}
+int dwpa_scan_num_groups(const dwpa_scan* scan) { return scan ? (int)scan->groups.size() : DWPA_E_ARG; }
+int dwpa_scan_line_status(const dwpa_scan* scan, size_t line) {
+    if (!scan || line >= scan->status.size()) return DWPA_E_ARG;
+    return scan->status[line];
+}
+int dwpa_scan_load_dict(dwpa_scan* scan, const uint64_t* d_offsets, const uint8_t* d_bytes, uint64_t first,
+                        uint32_t count, uint32_t minlen, uint32_t maxlen, void* hip_stream) {
+    return scan_load_dict(scan, d_offsets, d_bytes, first, count, minlen, maxlen, hip_stream);
+}
+int dwpa_scan_load_numeric(dwpa_scan* scan, uint64_t first, uint32_t count, uint32_t digits, void* hip_stream) {
+    return scan_load_numeric(scan, first, count, digits, hip_stream);
+}
+int dwpa_scan_pbkdf2(dwpa_scan* scan, int group, void* hip_stream) { return scan_pbkdf2(scan, group, hip_stream); }
+int dwpa_scan_verify(dwpa_scan* scan, int group, void* hip_stream) { return scan_verify(scan, group, hip_stream); }
+int dwpa_scan_hits(dwpa_scan* scan, dwpa_hit* out, size_t cap, size_t* nhits, void* hip_stream) {
+    if (!scan || !nhits || (!out && cap)) return DWPA_E_ARG;
+    std::vector<HitDev> raw;
+    RCHK(scan_hits_raw(scan, raw, hip_stream));
+    *nhits = raw.size();
+    for (size_t i = 0; i < raw.size() && i < cap; i++) hit_to_public(scan, raw[i], out[i]);
+    return raw.size() > cap ? DWPA_E_OVERFLOW : 0;
+}
+int dwpa_scan_loaded(dwpa_scan* scan, uint32_t* count, void* hip_stream) {
+    if (!scan || !count) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(scan->device));
+    hipStream_t s = as_stream(hip_stream);
+    HIPCHK(hipMemcpyAsync(count, scan->batch.counters.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (*count > scan->batch_cap) *count = scan->batch_cap;
+    return 0;
+}
+void dwpa_scan_destroy(dwpa_scan* scan) { scan_destroy(scan); }
+
+}  // extern "C"

@@ -1,0 +1,48 @@
+// engine.hpp -- internal interfaces of libdwpa22000.so shared by engine.cpp and crack.cpp.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "dwpa22000.h"
+#include "tables.hpp"
+
+namespace dwpa {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes);
+    void release();
+};
+
+// Per-batch device working set (cap candidate slots).
+struct Batch {
+    uint32_t cap = 0, hitcap = 0;
+    DevBuf mid;       // [10][cap] u32 HMAC key midstates
+    DevBuf pmk;       // [8][cap]  u32 PMKs
+    DevBuf ids;       // [cap]     u64 candidate ids
+    DevBuf hits;      // [hitcap]  HitDev
+    DevBuf counters;  // [0] loaded slots, [1] hit count
+    int reserve(uint32_t cap, uint32_t hitcap);
+};
+
+int engine_init();
+std::vector<int> engine_devices();
+uint32_t engine_batch();
+
+int scan_create(int device, const char* const* lines, const size_t* lens, size_t nlines, int nc, int nc_mode,
+                uint32_t batch, dwpa_scan** out);
+void scan_destroy(dwpa_scan* sc);
+int scan_load_dict(dwpa_scan* sc, const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t count,
+                   uint32_t minlen, uint32_t maxlen, void* stream);
+int scan_load_numeric(dwpa_scan* sc, uint64_t first, uint32_t count, uint32_t digits, void* stream);
+int scan_pbkdf2(dwpa_scan* sc, int group, void* stream);
+int scan_verify(dwpa_scan* sc, int group, void* stream);
+int scan_hits_raw(dwpa_scan* sc, std::vector<HitDev>& out, void* stream);
+void hit_to_public(const dwpa_scan* sc, const HitDev& h, dwpa_hit& o);
+void scan_mark_cracked(dwpa_scan* sc, uint32_t input_line);
+uint32_t scan_batch_cap(const dwpa_scan* sc);
+Batch& scan_batch_ref(dwpa_scan* sc);
+
+}  // namespace dwpa

@@ -1,0 +1,386 @@
+// kernels.hip -- the m22000 hot path on gfx950: candidate materialisation -> PBKDF2-HMAC-SHA1 x4096 -> verify.
+//
+//   k_prep_dict     dictionary words in HBM (offsets+bytes)  -> HMAC-SHA1 key midstates (ipad/opad), compacted
+//   k_prep_numeric  in-kernel decimal keyspace (C4)          -> midstates
+//   k_pbkdf2        midstates x ESSID salt                    -> PMK (32 B)      [~99 % of all work]
+//   k_verify        PMK x hashline(s) of that ESSID           -> hit records     [PMKID / EAPOL keyver 1,2,3 + NC]
+//
+// The PMK is defined by web/common.php:178-180,246-248 (openssl_pbkdf2($key,$essid,32,4096,'sha1')), the checks by
+// common.php:167-189 (PMKID) and :192-300 (EAPOL with nonce-error-correction).
+//
+// Layouts in HBM (cap = candidate slots per batch):
+//   mid[10][cap]  u32  SoA   ipad h0..h4, opad h0..h4     (40 B / candidate, written once, reused for every ESSID)
+//   ids[cap]      u64        candidate id of each slot (dictionary order survives compaction)
+//   pmk[8][cap]   u32  SoA   PMK big-endian words         (32 B / candidate / ESSID)
+// All loads/stores of these arrays are lane-contiguous (coalesced dwords).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crypto_dev.hpp"
+#include "prep_dev.hpp"
+#include "tables.hpp"
+#include "kernels.hpp"
+
+namespace dwpa {
+
+// ------------------------------------------------------------------------------------------------
+// stage 1: candidates -> HMAC key midstates
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_prep_dict(const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                                                   uint64_t first, uint32_t count, uint32_t minlen, uint32_t maxlen,
+                                                   uint32_t* __restrict__ mid, uint64_t* __restrict__ ids,
+                                                   uint32_t* __restrict__ counter, uint32_t cap, uint32_t compact) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool keep = false;
+    uint64_t b0 = 0;
+    uint32_t len = 0;
+    if (i < count) {
+        b0 = off[first + i];
+        const uint64_t b1 = off[first + i + 1];
+        len = (uint32_t)(b1 - b0);
+        keep = !compact || (len >= minlen && len <= maxlen);
+    }
+    uint32_t slot = i;
+    if (compact) slot = compact_slot(keep, counter);
+    if (!keep || slot >= cap) return;
+    uint32_t kb[16];
+    key_block_from_bytes(bytes + b0, len, kb);
+    store_mid(mid, cap, slot, kb);
+    if (ids) ids[slot] = first + i;
+}
+
+// Decimal keyspace: candidate v -> its `digits`-wide zero-padded decimal string (C4: 00000000..99999999).
+__global__ __launch_bounds__(256) void k_prep_numeric(uint64_t first, uint32_t count, uint32_t digits,
+                                                      uint32_t* __restrict__ mid, uint64_t* __restrict__ ids, uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count || i >= cap) return;
+    uint64_t v = first + i;
+    uint32_t kb[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) kb[j] = 0;
+    // digits <= 20; fill from the least significant character
+    for (int k = (int)digits - 1; k >= 0; k--) {
+        const uint32_t d = (uint32_t)(v % 10u);
+        v /= 10u;
+        const uint32_t c = 0x30u + d;
+        const int wi = k >> 2, sh = 24 - 8 * (k & 3);
+#pragma unroll
+        for (int j = 0; j < 5; j++)
+            if (j == wi) kb[j] |= c << sh;
+    }
+    store_mid(mid, cap, i, kb);
+    ids[i] = first + i;
+}
+
+// ------------------------------------------------------------------------------------------------
+// stage 2: PBKDF2-HMAC-SHA1, 4096 iterations, one (candidate, output block) per lane.
+// blockIdx.y selects the output block T_1 (PMK bytes 0..19) or T_2 (bytes 20..31).  The salt blocks
+// (ESSID || INT(i) || SHA1 padding, pre-padded on the host) are wave-uniform -> scalar loads.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pbkdf2(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base,
+                                                uint32_t count, const uint32_t* __restrict__ counter,
+                                                const uint32_t* __restrict__ salt, uint32_t nsalt,
+                                                uint32_t* __restrict__ pmk) {
+    const uint32_t blk = blockIdx.y;
+    const uint32_t s = base + blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = counter ? min(*counter, cap) : min(base + count, cap);
+    if (s >= n) return;
+    uint32_t hi[5], ho[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        hi[k] = mid[(size_t)k * cap + s];
+        ho[k] = mid[(size_t)(5 + k) * cap + s];
+    }
+    // U_1 = HMAC(P, S || INT(blk+1))
+    uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
+    const uint32_t* sb = salt + (size_t)blk * nsalt * 16;
+    for (uint32_t b = 0; b < nsalt; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) m[j] = sb[b * 16 + j];
+        sha1_compress(st, m);
+    }
+    const Sha1Mid MI = sha1_mid(hi);
+    const Sha1Mid MO = sha1_mid(ho);
+    uint32_t u[5], x[5], t[5];
+    sha1_84(MO, st, u);
+#pragma unroll
+    for (int k = 0; k < 5; k++) t[k] = u[k];
+#pragma unroll 1
+    for (int it = 1; it < 4096; it++) {
+        sha1_84(MI, u, x);
+        sha1_84(MO, x, u);
+#pragma unroll
+        for (int k = 0; k < 5; k++) t[k] ^= u[k];
+    }
+    if (blk == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) pmk[(size_t)k * cap + s] = t[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) pmk[(size_t)(5 + k) * cap + s] = t[k];
+    }
+}
+
+// Caller-supplied PMK for one slot (check_key_m22000's $pmk argument, common.php:157,178).
+__global__ void k_set_pmk(uint32_t* __restrict__ pmk, uint32_t cap, uint32_t slot, uint4 lo, uint4 hi) {
+    if (threadIdx.x == 0) {
+        pmk[0 * (size_t)cap + slot] = lo.x; pmk[1 * (size_t)cap + slot] = lo.y;
+        pmk[2 * (size_t)cap + slot] = lo.z; pmk[3 * (size_t)cap + slot] = lo.w;
+        pmk[4 * (size_t)cap + slot] = hi.x; pmk[5 * (size_t)cap + slot] = hi.y;
+        pmk[6 * (size_t)cap + slot] = hi.z; pmk[7 * (size_t)cap + slot] = hi.w;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// stage 3: verification.  One wave = one segment = up to 64 slots x one line (line data wave-uniform).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void sha1_blocks(uint32_t st[5], const uint32_t* __restrict__ w, uint32_t nblk) {
+    for (uint32_t b = 0; b < nblk; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) m[j] = w[b * 16 + j];
+        sha1_compress(st, m);
+    }
+}
+__device__ __forceinline__ void sha256_blocks(uint32_t st[8], const uint32_t* __restrict__ w, uint32_t nblk) {
+    for (uint32_t b = 0; b < nblk; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) m[j] = w[b * 16 + j];
+        sha256_compress(st, m);
+    }
+}
+__device__ __forceinline__ void md5_blocks(uint32_t st[4], const uint32_t* __restrict__ w, uint32_t nblk) {
+    for (uint32_t b = 0; b < nblk; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) m[j] = w[b * 16 + j];
+        md5_compress(st, m);
+    }
+}
+
+// HMAC outer hash over a 20-byte inner digest (generic state, no invariant folding).
+__device__ __forceinline__ void sha1_outer20(const uint32_t opad[5], const uint32_t in[5], uint32_t out[5]) {
+    uint32_t m[16] = {in[0], in[1], in[2], in[3], in[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 672u};
+#pragma unroll
+    for (int k = 0; k < 5; k++) out[k] = opad[k];
+    sha1_compress(out, m);
+}
+
+__global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk, uint32_t cap,
+                                                const uint64_t* __restrict__ ids, const uint32_t* __restrict__ counter,
+                                                const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t line_base,
+                                                const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
+                                                const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
+                                                uint32_t* __restrict__ hitcnt, uint32_t hitcap, uint32_t use_aes) {
+    __shared__ uint32_t te[256];
+    if (use_aes) {
+        for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) te[k] = AES_TABLES.te0[k];
+        __syncthreads();
+    }
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t segi = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (segi >= nsegs) return;
+    SegDev sg;
+    if (segs) sg = segs[segi];
+    else {  // implicit: every 64-slot chunk of the batch against line line_base + blockIdx.y
+        sg.line = line_base + blockIdx.y;
+        sg.slot = segi * 64;
+        sg.count = 64;
+    }
+    const uint32_t n = counter ? min(*counter, cap) : cap;
+    const uint32_t slot = sg.slot + lane;
+    const bool active = lane < sg.count && slot < n;
+    if (!__any(active)) return;
+    const LineDev L = lines[sg.line];
+
+    uint32_t p[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) p[k] = active ? pmk[(size_t)k * cap + slot] : 0u;
+    const uint64_t cand = active ? (ids ? ids[slot] : (uint64_t)slot) : 0ull;
+
+    uint32_t kb[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
+
+    bool found = false;
+    uint32_t found_att = 0;
+
+    if (L.kind == LINE_PMKID) {
+        uint32_t ip[5], op[5], st[5], out[5];
+        sha1_hmac_mid(kb, ip, op);
+#pragma unroll
+        for (int k = 0; k < 5; k++) st[k] = ip[k];
+        sha1_blocks(st, pool + L.msg_off, L.msg_nblk);
+        sha1_outer20(op, st, out);
+        found = active && out[0] == L.target[0] && out[1] == L.target[1] && out[2] == L.target[2] &&
+                out[3] == L.target[3];
+    } else {
+        // PMK-keyed PRF midstates + the attempt-invariant PRF prefix
+        uint32_t ip1[5], op1[5], pre1[5];
+        uint32_t ip2[8], op2[8], pre2[8];
+        const bool kv3 = L.keyver == 3;
+        if (!kv3) {
+            sha1_hmac_mid(kb, ip1, op1);
+#pragma unroll
+            for (int k = 0; k < 5; k++) pre1[k] = ip1[k];
+            sha1_blocks(pre1, pool + L.pre_off, L.pre_nblk);
+        } else {
+            sha256_hmac_mid(kb, ip2, op2);
+#pragma unroll
+            for (int k = 0; k < 8; k++) pre2[k] = ip2[k];
+            sha256_blocks(pre2, pool + L.pre_off, L.pre_nblk);
+        }
+        // PHP mutates $n across keys (common.php:255-259): list k serves the k-th non-null key, the last list the rest
+        const uint32_t sel = active ? (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1)) : 0xffffffffu;
+        uint32_t lo = sel, hi = active ? sel : 0u;
+        for (int o = 32; o >= 1; o >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+        }
+        lo = __builtin_amdgcn_readfirstlane(lo);
+        hi = __builtin_amdgcn_readfirstlane(hi);
+        for (uint32_t list = lo; list <= hi; list++) {
+            const bool mine = active && sel == list;
+            if (!__any(mine)) continue;
+            const AttDev* al = atts + L.list_off + list * L.natt;
+            for (uint32_t a = 0; a < L.natt; a++) {
+                const AttDev at = al[a];
+                uint32_t mic[4];
+                if (!kv3) {
+                    uint32_t st[5], ptk[5];
+#pragma unroll
+                    for (int k = 0; k < 5; k++) st[k] = pre1[k];
+                    sha1_blocks(st, pool + at.blk_off, at.nblk);
+                    sha1_outer20(op1, st, ptk);  // PTK[0..19]; KCK = PTK[0..15]
+                    if (L.keyver == 2) {
+                        uint32_t k2[16], mi[5], mo[5];
+#pragma unroll
+                        for (int k = 0; k < 16; k++) k2[k] = k < 4 ? ptk[k] : 0u;
+                        sha1_hmac_mid(k2, mi, mo);
+                        sha1_blocks(mi, pool + L.mic_off, L.mic_nblk);
+                        uint32_t o[5];
+                        sha1_outer20(mo, mi, o);
+                        mic[0] = o[0]; mic[1] = o[1]; mic[2] = o[2]; mic[3] = o[3];
+                    } else {
+                        uint32_t k1[16], mi[4], mo[4];
+#pragma unroll
+                        for (int k = 0; k < 16; k++) k1[k] = k < 4 ? bswap32(ptk[k]) : 0u;
+                        md5_hmac_mid(k1, mi, mo);
+                        md5_blocks(mi, pool + L.mic_off, L.mic_nblk);
+                        uint32_t m[16] = {mi[0], mi[1], mi[2], mi[3], 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 640u, 0};
+                        md5_compress(mo, m);
+                        mic[0] = mo[0]; mic[1] = mo[1]; mic[2] = mo[2]; mic[3] = mo[3];
+                    }
+                } else {
+                    uint32_t st[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) st[k] = pre2[k];
+                    sha256_blocks(st, pool + at.blk_off, at.nblk);
+                    uint32_t m[16] = {st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7],
+                                      0x80000000u, 0, 0, 0, 0, 0, 0, 768u};
+                    uint32_t ptk[8];
+#pragma unroll
+                    for (int k = 0; k < 8; k++) ptk[k] = op2[k];
+                    sha256_compress(ptk, m);
+                    // AES-128-CMAC(KCK = PTK[0..15], EAPOL)  (common.php:72-112)
+                    uint32_t rk[44];
+                    aes128_expand(te, ptk, rk);
+                    uint32_t Lb[4] = {0, 0, 0, 0}, K1[4], K2[4];
+                    aes128_encrypt(te, rk, Lb);
+                    cmac_dbl(Lb, K1);
+                    cmac_dbl(K1, K2);
+                    uint32_t c[4] = {0, 0, 0, 0};
+                    const uint32_t* eb = pool + L.mic_off;
+                    for (uint32_t b = 0; b < L.mic_nblk; b++) {
+                        const bool last = b + 1 == L.mic_nblk;
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            uint32_t v = eb[4 * b + k];
+                            if (last) v ^= L.cmac_complete ? K1[k] : K2[k];
+                            c[k] ^= v;
+                        }
+                        aes128_encrypt(te, rk, c);
+                    }
+                    mic[0] = c[0]; mic[1] = c[1]; mic[2] = c[2]; mic[3] = c[3];
+                }
+                const bool match = mine && !found && mic[0] == L.target[0] && mic[1] == L.target[1] &&
+                                   mic[2] == L.target[2] && mic[3] == L.target[3];
+                if (match) {
+                    found = true;
+                    found_att = a;
+                }
+            }
+        }
+    }
+
+    // hit reporting: one ballot, one atomic per wave, append to the small hit buffer
+    const uint64_t m = __ballot(found);
+    if (m) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(hitcnt, (uint32_t)__popcll(m));
+        base = __shfl(base, (int)leader);
+        if (found) {
+            const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            if (idx < hitcap) {
+                HitDev h;
+                h.cand = cand;
+                h.line = sg.line;
+                h.attempt = found_att;
+#pragma unroll
+                for (int k = 0; k < 8; k++) h.pmk[k] = p[k];
+                hits[idx] = h;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------------
+static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+hipError_t launch_prep_dict(const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t count, uint32_t minlen,
+                            uint32_t maxlen, uint32_t* mid, uint64_t* ids, uint32_t* counter, uint32_t cap,
+                            bool compact, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prep_dict, dim3(cdiv(count, 256)), dim3(256), 0, s, off, bytes, first, count, minlen, maxlen,
+                       mid, ids, counter, cap, compact ? 1u : 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_numeric(uint64_t first, uint32_t count, uint32_t digits, uint32_t* mid, uint64_t* ids,
+                               uint32_t cap, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prep_numeric, dim3(cdiv(count, 256)), dim3(256), 0, s, first, count, digits, mid, ids, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
+                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pbkdf2, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, base, count, counter, salt, nsalt,
+                       pmk);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s) {
+    uint4 lo = make_uint4(w[0], w[1], w[2], w[3]), hi = make_uint4(w[4], w[5], w[6], w[7]);
+    hipLaunchKernelGGL(k_set_pmk, dim3(1), dim3(64), 0, s, pmk, cap, slot, lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
+                         const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,
+                         const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt, uint32_t hitcap,
+                         bool use_aes, hipStream_t s) {
+    if (nsegs == 0 || nlines == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_verify, dim3(cdiv(nsegs, 4), segs ? 1 : nlines), dim3(256), 0, s, pmk, cap, ids, counter, segs,
+                       nsegs, line_base, lines, pool, atts, hits, hitcnt, hitcap, use_aes ? 1u : 0u);
+    return hipGetLastError();
+}
+
+}  // namespace dwpa

@@ -1,0 +1,23 @@
+// kernels.hpp -- host-side launchers for kernels.hip (internal to libdwpa22000.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tables.hpp"
+
+namespace dwpa {
+
+hipError_t launch_prep_dict(const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t count, uint32_t minlen,
+                            uint32_t maxlen, uint32_t* mid, uint64_t* ids, uint32_t* counter, uint32_t cap,
+                            bool compact, hipStream_t s);
+hipError_t launch_prep_numeric(uint64_t first, uint32_t count, uint32_t digits, uint32_t* mid, uint64_t* ids,
+                               uint32_t cap, hipStream_t s);
+hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
+                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s);
+hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s);
+hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
+                         const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,
+                         const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt, uint32_t hitcap,
+                         bool use_aes, hipStream_t s);
+
+}  // namespace dwpa

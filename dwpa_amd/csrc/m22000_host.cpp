@@ -1,0 +1,355 @@
+// m22000_host.cpp -- m22000 hashline parsing with PHP semantics and device-table building.
+//
+// Parsing follows web/common.php:157-237 exactly (PHP 8 quirks included, see ParsedLine).  The table builder
+// expands the nonce-error-correction loop (common.php:237-300) into explicit attempt lists: every PRF message the
+// PHP loop would hash is materialised here, pre-padded into SHA-1/SHA-256 blocks, so the GPU verifier only hashes
+// wave-uniform data.  PHP's in-place mutation of $n across attempts *and keys* (substr_replace with offset
+// clamping, :255-259) is simulated, which yields one list per key ordinal until the string reaches a fixed point.
+#include "m22000_host.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+
+#include "dwpa22000.h"
+
+namespace dwpa {
+
+// ---------------------------------------------------------------------------------------------------------
+// PHP helpers
+// ---------------------------------------------------------------------------------------------------------
+static bool is_xd(uint8_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
+static int hv(uint8_t c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; }
+
+// valid_hex(), common.php:28-36 (ctype_xdigit("") is false)
+static bool valid_hex(const char* s, size_t n) {
+    if (n == 0 || (n & 1)) return false;
+    for (size_t i = 0; i < n; i++)
+        if (!is_xd((uint8_t)s[i])) return false;
+    return true;
+}
+static std::string hex2bin(const char* s, size_t n) {
+    std::string o(n / 2, '\0');
+    for (size_t i = 0; i < n / 2; i++) o[i] = (char)(hv((uint8_t)s[2 * i]) << 4 | hv((uint8_t)s[2 * i + 1]));
+    return o;
+}
+
+bool starts_hex(const uint8_t* p, size_t n) { return n >= 5 && memcmp(p, "$HEX[", 5) == 0; }
+
+// hc_unhex(), common.php:3-25
+std::string hc_unhex(const std::string& k) {
+    if (k.size() <= 6) return k;
+    const size_t in = k.size() - 6;  // substr($key, 5, -1)
+    if (!(in & 1) && k.compare(0, 5, "$HEX[") == 0 && k.back() == ']') {
+        bool xd = true;
+        for (size_t i = 5; i < 5 + in && xd; i++) xd = is_xd((uint8_t)k[i]);
+        if (xd) return hex2bin(k.data() + 5, in);
+    }
+    return k;
+}
+
+// zend_binary_strncmp
+static int php_strncmp(const std::string& a, const std::string& b, size_t len) {
+    size_t m = std::min(len, std::min(a.size(), b.size()));
+    int r = memcmp(a.data(), b.data(), m);
+    if (r) return r;
+    size_t ma = std::min(len, a.size()), mb = std::min(len, b.size());
+    return (ma > mb) - (ma < mb);
+}
+
+// PHP 8 `$field == '0N'`: numeric strings compare by value (" 1", "1.0", "+1e0" all equal '01').
+static bool php_is_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
+static bool php_eq_type(const char* s, size_t n, int target) {
+    size_t i = 0;
+    while (i < n && php_is_ws(s[i])) i++;
+    const size_t st = i;
+    if (i < n && (s[i] == '+' || s[i] == '-')) i++;
+    size_t nd = 0, nf = 0;
+    while (i < n && s[i] >= '0' && s[i] <= '9') { i++; nd++; }
+    if (i < n && s[i] == '.') {
+        i++;
+        while (i < n && s[i] >= '0' && s[i] <= '9') { i++; nf++; }
+    }
+    if (nd + nf == 0) return false;  // not numeric -> plain string compare with "0N" (which is numeric): unequal
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+        size_t j = i + 1;
+        if (j < n && (s[j] == '+' || s[j] == '-')) j++;
+        size_t e0 = j;
+        while (j < n && s[j] >= '0' && s[j] <= '9') j++;
+        if (j > e0) i = j;
+    }
+    const size_t en = i;
+    while (i < n && php_is_ws(s[i])) i++;
+    if (i != n) return false;
+    std::string num(s + st, en - st);
+    return strtod(num.c_str(), nullptr) == (double)target;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// parse
+// ---------------------------------------------------------------------------------------------------------
+ParsedLine parse_m22000(const char* s, size_t n) {
+    ParsedLine p;
+    const char* f[9];
+    size_t fl[9];
+    size_t cnt = 0, st = 0;
+    for (size_t i = 0; i < n && cnt < 8; i++)
+        if (s[i] == '*') { f[cnt] = s + st; fl[cnt] = i - st; cnt++; st = i + 1; }
+    f[cnt] = s + st; fl[cnt] = n - st; cnt++;            // explode('*', $hashline, 9)
+    if (cnt != 9 || fl[0] != 3 || memcmp(f[0], "WPA", 3) != 0) { p.status = DWPA_E_FORMAT; return p; }
+    if (!valid_hex(f[3], fl[3]) || !valid_hex(f[4], fl[4]) || !valid_hex(f[5], fl[5])) { p.status = DWPA_E_HEX; return p; }
+    p.mac_ap = hex2bin(f[3], fl[3]);
+    p.mac_sta = hex2bin(f[4], fl[4]);
+    p.essid = hex2bin(f[5], fl[5]);
+    p.field2_hex.assign(f[2], fl[2]);
+    if (php_eq_type(f[1], fl[1], 1)) {
+        p.kind = LINE_PMKID;
+        if (!valid_hex(f[2], fl[2])) { p.status = DWPA_E_HEX; return p; }
+        p.pmkid = hex2bin(f[2], fl[2]);
+    } else if (php_eq_type(f[1], fl[1], 2)) {
+        p.kind = LINE_EAPOL;
+        for (int k : {2, 6, 7, 8})
+            if (!valid_hex(f[k], fl[k])) { p.status = DWPA_E_HEX; return p; }
+        p.keymic = hex2bin(f[2], fl[2]);
+        p.nonce_ap = hex2bin(f[6], fl[6]);
+        p.eapol = hex2bin(f[7], fl[7]);
+        p.mp = hex2bin(f[8], fl[8]);
+        // unpack('x5/nkey_information/x10/a32nonce_sta', $eapol) needs 49 bytes, else null -> keyver 0
+        if (p.eapol.size() >= 49) p.keyver = (((uint8_t)p.eapol[5] << 8) | (uint8_t)p.eapol[6]) & 3;
+        if (p.keyver == 0) p.status = DWPA_E_KEYVER;  // common.php:274-276: unknown keyver -> False
+    } else {
+        p.status = DWPA_E_TYPE;
+    }
+    return p;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// padding helpers
+// ---------------------------------------------------------------------------------------------------------
+// SHA-1 / SHA-256 message stream of `msg` hashed after `prefix_len` bytes (the HMAC key block), big-endian words.
+static std::vector<uint32_t> md_stream_be(const std::string& msg, uint64_t prefix_len) {
+    std::string b = msg;
+    b.push_back((char)0x80);
+    while (b.size() % 64 != 56) b.push_back('\0');
+    const uint64_t bits = (prefix_len + msg.size()) * 8;
+    for (int i = 7; i >= 0; i--) b.push_back((char)(bits >> (8 * i)));
+    std::vector<uint32_t> w(b.size() / 4);
+    for (size_t i = 0; i < w.size(); i++)
+        w[i] = (uint32_t)(uint8_t)b[4 * i] << 24 | (uint32_t)(uint8_t)b[4 * i + 1] << 16 |
+               (uint32_t)(uint8_t)b[4 * i + 2] << 8 | (uint8_t)b[4 * i + 3];
+    return w;
+}
+static std::vector<uint32_t> md5_stream_le(const std::string& msg, uint64_t prefix_len) {
+    std::string b = msg;
+    b.push_back((char)0x80);
+    while (b.size() % 64 != 56) b.push_back('\0');
+    const uint64_t bits = (prefix_len + msg.size()) * 8;
+    for (int i = 0; i < 8; i++) b.push_back((char)(bits >> (8 * i)));
+    std::vector<uint32_t> w(b.size() / 4);
+    for (size_t i = 0; i < w.size(); i++)
+        w[i] = (uint32_t)(uint8_t)b[4 * i] | (uint32_t)(uint8_t)b[4 * i + 1] << 8 |
+               (uint32_t)(uint8_t)b[4 * i + 2] << 16 | (uint32_t)(uint8_t)b[4 * i + 3] << 24;
+    return w;
+}
+static uint32_t be32(const std::string& s, size_t o) {
+    return (uint32_t)(uint8_t)s[o] << 24 | (uint32_t)(uint8_t)s[o + 1] << 16 | (uint32_t)(uint8_t)s[o + 2] << 8 |
+           (uint8_t)s[o + 3];
+}
+static uint32_t le32(const std::string& s, size_t o) {
+    return (uint32_t)(uint8_t)s[o] | (uint32_t)(uint8_t)s[o + 1] << 8 | (uint32_t)(uint8_t)s[o + 2] << 16 |
+           (uint32_t)(uint8_t)s[o + 3] << 24;
+}
+
+// PHP 8 substr_replace($s, $r, $off, $len) with offset/length clamping
+static void php_substr_replace(std::string& s, const std::string& r, size_t off, size_t len) {
+    if (off > s.size()) off = s.size();
+    if (off + len > s.size()) len = s.size() - off;
+    s.replace(off, len, r);
+}
+
+uint32_t build_salt_blocks(const std::string& essid, std::vector<uint32_t>& out) {
+    out.clear();
+    uint32_t nblk = 0;
+    for (int i = 1; i <= 2; i++) {
+        std::string m = essid;
+        m.push_back('\0'); m.push_back('\0'); m.push_back('\0'); m.push_back((char)i);
+        std::vector<uint32_t> w = md_stream_be(m, 64);
+        nblk = (uint32_t)(w.size() / 16);
+        out.insert(out.end(), w.begin(), w.end());
+    }
+    return nblk;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// table builder
+// ---------------------------------------------------------------------------------------------------------
+uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int nec) {
+    LineDev L;
+    memset(&L, 0, sizeof(L));
+    L.kind = (uint32_t)p.kind;
+    const uint32_t idx = (uint32_t)lines.size();
+    if (p.kind == LINE_PMKID) {
+        std::string msg = std::string("PMK Name") + p.mac_ap + p.mac_sta;
+        std::vector<uint32_t> w = md_stream_be(msg, 64);
+        L.msg_off = (uint32_t)pool.size();
+        L.msg_nblk = (uint32_t)(w.size() / 16);
+        pool.insert(pool.end(), w.begin(), w.end());
+        const bool ok = p.pmkid.size() >= 16;  // strncmp(20-byte digest, $pmkid, 16) needs >= 16 bytes
+        for (int k = 0; k < 4; k++) L.target[k] = ok ? be32(p.pmkid, 4 * k) : 0;
+        lines.push_back(L);
+        never.push_back(ok ? 0 : 1);
+        return idx;
+    }
+
+    // ---- EAPOL, common.php:192-300
+    L.keyver = (uint32_t)p.keyver;
+    const std::string nonce_sta = p.eapol.substr(17, 32);
+    const std::string m = php_strncmp(p.mac_ap, p.mac_sta, 6) < 0 ? p.mac_ap + p.mac_sta : p.mac_sta + p.mac_ap;
+    bool swap = false;
+    std::string n0;
+    if (php_strncmp(nonce_sta, p.nonce_ap, 6) < 0) n0 = nonce_sta + p.nonce_ap;
+    else { n0 = p.nonce_ap + nonce_sta; swap = true; }
+    int64_t corrV = 0, corrN = 0;  // unpack('x28/V'|'x28/N', $nonce_ap)[1], null -> 0 when < 32 bytes
+    if (p.nonce_ap.size() >= 32) {
+        corrV = le32(p.nonce_ap, 28);
+        corrN = be32(p.nonce_ap, 28);
+    }
+    struct Att { bool big; int64_t off; };
+    std::vector<Att> order;
+    order.push_back({true, 0});
+    if (nc_mode == DWPA_NC_HASHCAT) {
+        const uint8_t mp = p.mp.empty() ? 0 : (uint8_t)p.mp[0];
+        const bool none = mp & 0x10, le_only = (mp & 0x20) && !(mp & 0x40), be_only = (mp & 0x40) && !(mp & 0x20);
+        if (!none)
+            for (int64_t k = 1; k <= nec; k++) {
+                if (!be_only) { order.push_back({false, k}); order.push_back({false, -k}); }
+                if (!le_only) { order.push_back({true, k}); order.push_back({true, -k}); }
+            }
+    } else {
+        const int64_t halfnc = ((int64_t)nc >> 1) + 1;  // loop runs for offsets 1..halfnc (do/while, :293-300)
+        for (int64_t k = 1; k <= halfnc; k++) {
+            order.push_back({false, k}); order.push_back({false, -k});
+            order.push_back({true, k}); order.push_back({true, -k});
+        }
+    }
+    const bool kv3 = p.keyver == 3;
+    const std::string pre = kv3 ? std::string("\x01\x00Pairwise key expansion", 24) + m
+                                : std::string("Pairwise key expansion\0", 23) + m;
+    const std::string post = kv3 ? std::string("\x80\x01", 2) : std::string("\0", 1);
+    const size_t patch = swap ? 28 : 60;
+
+    auto raw_of = [&](const Att& a) {
+        const uint32_t v = (uint32_t)(uint64_t)((a.big ? corrN : corrV) + a.off);
+        std::string r(4, '\0');
+        for (int i = 0; i < 4; i++) r[i] = (char)(a.big ? v >> (24 - 8 * i) : v >> (8 * i));
+        return r;
+    };
+
+    // lists[k][a] = full PRF message of attempt a for the k-th non-null key
+    std::vector<std::vector<std::string>> lists;
+    if (nc_mode == DWPA_NC_HASHCAT) {
+        std::vector<std::string> lst;
+        for (const Att& a : order) {
+            std::string nn = n0;
+            php_substr_replace(nn, raw_of(a), patch, 4);
+            lst.push_back(pre + nn + post);
+        }
+        lists.push_back(std::move(lst));
+    } else {
+        std::string ns = n0;  // PHP's $n, carried across attempts and keys
+        std::vector<std::string> starts;
+        for (int q = 0; q < 256; q++) {
+            starts.push_back(ns);
+            std::vector<std::string> lst;
+            for (const Att& a : order) {
+                php_substr_replace(ns, raw_of(a), patch, 4);
+                lst.push_back(pre + ns + post);
+            }
+            lists.push_back(std::move(lst));
+            if (ns == starts.back()) break;  // fixed point: every later key sees this list again
+        }
+        while (lists.size() >= 2 && lists[lists.size() - 2] == lists.back()) lists.pop_back();
+    }
+
+    // pre-pad every attempt; share the leading blocks common to all of them
+    std::vector<std::vector<std::vector<uint32_t>>> streams(lists.size());
+    size_t minblk = SIZE_MAX;
+    for (size_t k = 0; k < lists.size(); k++)
+        for (const std::string& msg : lists[k]) {
+            streams[k].push_back(md_stream_be(msg, 64));
+            minblk = std::min(minblk, streams[k].back().size() / 16);
+        }
+    const std::vector<uint32_t>& ref = streams[0][0];
+    size_t prefix = 0;
+    while (prefix + 1 < minblk) {
+        bool same = true;
+        for (auto& lst : streams)
+            for (auto& w : lst)
+                if (!std::equal(w.begin() + 16 * prefix, w.begin() + 16 * (prefix + 1), ref.begin() + 16 * prefix)) same = false;
+        if (!same) break;
+        prefix++;
+    }
+    L.pre_off = (uint32_t)pool.size();
+    L.pre_nblk = (uint32_t)prefix;
+    pool.insert(pool.end(), ref.begin(), ref.begin() + 16 * prefix);
+    L.list_off = (uint32_t)atts.size();
+    L.nlists = (uint32_t)lists.size();
+    L.natt = (uint32_t)order.size();
+    for (size_t k = 0; k < lists.size(); k++)
+        for (size_t a = 0; a < order.size(); a++) {
+            const std::vector<uint32_t>& w = streams[k][a];
+            AttDev at;
+            at.blk_off = (uint32_t)pool.size();
+            at.nblk = (uint32_t)(w.size() / 16 - prefix);
+            at.nc = a == 0 ? 0 : (int32_t)order[a].off;
+            at.endian = a == 0 ? 0u : (order[a].big ? 1u : 2u);
+            pool.insert(pool.end(), w.begin() + 16 * prefix, w.end());
+            atts.push_back(at);
+        }
+
+    // MIC input
+    L.mic_off = (uint32_t)pool.size();
+    if (p.keyver == 1 || p.keyver == 2) {
+        std::vector<uint32_t> w = p.keyver == 1 ? md5_stream_le(p.eapol, 64) : md_stream_be(p.eapol, 64);
+        L.mic_nblk = (uint32_t)(w.size() / 16);
+        pool.insert(pool.end(), w.begin(), w.end());
+    } else {
+        any_aes = true;
+        const size_t len = p.eapol.size();
+        const size_t nb = (len + 15) / 16;
+        std::string b = p.eapol;
+        L.cmac_complete = (len % 16 == 0) ? 1u : 0u;
+        if (len % 16) {
+            b.push_back((char)0x80);
+            while (b.size() % 16) b.push_back('\0');
+        }
+        for (size_t i = 0; i < nb * 4; i++) pool.push_back(be32(b, 4 * i));
+        L.mic_nblk = (uint32_t)nb;
+    }
+    const bool ok = p.keymic.size() >= 16;
+    for (int k = 0; k < 4; k++) L.target[k] = !ok ? 0u : (p.keyver == 1 ? le32(p.keymic, 4 * k) : be32(p.keymic, 4 * k));
+    lines.push_back(L);
+    never.push_back(ok ? 0 : 1);
+    return idx;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// outfile helpers
+// ---------------------------------------------------------------------------------------------------------
+std::string hex_lower(const std::string& s) {
+    static const char* d = "0123456789abcdef";
+    std::string o;
+    o.reserve(s.size() * 2);
+    for (unsigned char c : s) { o.push_back(d[c >> 4]); o.push_back(d[c & 15]); }
+    return o;
+}
+
+std::string hashcat_plain(const std::string& s) {
+    bool hex = s.compare(0, 5, "$HEX[") == 0;
+    for (unsigned char c : s)
+        if (c < 0x20 || c > 0x7e || c == ':') hex = true;
+    return hex ? "$HEX[" + hex_lower(s) + "]" : s;
+}
+
+}  // namespace dwpa

@@ -1,0 +1,47 @@
+// m22000_host.hpp -- hashline parsing (PHP semantics) and device-table building (internal).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "tables.hpp"
+
+namespace dwpa {
+
+// A hashline parsed with the exact acceptance rules of web/common.php:157-195.
+struct ParsedLine {
+    int status = 0;          // 0 ok, else DWPA_E_*
+    int kind = 0;            // LINE_PMKID / LINE_EAPOL
+    std::string mac_ap, mac_sta, essid, pmkid, keymic, nonce_ap, eapol, mp;
+    int keyver = 0;          // EAPOL key_information & 3 (0 if the frame is < 49 bytes)
+    std::string field2_hex;  // PMKID/MIC exactly as written (outfile)
+};
+
+ParsedLine parse_m22000(const char* s, size_t n);
+
+// hashcat $HEX[] decoding as web/common.php:3-25 (only applied to keys starting with "$HEX[")
+std::string hc_unhex(const std::string& k);
+bool starts_hex(const uint8_t* p, size_t n);
+
+// Host image of the device tables of one work unit.
+struct TableBuilder {
+    std::vector<LineDev> lines;
+    std::vector<AttDev> atts;
+    std::vector<uint32_t> pool;  // pre-padded hash blocks (16 words each) and CMAC blocks (4 words each)
+    std::vector<uint8_t> never;  // per line: 1 if the line can never match (target shorter than 16 bytes)
+    bool any_aes = false;
+
+    // Adds a parsed (status 0) line; returns its index.
+    uint32_t add_line(const ParsedLine& p, int nc, int nc_mode, int nec);
+};
+
+// PBKDF2 salt blocks for an ESSID: [2][nblk][16] big-endian words of ESSID || INT(i) || SHA1 padding
+// (inner hash after the 64-byte ipad block).  Returns nblk.
+uint32_t build_salt_blocks(const std::string& essid, std::vector<uint32_t>& out);
+
+// outfile helpers (hashcat outfile-format 1 for -m 22000 as parsed by help_crack.py:807-815)
+std::string hex_lower(const std::string& s);
+std::string hashcat_plain(const std::string& s);  // printable ASCII without ':' as-is, else $HEX[..]
+
+}  // namespace dwpa

@@ -1,0 +1,57 @@
+// tables.hpp -- device-resident job tables shared by host builder (m22000_host.cpp) and kernels (kernels.hip).
+//
+// A work unit is a set of m22000 hashlines grouped by ESSID ("salt group"): one PMK per (ESSID, candidate) is
+// computed once and tested against every line of that ESSID (north_star "salt reuse"; get_work hands out one
+// ESSID per work unit, web/content/get_work.php:96-109).  Everything that is uniform across candidates -- the
+// PRF messages of every nonce-correction attempt, EAPOL frames, PMKID messages -- is pre-padded on the host into
+// hash blocks so that the verifier kernel reads it with wave-uniform (scalar) loads.
+#pragma once
+#include <stdint.h>
+
+namespace dwpa {
+
+enum : uint32_t { LINE_PMKID = 1, LINE_EAPOL = 2 };
+
+struct LineDev {
+    uint32_t kind;        // LINE_PMKID / LINE_EAPOL
+    uint32_t keyver;      // EAPOL key version 1/2/3 (key_information & 3, common.php:215-217)
+    uint32_t target[4];   // PMKID or MIC (first 16 bytes): BE words (SHA1/CMAC) or LE words (MD5, keyver 1)
+    uint32_t msg_off;     // PMKID: pre-padded HMAC-SHA1 inner blocks of "PMK Name"||AP||STA (word offset in pool)
+    uint32_t msg_nblk;
+    uint32_t pre_off;     // EAPOL: PRF message blocks shared by every attempt (pre-padded), word offset
+    uint32_t pre_nblk;
+    uint32_t list_off;    // EAPOL: attempt lists; list k = attempts [list_off + k*natt, +natt) in the attempt table
+    uint32_t nlists;      // list k applies to the k-th non-null key (PHP mutates $n across keys); last list to the rest
+    uint32_t natt;        // attempts per list (1 + 4*halfnc in PHP order, common.php:250-300)
+    uint32_t mic_off;     // EAPOL: HMAC inner blocks of the EAPOL frame (keyver 1/2), or CMAC blocks (keyver 3)
+    uint32_t mic_nblk;
+    uint32_t cmac_complete;  // keyver 3: 1 if the last EAPOL block is complete (XOR K1), else padded (XOR K2)
+};
+static_assert(sizeof(LineDev) % 16 == 0, "LineDev must stay 16-byte aligned");
+
+struct AttDev {
+    uint32_t blk_off;     // word offset of this attempt's PRF blocks after the shared prefix
+    uint32_t nblk;
+    int32_t nc;           // signed correction reported on a hit (0 for the first attempt)
+    uint32_t endian;      // 0 none (exact), 1 BE ('N'), 2 LE ('V')
+};
+
+// One wave (64 lanes) verifies up to 64 consecutive candidate slots against one line.
+struct SegDev {
+    uint32_t line;        // index into the line table
+    uint32_t slot;        // first candidate slot (PMK buffer index)
+    uint32_t count;       // <= 64
+    uint32_t pad;
+};
+
+struct HitDev {
+    uint64_t cand;        // candidate id (dictionary word index / key ordinal / numeric value / word*nrules+rule)
+    uint32_t line;
+    uint32_t attempt;     // attempt index within the applicable list (PMKID: 0)
+    uint32_t pmk[8];      // PMK as big-endian words
+};
+
+constexpr int MID_WORDS = 10;   // ipad h0..h4, opad h0..h4 (SoA: word k of slot s at mid[k*cap + s])
+constexpr int PMK_WORDS = 8;
+
+}  // namespace dwpa

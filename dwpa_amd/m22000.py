@@ -1,0 +1,213 @@
+"""Python host side of libdwpa22000.so, mirroring dwpa's own interfaces for the m22000 path.
+
+``check_key_m22000`` keeps the exact call signature and return shape of the PHP function it replaces
+(web/common.php:157-307): ``False`` or ``[PSK, NC, endian, PMK]`` with ``NC``/``endian`` ``None`` for PMKID
+lines, ``endian`` in ``{None, 'BE', 'LE'}``, ``PSK`` after ``$HEX[]`` decoding and ``PMK`` as 32 raw bytes.
+All arithmetic runs on the GPU through the C ABI; without a device the calls raise ``DwpaError``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib as L
+
+_ENDIAN = {0: None, 1: "BE", 2: "LE"}
+
+
+def _b(x) -> bytes:
+    if isinstance(x, str):
+        return x.encode("utf-8", "surrogateescape")
+    return bytes(x)
+
+
+def device_count() -> int:
+    return L.check(L.load().dwpa_device_count(), "device_count")
+
+
+def hc_unhex(key) -> bytes:
+    """common.php:3-25 ($HEX[...] decoding), executed by the library's host code."""
+    k = _b(key)
+    out = ctypes.create_string_buffer(max(1, len(k)))
+    n = ctypes.c_size_t(0)
+    L.check(L.load().dwpa_hc_unhex(k, len(k), out, ctypes.byref(n)), "hc_unhex")
+    return out.raw[:n.value]
+
+
+def hash_m22000(hashline):
+    """common.php:310-315: raw md5 over fields 1..7, or False."""
+    h = _b(hashline)
+    out = ctypes.create_string_buffer(16)
+    if L.load().dwpa_hash_m22000(h, len(h), out) < 0:
+        return False
+    return out.raw
+
+
+def _result(keys, r: L.Result):
+    key = keys[r.key_index]
+    key = _b(key)
+    if key.startswith(b"$HEX["):
+        key = hc_unhex(key)
+    pmk = bytes(r.pmk)
+    if not r.nc_valid:
+        return [key, None, None, pmk]
+    return [key, int(r.nc), _ENDIAN[int(r.endian)], pmk]
+
+
+def check_key_m22000(hashline, keys, pmk=False, nc: int = 128):
+    """Drop-in for PHP check_key_m22000($hashline, $keys, $pmk=False, $nc=128)."""
+    h = _b(hashline)
+    keys = list(keys)
+    arr, keep = L.bytes_array([None if k is None else _b(k) for k in keys])
+    res = L.Result()
+    pm = bytes(pmk) if pmk else None  # PHP: `if (!$pmk)` -- False/''/None all mean "derive"
+    if pm is not None and len(pm) != 32:
+        raise ValueError("pmk must be 32 bytes")
+    rc = L.check(L.load().dwpa_check_m22000(h, len(h), arr, len(keys), pm, int(nc), ctypes.byref(res)),
+                 "check_m22000")
+    if rc != L.DWPA_HIT:
+        return False
+    return _result(keys, res)
+
+
+def check_batch(jobs):
+    """jobs: iterable of (hashline, keys, pmk_or_False, nc).  Returns a list of check_key_m22000 results."""
+    jobs = list(jobs)
+    n = len(jobs)
+    carr = (L.Job * max(1, n))()
+    keep = []
+    key_lists = []
+    for i, (line, keys, pmk, nc) in enumerate(jobs):
+        h = _b(line)
+        keys = list(keys)
+        arr, k = L.bytes_array([None if x is None else _b(x) for x in keys])
+        keep += [h, arr, k]
+        key_lists.append(keys)
+        pm = bytes(pmk) if pmk else None
+        keep.append(pm)
+        carr[i].line, carr[i].line_len = h, len(h)
+        carr[i].keys, carr[i].nkeys = ctypes.cast(arr, ctypes.POINTER(L.Bytes)), len(keys)
+        carr[i].pmk, carr[i].nc = pm, int(nc)
+    out = (L.Result * max(1, n))()
+    rcs = (ctypes.c_int * max(1, n))()
+    L.check(L.load().dwpa_check_batch(carr, n, out, rcs), "check_batch")
+    res = []
+    for i in range(n):
+        if rcs[i] == L.DWPA_HIT:
+            res.append(_result(key_lists[i], out[i]))
+        else:
+            L.check(rcs[i], "check_batch job")
+            res.append(False)
+    return res
+
+
+def pbkdf2_pmk(keys, essid) -> list:
+    """PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes), on the GPU."""
+    keys = [_b(k) for k in keys]
+    e = _b(essid)
+    arr, keep = L.bytes_array(keys)
+    out = ctypes.create_string_buffer(32 * max(1, len(keys)))
+    L.check(L.load().dwpa_pbkdf2_pmk(arr, len(keys), e, len(e), out), "pbkdf2_pmk")
+    raw = out.raw
+    return [raw[32 * i:32 * i + 32] for i in range(len(keys))]
+
+
+def rules_expand(rules_text, words, device: int = 0):
+    """GPU rule application (hashcat --stdout -r): returns [[candidate or None (rejected)] per rule] per word."""
+    rt = _b(rules_text)
+    words = [_b(w) for w in words]
+    nr = ctypes.c_uint32(0)
+    lib = L.load()
+    L.check(lib.dwpa_rules_expand(device, rt, len(rt), None, 0, None, None, ctypes.byref(nr)), "rules_expand")
+    nrules = nr.value
+    if not words or not nrules:
+        return [[] for _ in words]
+    arr, keep = L.bytes_array(words)
+    out = ctypes.create_string_buffer(len(words) * nrules * 256)
+    lens = (ctypes.c_uint32 * (len(words) * nrules))()
+    L.check(lib.dwpa_rules_expand(device, rt, len(rt), arr, len(words), out, lens, ctypes.byref(nr)), "rules_expand")
+    raw = out.raw
+    res = []
+    for i in range(len(words)):
+        row = []
+        for r in range(nrules):
+            c = i * nrules + r
+            n = lens[c]
+            row.append(None if n == 0xFFFFFFFF else raw[c * 256:c * 256 + n])
+        res.append(row)
+    return res
+
+
+def crack_files(hash_file, dicts, rules_file=None, nonce_error_corrections: int = 8, out_file="help_crack.key",
+                device_mask: int = 0, batch: int = 0, nc_mode: int = L.DWPA_NC_HASHCAT) -> int:
+    """In-process hashcat -m22000 replacement; returns a hashcat exit code (0 cracked, 1 exhausted, -1 error)."""
+    cfg = L.Config(ctypes.sizeof(L.Config), device_mask, batch, nc_mode)
+    dl = [_b(d) for d in dicts]
+    darr = (ctypes.c_char_p * max(1, len(dl)))(*dl)
+    return L.load().dwpa_crack_files(_b(hash_file), darr, len(dl), _b(rules_file) if rules_file else None,
+                                     int(nonce_error_corrections), _b(out_file), ctypes.byref(cfg))
+
+
+class Scan:
+    """Device-resident scan of one work unit (hashlines grouped by ESSID) -- the client hot loop.
+
+    Pointers are raw device addresses (e.g. ``tensor.data_ptr()``), streams raw ``hipStream_t`` handles
+    (e.g. ``torch.cuda.Stream.cuda_stream``); 0 = the null stream.
+    """
+
+    def __init__(self, lines, device: int = 0, nc: int = 8, nc_mode: int = L.DWPA_NC_PHP, batch: int = 1 << 22):
+        self.lines = [_b(x) for x in lines]
+        self._lib = L.load()
+        n = len(self.lines)
+        lp = (ctypes.c_char_p * max(1, n))(*self.lines)
+        ll = (ctypes.c_size_t * max(1, n))(*[len(x) for x in self.lines])
+        h = ctypes.c_void_p()
+        L.check(self._lib.dwpa_scan_create(device, lp, ll, n, int(nc), int(nc_mode), int(batch), ctypes.byref(h)),
+                "scan_create")
+        self._h = h
+        self.batch = (int(batch) + 63) & ~63
+        self.groups = self._lib.dwpa_scan_num_groups(h)
+
+    def line_status(self, i: int) -> int:
+        return self._lib.dwpa_scan_line_status(self._h, i)
+
+    def load_dict(self, d_offsets: int, d_bytes: int, first: int, count: int, minlen=8, maxlen=63, stream: int = 0):
+        L.check(self._lib.dwpa_scan_load_dict(self._h, d_offsets, d_bytes, first, count, minlen, maxlen, stream),
+                "scan_load_dict")
+
+    def load_numeric(self, first: int, count: int, digits: int = 8, stream: int = 0):
+        L.check(self._lib.dwpa_scan_load_numeric(self._h, first, count, digits, stream), "scan_load_numeric")
+
+    def pbkdf2(self, group: int = 0, stream: int = 0):
+        L.check(self._lib.dwpa_scan_pbkdf2(self._h, group, stream), "scan_pbkdf2")
+
+    def verify(self, group: int = 0, stream: int = 0):
+        L.check(self._lib.dwpa_scan_verify(self._h, group, stream), "scan_verify")
+
+    def loaded(self, stream: int = 0) -> int:
+        c = ctypes.c_uint32(0)
+        L.check(self._lib.dwpa_scan_loaded(self._h, ctypes.byref(c), stream), "scan_loaded")
+        return c.value
+
+    def hits(self, stream: int = 0, cap: int = 1 << 16):
+        buf = (L.Hit * cap)()
+        n = ctypes.c_size_t(0)
+        L.check(self._lib.dwpa_scan_hits(self._h, buf, cap, ctypes.byref(n), stream), "scan_hits")
+        out = []
+        for i in range(min(n.value, cap)):
+            h = buf[i]
+            out.append({"cand": int(h.cand), "line": int(h.line),
+                        "nc": int(h.nc) if h.nc_valid else None,
+                        "endian": _ENDIAN[int(h.endian)] if h.nc_valid else None,
+                        "pmk": bytes(h.pmk)})
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.dwpa_scan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,157 @@
+/*
+ * dwpa22000.h -- C ABI of libdwpa22000.so, the MI355X (gfx950) m22000 PMK derivation + verification engine.
+ *
+ * Drop-in boundary for dwpa's one data-parallel hot path (PBKDF2-HMAC-SHA1 x4096 over an ESSID salt, then
+ * PMKID / EAPOL keyver 1,2,3 checks with nonce-error-correction).  Two callers bind it:
+ *
+ *   (1) PHP FFI on the server, in place of check_key_m22000()      web/common.php:157-307
+ *       call sites common.php:592 (zero PMK), :606 (PMK reuse), :902 (put_work), :919 (PMK propagation),
+ *       web/rkg.php:126,147 (router-keygen / single-mode bulk checks)
+ *   (2) Python ctypes in help_crack.py, in place of run_cracker()'s hashcat subprocess
+ *       help_crack/help_crack.py:765-802 (command line :773, rc handling :776-786, outfile parsed by get_key :804-879)
+ *
+ * Plain C types only.  The caller owns every buffer; the library keeps no caller pointer after a call returns and
+ * returns no heap memory.  All entry points are thread-safe.  There is no CPU fallback: without a usable gfx950
+ * device every compute entry point returns DWPA_E_NODEV.
+ */
+#ifndef DWPA22000_H
+#define DWPA22000_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DWPA_ABI_VERSION 1
+
+/* ---- return codes ------------------------------------------------------------------------------------------ */
+#define DWPA_MISS 0            /* no key matched (PHP: False)                                                 */
+#define DWPA_HIT 1             /* a key matched; the result struct is filled (PHP: [PSK, NC, endian, PMK])   */
+#define DWPA_E_FORMAT (-1)     /* not 9 '*'-separated fields or signature != "WPA"   (common.php:159-161)     */
+#define DWPA_E_HEX (-2)        /* a required field is not valid even-length hex       (common.php:28-36,162-195) */
+#define DWPA_E_TYPE (-3)       /* type field is neither 01 nor 02                     (common.php:167,190,306) */
+#define DWPA_E_KEYVER (-4)     /* EAPOL key version not 1/2/3 or EAPOL < 49 bytes     (common.php:274-276)     */
+#define DWPA_E_NODEV (-10)     /* no usable gfx950 device                                                      */
+#define DWPA_E_HIP (-11)       /* HIP runtime error                                                            */
+#define DWPA_E_ARG (-12)       /* invalid argument                                                             */
+#define DWPA_E_NOMEM (-13)     /* host or device allocation failed                                             */
+#define DWPA_E_IO (-14)        /* file could not be read or written                                            */
+#define DWPA_E_OVERFLOW (-15)  /* hit buffer overflow                                                          */
+#define DWPA_E_RULE (-16)      /* unsupported or malformed rule                                                */
+/* Every negative code maps to PHP False in the wrappers (check_key_m22000 returns False on all of them). */
+
+/* hashcat exit codes returned by dwpa_crack_files (help_crack.py:776-786,930 interpret them) */
+#define DWPA_RC_CRACKED 0      /* every hashline cracked                                                       */
+#define DWPA_RC_EXHAUSTED 1    /* keyspace exhausted, not every hashline cracked                               */
+#define DWPA_RC_ERROR (-1)
+
+/* nonce-error-correction semantics */
+#define DWPA_NC_PHP 0          /* common.php:250-300: N+0, then V+k,V-k,N+k,N-k for k = 1..(nc>>1)+1, $n mutated */
+#define DWPA_NC_HASHCAT 1      /* hashcat --nonce-error-corrections=N: N+0, then +-k, k = 1..N, message_pair bits
+                                  0x10 (no NC), 0x20 (LE only), 0x40 (BE only) honoured (third-party semantics)   */
+
+typedef struct {
+    const uint8_t *ptr;        /* NULL = PHP null key (skipped, common.php:172,240) */
+    size_t len;
+} dwpa_bytes;
+
+typedef struct {
+    int32_t key_index;         /* index into keys[] of the first matching key (input order), -1 if none    */
+    int32_t nc;                /* nonce correction (DB column nets.nc); valid when nc_valid                */
+    int8_t endian;             /* 0 = Null, 1 = 'BE', 2 = 'LE'  (DB column nets.endian)                    */
+    uint8_t nc_valid;          /* 0 = PHP Null (PMKID lines), 1 = integer                                  */
+    uint8_t reserved[2];
+    uint8_t pmk[32];           /* PMK used for the hit (DB column nets.pmk)                                */
+} dwpa_result;
+
+typedef struct {
+    const char *line;          /* one m22000 hashline (WPA*01*... / WPA*02*...), not NUL-terminated needed  */
+    size_t line_len;
+    const dwpa_bytes *keys;
+    size_t nkeys;
+    const uint8_t *pmk;        /* NULL, or 32 bytes used for the first non-null key (common.php:157,178)    */
+    int32_t nc;                /* PHP $nc (default 128)                                                    */
+} dwpa_job;
+
+typedef struct {
+    uint32_t struct_size;      /* sizeof(dwpa_config) */
+    uint32_t device_mask;      /* bit d = use device d; 0 = all visible devices */
+    uint32_t batch;            /* candidate slots per device per launch; 0 = auto */
+    int32_t nc_mode;           /* DWPA_NC_PHP or DWPA_NC_HASHCAT (crack_files default: HASHCAT) */
+    int32_t reserved[4];
+} dwpa_config;
+
+typedef struct {
+    uint64_t cand;             /* candidate id: dictionary word index, numeric value, or word*nrules+rule */
+    uint32_t line;             /* index of the hashline in the scan's line array */
+    int32_t nc;
+    int8_t endian;
+    uint8_t nc_valid;
+    uint8_t reserved[2];
+    uint8_t pmk[32];
+} dwpa_hit;
+
+/* ---- library ------------------------------------------------------------------------------------------------ */
+int dwpa_abi_version(void);
+/* Optional: select devices / batch size.  Lazy and idempotent; every entry point initialises on first use. */
+int dwpa_init(const dwpa_config *cfg);
+int dwpa_device_count(void);
+const char *dwpa_strerror(int code);
+void dwpa_shutdown(void);
+
+/* ---- server-side check: PHP FFI replacement of check_key_m22000 (web/common.php:157-307) -------------------- */
+/* Returns DWPA_HIT and fills *out, DWPA_MISS, or a negative code (all of which PHP reads as False). */
+int dwpa_check_m22000(const char *line, size_t line_len, const dwpa_bytes *keys, size_t nkeys,
+                      const uint8_t *pmk /* nullable, 32 bytes */, int nc, dwpa_result *out);
+/* Bulk form (put_work's per-candidate loop, rkg.php's per-net loop): jobs grouped by ESSID internally so
+ * each (ESSID, key) PMK is derived once.  rcs[i] / out[i] as for dwpa_check_m22000.  Returns 0 or a
+ * negative code if the whole batch failed (device error). */
+int dwpa_check_batch(const dwpa_job *jobs, size_t njobs, dwpa_result *out, int *rcs);
+
+/* ---- primitives exposed for parity tests and wrappers ------------------------------------------------------ */
+/* PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes, no $HEX[] decoding). */
+int dwpa_pbkdf2_pmk(const dwpa_bytes *keys, size_t nkeys, const uint8_t *essid, size_t essid_len,
+                    uint8_t *pmks_out /* nkeys * 32 */);
+/* hashcat $HEX[...] decoding as web/common.php:3-25; *out_len <= in_len. */
+int dwpa_hc_unhex(const uint8_t *in, size_t in_len, uint8_t *out, size_t *out_len);
+/* md5 over fields 1..7 (common.php:310-315); DWPA_E_FORMAT if the line has != 9 fields. */
+int dwpa_hash_m22000(const char *line, size_t line_len, uint8_t out[16]);
+
+/* ---- client-side: ctypes replacement of run_cracker() (help_crack.py:765-802) ------------------------------ */
+/* Reads hash_file (one m22000 line per line), the dictionaries (plain text or .gz, one word per line, $HEX[]
+ * decoded), applies rules_file (hashcat rule syntax, may be NULL) and writes one outfile record per cracked line:
+ *   <PMKID|MIC hex>:<MAC_AP hex>:<MAC_STA hex>:<ESSID>:<PSK>   (ESSID/PSK as $HEX[..] when not printable)
+ * Returns a hashcat exit code (DWPA_RC_*).  nonce_error_corrections as --nonce-error-corrections. */
+int dwpa_crack_files(const char *hash_file, const char *const *dicts, size_t ndicts, const char *rules_file,
+                     int nonce_error_corrections, const char *out_file, const dwpa_config *cfg);
+
+/* ---- device-resident scan API (inputs already in HBM; used by the client loop and bench.py) --------------- */
+typedef struct dwpa_scan dwpa_scan;
+/* Upload a work unit's hashlines (any number of ESSIDs) to `device` with a batch of `batch` candidate slots. */
+int dwpa_scan_create(int device, const char *const *lines, const size_t *line_lens, size_t nlines, int nc,
+                     int nc_mode, uint32_t batch, dwpa_scan **out);
+int dwpa_scan_num_groups(const dwpa_scan *scan);              /* number of distinct ESSIDs */
+int dwpa_scan_line_status(const dwpa_scan *scan, size_t line); /* 0 usable, or the negative parse code */
+/* Stage 1: candidates into the batch.  Dictionary words [first, first+count) of an HBM-resident dictionary
+ * (d_offsets: count+1 uint64 byte offsets into d_bytes).  Words outside [minlen, maxlen] are dropped
+ * (hashcat m22000 accepts 8..63).  count <= batch. */
+int dwpa_scan_load_dict(dwpa_scan *scan, const uint64_t *d_offsets, const uint8_t *d_bytes, uint64_t first,
+                        uint32_t count, uint32_t minlen, uint32_t maxlen, void *hip_stream);
+/* Decimal keyspace first..first+count-1, zero-padded to `digits` characters. */
+int dwpa_scan_load_numeric(dwpa_scan *scan, uint64_t first, uint32_t count, uint32_t digits, void *hip_stream);
+/* Stages 2 and 3 for ESSID group g (PMKs of the loaded batch, then every uncracked line of that ESSID). */
+int dwpa_scan_pbkdf2(dwpa_scan *scan, int group, void *hip_stream);
+int dwpa_scan_verify(dwpa_scan *scan, int group, void *hip_stream);
+/* Synchronises the stream, returns hits found since the last call (*nhits may exceed cap: then call again
+ * with a bigger buffer is not possible -- size cap >= batch). */
+int dwpa_scan_hits(dwpa_scan *scan, dwpa_hit *out, size_t cap, size_t *nhits, void *hip_stream);
+/* Candidate slots filled by the last load (synchronises). */
+int dwpa_scan_loaded(dwpa_scan *scan, uint32_t *count, void *hip_stream);
+void dwpa_scan_destroy(dwpa_scan *scan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DWPA22000_H */

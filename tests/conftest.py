@@ -1,0 +1,46 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built libdwpa22000.so")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def dec(v):
+    """JSON fixture value -> python (bytes for {'hex': ...})."""
+    if isinstance(v, dict) and "hex" in v:
+        return bytes.fromhex(v["hex"])
+    if isinstance(v, list):
+        return [dec(x) for x in v]
+    return v
+
+
+def job_args(j):
+    line = j["line"].encode("latin-1")
+    keys = [None if k is None else bytes.fromhex(k) for k in j["keys"]]
+    pmk = bytes.fromhex(j["pmk"]) if j["pmk"] else False
+    return line, keys, pmk, j["nc"]
+
+
+@pytest.fixture(scope="session")
+def mixed():
+    return load_golden("mixed.json")["jobs"]
+
+
+@pytest.fixture(scope="session")
+def kat():
+    return load_golden("kat.json")

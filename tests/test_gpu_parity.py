@@ -1,0 +1,199 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle, bit-exact on every result tuple.
+
+Oracle = CPU restatement of web/common.php (oracle/), pinned by tests/test_oracle.py.  Fixtures under
+tests/golden/ were produced by the oracle (tests/golden/make_golden.py).
+"""
+import gzip
+import os
+import random
+from concurrent.futures import ThreadPoolExecutor
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import dwpa_amd  # noqa: E402
+from dwpa_amd import synth as S  # noqa: E402
+from dwpa_amd.rulesets import wpa_rules  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+from oracle import rules as R  # noqa: E402
+from tests.conftest import dec, job_args  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert dwpa_amd.device_count() >= 1
+    yield
+
+
+def test_pbkdf2_vectors(kat):
+    for v in kat["pbkdf2"]:
+        p, s = bytes.fromhex(v["password"]), bytes.fromhex(v["salt"])
+        assert dwpa_amd.pbkdf2_pmk([p], s)[0].hex() == v["pmk32"]
+
+
+def test_pbkdf2_random_lengths():
+    rng = random.Random(7)
+    keys = [bytes(rng.randrange(256) for _ in range(n)) for n in list(range(0, 70)) + [100, 127, 128, 200, 300]]
+    for essid_len in (1, 7, 32, 47, 51, 52, 60, 120):
+        essid = bytes(rng.randrange(256) for _ in range(essid_len))
+        got = dwpa_amd.pbkdf2_pmk(keys, essid)
+        exp = O.c_pbkdf2_many(keys, essid, threads=16)
+        assert b"".join(got) == exp, essid_len
+
+
+def test_challenge_kat(kat):
+    for c in kat["challenge"]:
+        assert dwpa_amd.check_key_m22000(c["line"], [b"aaaa1234"]) == dec(c["expect"])
+    # the outfile must carry both challenge records with the same PSK (help_crack.py:886-895)
+    r = dwpa_amd.check_key_m22000(kat["challenge"][1]["line"], [b"x" * 8, b"aaaa1234"], False, 8)
+    assert r[0] == b"aaaa1234" and r[1:3] == [4, "LE"]
+
+
+def test_mixed_golden_single(mixed):
+    for j in mixed:
+        line, keys, pmk, nc = job_args(j)
+        assert dwpa_amd.check_key_m22000(line, keys, pmk, nc) == dec(j["expect"]), j["tag"]
+
+
+def test_mixed_golden_batch(mixed):
+    jobs = [job_args(j) for j in mixed]
+    got = dwpa_amd.check_batch(jobs)
+    for j, g in zip(mixed, got):
+        assert g == dec(j["expect"]), j["tag"]
+
+
+def _oracle_many(jobs):
+    with ThreadPoolExecutor(16) as ex:
+        return list(ex.map(lambda a: O.c_check_key_m22000(*a), jobs))
+
+
+def test_random_batch_vs_oracle():
+    """C5-shaped: PMKID + keyver 1/2/3, planted corrections, decoys, shared ESSIDs, zero-PMK jobs."""
+    rng = random.Random(2024)
+    jobs = []
+    nets = [S.random_net(rng) for _ in range(12)]
+    for i in range(160):
+        essid, ap, sta, an, sn = nets[rng.randrange(len(nets))]
+        ap, sta = rng.randbytes(6), rng.randbytes(6)
+        psk = S.random_psk(rng)
+        kind = rng.choice(["pmkid", 1, 2, 3])
+        if kind == "pmkid":
+            line = S.pmkid_line(psk, essid, ap, sta)
+        else:
+            line = S.eapol_line(psk, essid, ap, sta, rng.randbytes(32), rng.randbytes(32), kind, rng.randint(-9, 9),
+                                rng.choice(["LE", "BE"]), rng=rng)
+        keys = [S.random_psk(rng) for _ in range(rng.randint(0, 12))]
+        if rng.random() < 0.8:
+            keys.insert(rng.randint(0, len(keys)), psk)
+        if rng.random() < 0.1:
+            keys.insert(0, None)
+        nc = rng.choice([0, 1, 8, 16, 128])
+        jobs.append((line, keys, False, nc))
+    exp = _oracle_many(jobs)
+    got = dwpa_amd.check_batch(jobs)
+    mism = [(i, g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    assert not mism, mism[:3]
+    assert sum(1 for e in exp if e) > 60
+
+
+def test_scan_dictionary_hbm():
+    import torch
+    rng = random.Random(3)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    words = [S.random_psk(rng, 8, 20) for _ in range(20000)]
+    words[123] = b"short"          # dropped by the 8..63 filter
+    words[124] = b"x" * 64         # dropped
+    psk1, psk2 = words[7777], words[19999]
+    lines = [S.eapol_line(psk1, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rng),
+             S.pmkid_line(psk2, essid, rng.randbytes(6), sta),
+             S.eapol_line(words[5], b"other", ap, sta, an, sn, 3, -2, "BE", rng=rng)]
+    off = [0]
+    for w in words:
+        off.append(off[-1] + len(w))
+    dev = torch.device("cuda:0")
+    d_off = torch.tensor(off, dtype=torch.int64, device=dev)
+    d_bytes = torch.tensor(list(b"".join(words)) + [0] * 64, dtype=torch.uint8, device=dev)
+    sc = dwpa_amd.Scan(lines, nc=8, batch=8192)
+    hits = []
+    for first in range(0, len(words), 8192):
+        cnt = min(8192, len(words) - first)
+        sc.load_dict(d_off.data_ptr(), d_bytes.data_ptr(), first, cnt)
+        for g in range(sc.groups):
+            sc.pbkdf2(g)
+            sc.verify(g)
+        hits += sc.hits()
+    got = sorted((h["line"], h["cand"], h["nc"], h["endian"]) for h in hits)
+    assert got == [(0, 7777, 3, "LE"), (1, 19999, None, None), (2, 5, -2, "BE")]
+    for h in hits:
+        w = words[h["cand"]]
+        assert h["pmk"] == S.pmk(w, essid if h["line"] < 2 else b"other")
+    sc.close()
+
+
+def test_scan_numeric_keyspace():
+    rng = random.Random(4)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    lines = [S.pmkid_line(b"00731941", essid, ap, sta),
+             S.eapol_line(b"00999999", essid, ap, sta, an, sn, 1, -1, "BE", rng=rng)]
+    sc = dwpa_amd.Scan(lines, nc=8, batch=1 << 16)
+    hits = []
+    for first in range(700000, 1000000, 1 << 16):
+        sc.load_numeric(first, min(1 << 16, 1000000 - first), 8)
+        sc.pbkdf2(0)
+        sc.verify(0)
+        hits += sc.hits()
+    assert sorted((h["line"], h["cand"], h["nc"]) for h in hits) == [(0, 731941, None), (1, 999999, -1)]
+    sc.close()
+
+
+def test_rules_expand_vs_oracle():
+    rng = random.Random(5)
+    rules = wpa_rules() + ["C", "t", "q", "{", "}", "z2", "Z3", "@a", "sab", "p3", "D0", "'0", "T9", "$ ", "^ "]
+    words = [S.random_psk(rng, 1, 30) for _ in range(300)] + [b"a", b"Password", b"x" * 130, b"y" * 255, b"z" * 256]
+    got = dwpa_amd.rules_expand("\n".join(rules), words)
+    exp = R.expand(rules, words)
+    assert got == exp
+
+
+def test_crack_files_challenge(tmp_path):
+    hf = tmp_path / "help_crack.hash"
+    hf.write_bytes(b"\n".join(S.CHALLENGE_LINES) + b"\n")
+    d1 = tmp_path / "d1.txt.gz"
+    with gzip.open(d1, "wb") as f:
+        f.write(b"\n".join([b"password%d" % i for i in range(5000)] + [b"aaaa1234"]) + b"\n")
+    out = tmp_path / "help_crack.key"
+    rc = dwpa_amd.crack_files(str(hf), [str(d1)], None, 8, str(out))
+    assert rc == 0
+    txt = out.read_text()
+    recs = txt.strip().split("\n")
+    assert len(recs) == 2
+    for r in recs:
+        assert "1c7ee5e2f2d0:0026c72e4900:dlink:aaaa1234" in r  # help_crack.py:858-860
+    # help_crack's parser (get_key, :807-815) reads k = MAC_AP, v = hex(PSK)
+    for r in recs:
+        arr = r.split(":", 4)
+        assert arr[1][:12] == "1c7ee5e2f2d0" and arr[4].encode().hex() == b"aaaa1234".hex()
+
+
+def test_crack_files_rules_and_exhausted(tmp_path):
+    rng = random.Random(6)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    base = [S.random_psk(rng, 6, 12) for _ in range(3000)]
+    rules = wpa_rules()
+    target_word, target_rule = base[1234], rules.index("c $1 $2 $3")
+    psk = R.apply(R.parse(rules[target_rule]), target_word)
+    lines = [S.eapol_line(psk, essid, ap, sta, an, sn, 2, 2, "BE", rng=rng),
+             S.pmkid_line(b"not-in-dict-!!", essid, ap, sta)]
+    hf = tmp_path / "h.hash"
+    hf.write_bytes(b"\n".join(lines) + b"\n")
+    d = tmp_path / "d.txt"
+    d.write_bytes(b"\n".join(base) + b"\n")
+    rf = tmp_path / "r.rule"
+    rf.write_text("\n".join(rules) + "\n")
+    out = tmp_path / "o.key"
+    rc = dwpa_amd.crack_files(str(hf), [str(d)], str(rf), 8, str(out), batch=1 << 16)
+    assert rc == 1
+    recs = out.read_bytes().strip().split(b"\n")
+    assert len(recs) == 1
+    assert recs[0].endswith(b":" + psk)
