@@ -46,48 +46,47 @@ def parse():
     return ap.parse_args()
 
 
-def make_dictionary(torch, n, dev, seed=2):
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
-    lens = torch.empty(n, dtype=torch.float32, device=dev).geometric_(0.3, generator=g).add_(7).clamp_(8, 63)
-    lens = lens.to(torch.int64)
-    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(lens, 0, out=off[1:])
-    total = int(off[-1].item())
-    data = torch.randint(0x21, 0x7F, (total + 64,), dtype=torch.uint8, device=dev, generator=g)
-    return off, data, lens
+def make_dictionary(n, seed=2):
+    """Host-side synthetic dictionary in the HBM layout (uint64 offsets + bytes), lengths geometric(0.3)+7 -> [8, 63]."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lens = np.clip(rng.geometric(0.3, n) + 7, 8, 63).astype(np.uint64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = rng.integers(0x21, 0x7F, int(off[-1]) + 64, dtype=np.uint8)
+    return off, data
 
 
 def main():
     args = parse()
-    import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        # control plane only (barrier, max-over-ranks time, sum of PMKs): the data path shards the keyspace and
+        # never exchanges data, so there is no RCCL collective on the GPU.
+        dist.init_process_group("gloo")
 
     import dwpa_amd
     from dwpa_amd import synth as S
+    from dwpa_amd.device import Dictionary, Event, Stream
 
     n = args.dict_words
     plant = min(PLANT_INDEX, n - 1)
-    off, data, lens = make_dictionary(torch, n, dev)
-    b0, b1 = int(off[plant].item()), int(off[plant + 1].item())
-    psk = data[b0:b1].cpu().numpy().tobytes()
+    off, data = make_dictionary(n)
+    psk = data[int(off[plant]):int(off[plant + 1])].tobytes()
     import random
     rng = random.Random(1)
     essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
     line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rng)
 
+    d = Dictionary(off, data, device=local)
     B = (args.batch + 63) & ~63
     nbatches = (n + B - 1) // B
-    stream = torch.cuda.Stream(device=dev)
-    hs = stream.cuda_stream
+    stream = Stream(local)
+    hs = stream.handle
     sc = dwpa_amd.Scan([line], device=local, nc=NC, nc_mode=0, batch=B)
 
     def batch_range(i):
@@ -96,7 +95,7 @@ def main():
 
     def step(i, ev=None):
         first, cnt = batch_range(i)
-        sc.load_dict(off.data_ptr(), data.data_ptr(), first, cnt, 8, 63, hs)
+        sc.load_dict(d.off.ptr, d.data.ptr, first, cnt, 8, 63, hs)
         if ev is not None:
             ev[0].record(stream)
         sc.pbkdf2(0, hs)
@@ -105,16 +104,15 @@ def main():
         sc.verify(0, hs)
         return cnt
 
-    torch.cuda.synchronize()
     for w in range(args.warmup):
         step(rank + w * world)
     stream.synchronize()
     sc.hits(hs)  # drop warmup hits
 
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    kev = [(Event(local), Event(local)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    stream.synchronize()
     t0 = time.perf_counter()
     done = 0
     counts = []
@@ -122,38 +120,36 @@ def main():
         counts.append(step(rank + (args.warmup + s) * world, kev[s]))
         done += counts[-1]
     stream.synchronize()
-    torch.cuda.synchronize()
+    elapsed_local = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kms = [a.elapsed_time(b) for a, b in kev]
+    kms = [a.elapsed_ms(b) for a, b in kev]
     kernel_ms = sum(kms) / len(kms)
 
-    t = torch.tensor([elapsed, float(done)], dtype=torch.float64, device=dev)
     if world > 1:
-        tm = t[:1].clone()
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        td = t[1:].clone()
-        dist.all_reduce(td, op=dist.ReduceOp.SUM)
-        elapsed, total = float(tm.item()), float(td.item())
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        c = torch.tensor([float(done)], dtype=torch.float64)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        elapsed, total = float(t.item()), float(c.item())
     else:
         total = float(done)
 
     # correctness: the batch holding the planted PSK must report it with nc +3 LE and the right PMK (untimed)
-    pi = plant // B
-    step(pi)
+    step(plant // B)
     hits = sc.hits(hs)
     verified = any(h["cand"] == plant and h["nc"] == 3 and h["endian"] == "LE" and h["pmk"] == S.pmk(psk, essid)
                    for h in hits)
 
     pmk_per_launch = sum(counts) / len(counts)
     achieved = sum(counts) * COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION / (sum(kms) * 1e-3)
-    result = None
     if rank == 0:
         value = total / elapsed
         cpu = None
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(line, data, off, lens, plant, args.cpu_seconds)
+            cpu = cpu_baseline(line, data, off, plant, args.cpu_seconds)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -189,6 +185,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "hits_verified": bool(verified),
+            "rank0_local_s": round(elapsed_local, 4),
         }
         print(json.dumps(result), flush=True)
     sc.close()
@@ -199,22 +196,22 @@ def main():
         sys.exit(3)
 
 
-def cpu_baseline(line, data, off, lens, plant, seconds):
-    """The PHP CPU path: check_key_m22000(line, [word]) per word (one PHP request per key, as put_work does),
-    restated in C on OpenSSL (oracle/), on this host's cores; bounded sample ending at the planted PSK."""
+def cpu_baseline(line, data, off, plant, seconds):
+    """The PHP CPU path: check_key_m22000(line, [word]) per word (one PHP request per key, as put_work does,
+    common.php:902), restated in C on OpenSSL (oracle/), on this host's cores; bounded sample ending at the
+    planted PSK so the sample must also find it."""
     from oracle import oracle as O
     threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
 
     def words(lo, hi):
-        o = off[lo:hi + 1].cpu().tolist()
-        raw = data[o[0]:o[-1]].cpu().numpy().tobytes()
+        o = off[lo:hi + 1].astype("int64")
+        raw = data[o[0]:o[-1]].tobytes()
         return [raw[o[i] - o[0]:o[i + 1] - o[0]] for i in range(hi - lo)]
 
     probe = words(plant - 64 * threads + 1, plant + 1)
     t0 = time.perf_counter()
-    idx, res = O.c_check_many(line, probe, NC, threads)
-    dt = time.perf_counter() - t0
-    rate = len(probe) / dt
+    O.c_check_many(line, probe, NC, threads)
+    rate = len(probe) / (time.perf_counter() - t0)
     m = int(max(len(probe), min(400_000, rate * seconds)))
     sample = words(plant - m + 1, plant + 1)
     t0 = time.perf_counter()

@@ -79,6 +79,17 @@ SIGNATURES = {
     "dwpa_scan_hits": ([_P, ctypes.POINTER(Hit), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), _P], ctypes.c_int),
     "dwpa_scan_loaded": ([_P, ctypes.POINTER(ctypes.c_uint32), _P], ctypes.c_int),
     "dwpa_scan_destroy": ([_P], None),
+    "dwpa_dev_alloc": ([ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(_P)], ctypes.c_int),
+    "dwpa_dev_free": ([ctypes.c_int, _P], ctypes.c_int),
+    "dwpa_dev_upload": ([ctypes.c_int, _P, _P, ctypes.c_size_t], ctypes.c_int),
+    "dwpa_dev_download": ([ctypes.c_int, _P, _P, ctypes.c_size_t], ctypes.c_int),
+    "dwpa_stream_create": ([ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
+    "dwpa_stream_sync": ([_P], ctypes.c_int),
+    "dwpa_stream_destroy": ([_P], ctypes.c_int),
+    "dwpa_event_create": ([ctypes.c_int, ctypes.POINTER(_P)], ctypes.c_int),
+    "dwpa_event_record": ([_P, _P], ctypes.c_int),
+    "dwpa_event_elapsed_ms": ([_P, _P, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+    "dwpa_event_destroy": ([_P], ctypes.c_int),
 }
 
 _lib = None

@@ -705,4 +705,70 @@ int dwpa_scan_loaded(dwpa_scan* scan, uint32_t* count, void* hip_stream) {
 }
 void dwpa_scan_destroy(dwpa_scan* scan) { scan_destroy(scan); }
 
+static int set_dev(int device) {
+    RCHK(ensure_init());
+    if (device < 0 || device >= g_ndev) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(device));
+    return 0;
+}
+int dwpa_dev_alloc(int device, size_t bytes, void** out) {
+    if (!out) return DWPA_E_ARG;
+    RCHK(set_dev(device));
+    if (hipMalloc(out, bytes ? bytes : 16) != hipSuccess) return DWPA_E_NOMEM;
+    return 0;
+}
+int dwpa_dev_free(int device, void* p) {
+    RCHK(set_dev(device));
+    if (p) HIPCHK(hipFree(p));
+    return 0;
+}
+int dwpa_dev_upload(int device, void* dst, const void* src, size_t bytes) {
+    RCHK(set_dev(device));
+    if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+int dwpa_dev_download(int device, void* dst, const void* src, size_t bytes) {
+    RCHK(set_dev(device));
+    if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+int dwpa_stream_create(int device, void** out) {
+    if (!out) return DWPA_E_ARG;
+    RCHK(set_dev(device));
+    hipStream_t s;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = (void*)s;
+    return 0;
+}
+int dwpa_stream_sync(void* stream) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    return 0;
+}
+int dwpa_stream_destroy(void* stream) {
+    if (stream) HIPCHK(hipStreamDestroy((hipStream_t)stream));
+    return 0;
+}
+int dwpa_event_create(int device, void** out) {
+    if (!out) return DWPA_E_ARG;
+    RCHK(set_dev(device));
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    *out = (void*)e;
+    return 0;
+}
+int dwpa_event_record(void* event, void* stream) {
+    HIPCHK(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+    return 0;
+}
+int dwpa_event_elapsed_ms(void* start, void* stop, float* ms) {
+    if (!ms) return DWPA_E_ARG;
+    HIPCHK(hipEventSynchronize((hipEvent_t)stop));
+    HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+    return 0;
+}
+int dwpa_event_destroy(void* event) {
+    if (event) HIPCHK(hipEventDestroy((hipEvent_t)event));
+    return 0;
+}
+
 }  // extern "C"

@@ -127,6 +127,12 @@ int dwpa_hash_m22000(const char *line, size_t line_len, uint8_t out[16]);
 int dwpa_crack_files(const char *hash_file, const char *const *dicts, size_t ndicts, const char *rules_file,
                      int nonce_error_corrections, const char *out_file, const dwpa_config *cfg);
 
+/* GPU rule application (replaces `hashcat --stdout -r rules words`, help_crack.py:508,575): out holds
+ * nwords*nrules candidates of 256 bytes (word-major), out_len their lengths (0xFFFFFFFF = input rejected).
+ * With out == NULL only *nrules_out is set (number of rules that parse). */
+int dwpa_rules_expand(int device, const char *rules_text, size_t rules_len, const dwpa_bytes *words, size_t nwords,
+                      uint8_t *out, uint32_t *out_len, uint32_t *nrules_out);
+
 /* ---- device-resident scan API (inputs already in HBM; used by the client loop and bench.py) --------------- */
 typedef struct dwpa_scan dwpa_scan;
 /* Upload a work unit's hashlines (any number of ESSIDs) to `device` with a batch of `batch` candidate slots. */
@@ -150,6 +156,21 @@ int dwpa_scan_hits(dwpa_scan *scan, dwpa_hit *out, size_t cap, size_t *nhits, vo
 /* Candidate slots filled by the last load (synchronises). */
 int dwpa_scan_loaded(dwpa_scan *scan, uint32_t *count, void *hip_stream);
 void dwpa_scan_destroy(dwpa_scan *scan);
+
+/* ---- device plumbing for callers without their own HIP runtime (ctypes/PHP) ---------------------------------
+ * Buffers, streams and events of the runtime the kernels run on.  Callers that already hold HIP objects from a
+ * different HIP runtime instance (e.g. a framework bundling its own libamdhip64) must not pass them here. */
+int dwpa_dev_alloc(int device, size_t bytes, void **out);
+int dwpa_dev_free(int device, void *p);
+int dwpa_dev_upload(int device, void *dst, const void *src, size_t bytes);
+int dwpa_dev_download(int device, void *dst, const void *src, size_t bytes);
+int dwpa_stream_create(int device, void **out);
+int dwpa_stream_sync(void *stream);
+int dwpa_stream_destroy(void *stream);
+int dwpa_event_create(int device, void **out);
+int dwpa_event_record(void *event, void *stream);
+int dwpa_event_elapsed_ms(void *start, void *stop, float *ms); /* synchronises on stop */
+int dwpa_event_destroy(void *event);
 
 #ifdef __cplusplus
 }

@@ -98,7 +98,7 @@ def test_random_batch_vs_oracle():
 
 
 def test_scan_dictionary_hbm():
-    import torch
+    from dwpa_amd.device import Dictionary
     rng = random.Random(3)
     essid, ap, sta, an, sn = S.random_net(rng)
     words = [S.random_psk(rng, 8, 20) for _ in range(20000)]
@@ -108,17 +108,12 @@ def test_scan_dictionary_hbm():
     lines = [S.eapol_line(psk1, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rng),
              S.pmkid_line(psk2, essid, rng.randbytes(6), sta),
              S.eapol_line(words[5], b"other", ap, sta, an, sn, 3, -2, "BE", rng=rng)]
-    off = [0]
-    for w in words:
-        off.append(off[-1] + len(w))
-    dev = torch.device("cuda:0")
-    d_off = torch.tensor(off, dtype=torch.int64, device=dev)
-    d_bytes = torch.tensor(list(b"".join(words)) + [0] * 64, dtype=torch.uint8, device=dev)
+    d = Dictionary.from_words(words)
     sc = dwpa_amd.Scan(lines, nc=8, batch=8192)
     hits = []
     for first in range(0, len(words), 8192):
         cnt = min(8192, len(words) - first)
-        sc.load_dict(d_off.data_ptr(), d_bytes.data_ptr(), first, cnt)
+        sc.load_dict(d.off.ptr, d.data.ptr, first, cnt)
         for g in range(sc.groups):
             sc.pbkdf2(g)
             sc.verify(g)
@@ -196,4 +191,5 @@ def test_crack_files_rules_and_exhausted(tmp_path):
     assert rc == 1
     recs = out.read_bytes().strip().split(b"\n")
     assert len(recs) == 1
-    assert recs[0].endswith(b":" + psk)
+    plain = psk if all(0x20 <= c <= 0x7E and c != 0x3A for c in psk) else b"$HEX[" + psk.hex().encode() + b"]"
+    assert recs[0].endswith(b":" + plain)
