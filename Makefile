@@ -35,7 +35,11 @@ clean:
 
 .PHONY: all oracle clean asm
 
-tools: tools/bin/valu_peak
+tools: tools/bin/valu_peak tools/bin/pbkdf2_lab
+
+tools/bin/pbkdf2_lab: tools/pbkdf2_lab.hip dwpa_amd/csrc/crypto_dev.hpp
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 tools/bin/valu_peak: tools/valu_peak.hip
 	@mkdir -p tools/bin

@@ -1,0 +1,85 @@
+"""help_crack.py drop-in: run the m22000 attack in-process through libdwpa22000.so instead of a hashcat subprocess.
+
+Replaces ``HelpCrack.run_cracker`` (help_crack/help_crack.py:765-802) and the ``hashcat --stdout -r`` rule
+expansions (:508, :575) with the same inputs, outputs and return codes:
+
+* inputs   -- ``conf["hash_file"]`` (one m22000 line per hash, written by prepare_work :439-442),
+              ``conf["rules"]`` ("" or "-S -r <file>", :445-447 / :931-933), ``conf["key_file"]``, the dictionary
+              list (plain or .gz), ``conf["coptions"]`` (``-d 1,2`` selects devices like hashcat's ``-d``);
+* output   -- the ``-o`` key file in hashcat's m22000 outfile format, parsed unchanged by ``get_key`` (:804-879);
+* rc       -- hashcat semantics: 0 all cracked, 1 exhausted (drives the second pass at :930), -1 error.
+
+Usage from help_crack.py (the one-line change INTEGRATION.md shows)::
+
+    from dwpa_amd.help_crack import run_cracker as _gpu_run_cracker
+    HelpCrack.run_cracker = lambda self, dictlist, disablestdout=False: _gpu_run_cracker(self.conf, dictlist)
+"""
+from __future__ import annotations
+
+import gzip
+import os
+import shlex
+
+from . import m22000 as M
+from . import _lib as L
+
+NONCE_ERROR_CORRECTIONS = 8  # help_crack.py:773 passes --nonce-error-corrections=8
+
+
+def _parse_options(rules: str, coptions: str):
+    rules_file, devices = None, 0
+    toks = shlex.split(rules or "") + shlex.split(coptions or "")
+    i = 0
+    while i < len(toks):
+        t = toks[i]
+        if t in ("-r", "--rules-file") and i + 1 < len(toks):
+            rules_file = toks[i + 1]
+            i += 2
+            continue
+        if t.startswith("--rules-file="):
+            rules_file = t.split("=", 1)[1]
+        elif t in ("-d", "--backend-devices") and i + 1 < len(toks):
+            for d in toks[i + 1].split(","):
+                if d.strip().isdigit() and int(d) >= 1:
+                    devices |= 1 << (int(d) - 1)  # hashcat numbers devices from 1
+            i += 2
+            continue
+        i += 1
+    return rules_file, devices
+
+
+def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR_CORRECTIONS) -> int:
+    """In-process equivalent of the hashcat command line at help_crack.py:773; returns its exit code."""
+    if not os.path.exists(conf["hash_file"]):
+        return L.DWPA_RC_ERROR
+    rules_file, mask = _parse_options(conf.get("rules", ""), conf.get("coptions", ""))
+    return M.crack_files(conf["hash_file"], list(dictlist), rules_file, nonce_error_corrections, conf["key_file"],
+                         device_mask=mask)
+
+
+def expand_rules(rules_file: str, source: str, out_gz: str, chunk: int = 1 << 16) -> int:
+    """`hashcat --stdout -r rules_file source > out_gz` (help_crack.py:508) with the rules applied on the GPU.
+    Rejected words are skipped like hashcat does; returns the number of candidates written."""
+    with open(rules_file, "rb") as f:
+        rules_text = f.read()
+    written = 0
+    opener = gzip.open if source.endswith(".gz") else open
+    with opener(source, "rb") as src, gzip.open(out_gz, "wb") as dst:
+        batch = []
+
+        def flush():
+            nonlocal written
+            for row in M.rules_expand(rules_text, batch):
+                for cand in row:
+                    if cand is not None:
+                        dst.write(cand + b"\n")
+                        written += 1
+            batch.clear()
+
+        for line in src:
+            batch.append(line.rstrip(b"\r\n"))
+            if len(batch) >= chunk:
+                flush()
+        if batch:
+            flush()
+    return written
