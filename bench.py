@@ -25,13 +25,17 @@ METRIC = "PMK/s (PBKDF2-HMAC-SHA1 x4096) per GPU and per 8×MI355X node, m22000"
 DICT_WORDS = 100_000_000
 PLANT_INDEX = 99_999_000
 NC = 8
-# Algorithmic work per PMK: 16,388 SHA-1 compressions (north_star), each priced at the minimal gfx950 VALU
-# instruction count of the HMAC inner-loop compression (DESIGN.md "roofline"): 78 rounds x 5 + rounds 0-1 in
-# 3 (midstate invariants) + 176 schedule ops (constant-folded padding) + 5 digest adds + 2.5 for T ^= U.
+# Roofline.  Work unit: 16,388 SHA-1 compressions per PMK (north_star).  Bound: integer
+# VALU issue.  Measured on gfx950 (tools/valu_peak, profiles/r01/valu_issue_costs.json): xor/bitop3/add_u32 take
+# 2 SIMD cycles per wave64 instruction, alignbit (rotate) and add3 take 4, so the cheapest HMAC inner-loop
+# compression costs C_MIN = 1887 SIMD-cycles per wave (64 lanes).
 COMPRESSIONS_PER_PMK = 16388
+C_MIN_CYCLES = 1887
+SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
+# Nominal all-ops-full-rate view (128 int32 lane-ops/clk/CU, 576.5 ops/compression): reported, not attainable.
 OPS_PER_COMPRESSION = 576.5
-# gfx950: 256 CUs x 4 SIMD-32 (a wave64 VALU op issues over 2 cycles) = 128 int32 lane-ops / clk / CU, 2.4 GHz.
-PEAK_LANE_OPS = 256 * 128 * 2.4e9
+PEAK_LANE_OPS = 256 * 128 * CLOCK_HZ
 
 
 def parse():
@@ -72,6 +76,7 @@ def main():
     import dwpa_amd
     from dwpa_amd import synth as S
     from dwpa_amd.device import Dictionary, Event, Stream
+    from dwpa_amd.shard import batch_ids, reduce_timing
 
     n = args.dict_words
     plant = min(PLANT_INDEX, n - 1)
@@ -104,8 +109,8 @@ def main():
         sc.verify(0, hs)
         return cnt
 
-    for w in range(args.warmup):
-        step(rank + w * world)
+    for b in batch_ids(rank, world, 0, args.warmup, nbatches):
+        step(b)
     stream.synchronize()
     sc.hits(hs)  # drop warmup hits
 
@@ -116,8 +121,8 @@ def main():
     t0 = time.perf_counter()
     done = 0
     counts = []
-    for s in range(args.steps):
-        counts.append(step(rank + (args.warmup + s) * world, kev[s]))
+    for s, b in enumerate(batch_ids(rank, world, args.warmup, args.steps, nbatches)):
+        counts.append(step(b, kev[s]))
         done += counts[-1]
     stream.synchronize()
     elapsed_local = time.perf_counter() - t0
@@ -128,12 +133,7 @@ def main():
     kernel_ms = sum(kms) / len(kms)
 
     if world > 1:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        c = torch.tensor([float(done)], dtype=torch.float64)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        elapsed, total = float(t.item()), float(c.item())
+        elapsed, total = reduce_timing(dist, elapsed, done)
     else:
         total = float(done)
 
@@ -144,7 +144,8 @@ def main():
                    for h in hits)
 
     pmk_per_launch = sum(counts) / len(counts)
-    achieved = sum(counts) * COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION / (sum(kms) * 1e-3)
+    kernel_pmk_s = sum(counts) / (sum(kms) * 1e-3)
+    achieved = kernel_pmk_s * COMPRESSIONS_PER_PMK
     if rank == 0:
         value = total / elapsed
         cpu = None
@@ -173,15 +174,18 @@ def main():
             "roofline": {
                 "bound": "valu",
                 "kernel": "k_pbkdf2",
-                "achieved": round(achieved / 1e12, 3),
-                "peak": round(PEAK_LANE_OPS / 1e12, 3),
-                "unit": "TOP/s (int32 VALU lane-ops)",
-                "frac": round(achieved / PEAK_LANE_OPS, 4),
+                "achieved": round(achieved / 1e9, 3),
+                "peak": round(PEAK_COMPRESSIONS / 1e9, 3),
+                "unit": "G SHA-1 compressions/s",
+                "frac": round(achieved / PEAK_COMPRESSIONS, 4),
                 "traffic": None,
                 "kernel_ms": round(kernel_ms, 3),
                 "pmk_per_launch": pmk_per_launch,
-                "ops_per_pmk": COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION,
-                "roofline_pmk_per_s": round(PEAK_LANE_OPS / (COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION), 1),
+                "kernel_pmk_per_s": round(kernel_pmk_s, 1),
+                "roofline_pmk_per_s": round(PEAK_COMPRESSIONS / COMPRESSIONS_PER_PMK, 1),
+                "peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x 64 lanes / {C_MIN_CYCLES} SIMD-cycles per "
+                              "compression (measured gfx950 issue costs)",
+                "frac_nominal_ops": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION / PEAK_LANE_OPS, 4),
             },
             "cpu_baseline": cpu,
             "hits_verified": bool(verified),

@@ -1,0 +1,28 @@
+"""Static keyspace sharding shared by bench.py and the multi-rank tests.
+
+Every (ESSID, candidate) PMK is independent, so shards never exchange data: rank r of N scans batches
+r, r+N, r+2N, ... of the dictionary (weak scaling: fixed work per GPU per step), and crack_files splits every
+dictionary chunk into N contiguous equal ranges (dwpa_amd/csrc/crack.cpp).  The only cross-rank traffic is the
+bench's control plane: a barrier around the timed region, the max elapsed time and the total PMK count.
+"""
+from __future__ import annotations
+
+
+def batch_ids(rank: int, world: int, first_step: int, steps: int, nbatches: int):
+    """Dictionary batch index of each step of `rank` (step s -> batch (rank + s*world) mod nbatches)."""
+    return [(rank + s * world) % nbatches for s in range(first_step, first_step + steps)]
+
+
+def contiguous_shard(n: int, k: int, g: int):
+    """[b, e) of shard k of g over n items (same split as crack.cpp: W*k/G .. W*(k+1)/G)."""
+    return n * k // g, n * (k + 1) // g
+
+
+def reduce_timing(dist, elapsed: float, done: float):
+    """max elapsed and summed PMKs over ranks (gloo tensors on the CPU)."""
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([float(done)], dtype=torch.float64)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(c.item())
