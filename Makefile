@@ -35,7 +35,11 @@ clean:
 
 .PHONY: all oracle clean asm
 
-tools: tools/bin/valu_peak tools/bin/pbkdf2_lab
+tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat
+
+tools/bin/valu_lat: tools/valu_lat.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 tools/bin/pbkdf2_lab: tools/pbkdf2_lab.hip dwpa_amd/csrc/crypto_dev.hpp
 	@mkdir -p tools/bin
