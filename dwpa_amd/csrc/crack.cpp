@@ -244,27 +244,33 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     std::vector<std::string> dpaths;
     for (size_t i = 0; i < ndicts; i++) dpaths.push_back(dicts[i]);
     DictReader reader(dpaths);
-    Chunk chunk;
     bool ioerr = false;
     const size_t chunk_words = (size_t)batch * devs.size() * 8;
-    while (rc >= 0 && sh.ncracked < sh.valid && reader.next(chunk, chunk_words, (size_t)1 << 31, ioerr)) {
-        // retire lines cracked so far on every device
+    // double-buffered: the next chunk is read/inflated on a host thread while the devices scan this one
+    Chunk cur, nxt;
+    bool have = reader.next(cur, chunk_words, (size_t)1 << 31, ioerr);
+    while (rc >= 0 && have && sh.ncracked < sh.valid) {
+        bool have_next = false;
+        std::thread prefetch([&] { have_next = reader.next(nxt, chunk_words, (size_t)1 << 31, ioerr); });
         {
-            std::lock_guard<std::mutex> lk(sh.mu);
+            std::lock_guard<std::mutex> lk(sh.mu);  // retire lines cracked so far on every device
             for (size_t k = 0; k < work.size(); k++)
                 for (size_t i = 0; i < lines.size(); i++)
                     if (sh.cracked[i]) scan_mark_cracked(work[k].scan, (uint32_t)i);
         }
-        const size_t W = chunk.words(), G = work.size();
+        const size_t W = cur.words(), G = work.size();
         std::vector<std::thread> th;
         std::vector<int> rcs(G, 0);
         for (size_t k = 0; k < G; k++) {
             const size_t b = W * k / G, e = W * (k + 1) / G;
-            th.emplace_back([&, k, b, e] { rcs[k] = scan_shard(work[k], sh, chunk, b, e, rp, &drules[k]); });
+            th.emplace_back([&, k, b, e] { rcs[k] = scan_shard(work[k], sh, cur, b, e, rp, &drules[k]); });
         }
         for (auto& t : th) t.join();
+        prefetch.join();
         for (int r : rcs)
             if (r < 0) rc = r;
+        std::swap(cur, nxt);
+        have = have_next;
     }
     for (size_t k = 0; k < work.size(); k++) {
         if (work[k].scan) scan_destroy(work[k].scan);
