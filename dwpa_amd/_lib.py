@@ -44,6 +44,14 @@ class Config(ctypes.Structure):
                 ("nc_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
+class LineInfo(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("keyver", ctypes.c_int32), ("essid_len", ctypes.c_uint32),
+                ("mac_ap_len", ctypes.c_uint32), ("mac_sta_len", ctypes.c_uint32), ("target_len", ctypes.c_uint32),
+                ("attempts", ctypes.c_uint32), ("lists", ctypes.c_uint32), ("never_matches", ctypes.c_uint32),
+                ("essid", ctypes.c_uint8 * 32), ("mac_ap", ctypes.c_uint8 * 16), ("mac_sta", ctypes.c_uint8 * 16),
+                ("hash_m22000", ctypes.c_uint8 * 16)]
+
+
 class Hit(ctypes.Structure):
     _fields_ = [("cand", ctypes.c_uint64), ("line", ctypes.c_uint32), ("nc", ctypes.c_int32), ("endian", ctypes.c_int8),
                 ("nc_valid", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2), ("pmk", ctypes.c_uint8 * 32)]
@@ -63,6 +71,7 @@ SIGNATURES = {
     "dwpa_pbkdf2_pmk": ([ctypes.POINTER(Bytes), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),
     "dwpa_hc_unhex": ([ctypes.c_char_p, ctypes.c_size_t, _P, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dwpa_hash_m22000": ([ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),
+    "dwpa_parse_m22000": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "dwpa_crack_files": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
                           ctypes.c_char_p, ctypes.POINTER(Config)], ctypes.c_int),
     "dwpa_rules_expand": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Bytes), ctypes.c_size_t, _P, _P,

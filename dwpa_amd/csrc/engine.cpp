@@ -659,6 +659,30 @@ int dwpa_pbkdf2_pmk(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, 
     return pbkdf2_impl(keys, nkeys, essid, essid_len, pmks_out);
 }
 
+int dwpa_parse_m22000(const char* line, size_t line_len, int nc, int nc_mode, dwpa_line_info* out) {
+    if (!line || !out) return DWPA_E_ARG;
+    memset(out, 0, sizeof(*out));
+    ParsedLine p = parse_m22000(line, line_len);
+    if (p.status) return p.status;
+    TableBuilder tb;
+    const uint32_t li = tb.add_line(p, nc, nc_mode, nc);
+    const LineDev& L = tb.lines[li];
+    out->type = p.kind;
+    out->keyver = p.keyver;
+    out->essid_len = (uint32_t)p.essid.size();
+    out->mac_ap_len = (uint32_t)p.mac_ap.size();
+    out->mac_sta_len = (uint32_t)p.mac_sta.size();
+    out->target_len = (uint32_t)(p.kind == LINE_PMKID ? p.pmkid.size() : p.keymic.size());
+    out->attempts = p.kind == LINE_PMKID ? 1 : L.natt;
+    out->lists = p.kind == LINE_PMKID ? 1 : L.nlists;
+    out->never_matches = tb.never[li];
+    memcpy(out->essid, p.essid.data(), std::min<size_t>(32, p.essid.size()));
+    memcpy(out->mac_ap, p.mac_ap.data(), std::min<size_t>(16, p.mac_ap.size()));
+    memcpy(out->mac_sta, p.mac_sta.data(), std::min<size_t>(16, p.mac_sta.size()));
+    dwpa_hash_m22000(line, line_len, out->hash_m22000);
+    return 0;
+}
+
 int dwpa_hc_unhex(const uint8_t* in, size_t in_len, uint8_t* out, size_t* out_len) {
     if ((!in && in_len) || !out || !out_len) return DWPA_E_ARG;
     std::string r = hc_unhex(std::string((const char*)in, in_len));

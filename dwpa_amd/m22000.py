@@ -42,6 +42,33 @@ def hash_m22000(hashline):
     return out.raw
 
 
+def parse_m22000(hashline, nc: int = 128, nc_mode: int = L.DWPA_NC_PHP):
+    """Host-side parse (common.php:157-237 acceptance rules): dict of fields, or the negative parse code."""
+    h = _b(hashline)
+    info = L.LineInfo()
+    rc = L.load().dwpa_parse_m22000(h, len(h), int(nc), int(nc_mode), ctypes.byref(info))
+    if rc < 0:
+        return rc
+    return {"type": info.type, "keyver": info.keyver, "essid": bytes(info.essid[:min(32, info.essid_len)]),
+            "essid_len": info.essid_len, "mac_ap": bytes(info.mac_ap[:min(16, info.mac_ap_len)]),
+            "mac_sta": bytes(info.mac_sta[:min(16, info.mac_sta_len)]), "target_len": info.target_len,
+            "attempts": info.attempts, "lists": info.lists, "never_matches": bool(info.never_matches),
+            "hash_m22000": bytes(info.hash_m22000)}
+
+
+def group_by_essid(hashlines):
+    """Per-ESSID grouping of a work unit (get_work hands out one ESSID, web/content/get_work.php:96-109);
+    duplicate lines (same hash_m22000 key, common.php:310-315) are dropped.  Returns {essid: [lines]}."""
+    groups, seen = {}, set()
+    for line in hashlines:
+        p = parse_m22000(line)
+        if isinstance(p, int) or p["hash_m22000"] in seen:
+            continue
+        seen.add(p["hash_m22000"])
+        groups.setdefault(p["essid"] if p["essid_len"] <= 32 else _b(line).split(b"*")[5], []).append(_b(line))
+    return groups
+
+
 def _result(keys, r: L.Result):
     key = keys[r.key_index]
     key = _b(key)

@@ -116,6 +116,21 @@ int dwpa_pbkdf2_pmk(const dwpa_bytes *keys, size_t nkeys, const uint8_t *essid, 
                     uint8_t *pmks_out /* nkeys * 32 */);
 /* hashcat $HEX[...] decoding as web/common.php:3-25; *out_len <= in_len. */
 int dwpa_hc_unhex(const uint8_t *in, size_t in_len, uint8_t *out, size_t *out_len);
+/* Parse one hashline with check_key_m22000's acceptance rules (common.php:157-237) and describe the nonce-
+ * correction attempt lists the verifier would run for `nc` (host only, no device needed).  Returns 0 or the
+ * negative parse code.  essid is copied up to essid_cap bytes (essid_len holds the full length). */
+typedef struct {
+    int32_t type;              /* 1 PMKID, 2 EAPOL */
+    int32_t keyver;            /* EAPOL key version (0 if unknown) */
+    uint32_t essid_len, mac_ap_len, mac_sta_len, target_len;
+    uint32_t attempts;         /* attempts per key (1 + 4*((nc>>1)+1) in PHP mode) */
+    uint32_t lists;            /* distinct attempt lists (> 1 only when PHP's $n grows, short ANONCE) */
+    uint32_t never_matches;    /* PMKID/MIC shorter than 16 bytes */
+    uint8_t essid[32];
+    uint8_t mac_ap[16], mac_sta[16];
+    uint8_t hash_m22000[16];   /* common.php:310-315 dedupe key */
+} dwpa_line_info;
+int dwpa_parse_m22000(const char *line, size_t line_len, int nc, int nc_mode, dwpa_line_info *out);
 /* md5 over fields 1..7 (common.php:310-315); DWPA_E_FORMAT if the line has != 9 fields. */
 int dwpa_hash_m22000(const char *line, size_t line_len, uint8_t out[16]);
 
