@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--dict-words", type=int, default=DICT_WORDS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2",
+                    help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs")
+    ap.add_argument("--essids", type=int, default=8, help="c3: number of ESSIDs (BASELINE: 1000)")
     return ap.parse_args()
 
 
@@ -59,6 +62,129 @@ def make_dictionary(n, seed=2):
     np.cumsum(lens, out=off[1:])
     data = rng.integers(0x21, 0x7F, int(off[-1]) + 64, dtype=np.uint8)
     return off, data
+
+
+class Workload:
+    """One BASELINE.json config as a sequence of steps over HBM-resident candidates."""
+    name = ""
+    description = ""
+
+
+def build_c2(args, local, S, Scan, Dictionary):
+    """configs[1]: one ESSID, one EAPOL keyver-2 line, 100M-word dictionary."""
+    import random
+    w = Workload()
+    n = args.dict_words
+    w.plant = min(PLANT_INDEX, n - 1)
+    w.off, w.data = make_dictionary(n)
+    w.psk = w.data[int(w.off[w.plant]):int(w.off[w.plant + 1])].tobytes()
+    rng = random.Random(1)
+    w.essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
+    w.line = S.eapol_line(w.psk, w.essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rng)
+    w.dict = Dictionary(w.off, w.data, device=local)
+    w.B = (args.batch + 63) & ~63
+    w.nbatches = (n + w.B - 1) // w.B
+    w.scan = Scan([w.line], device=local, nc=NC, nc_mode=0, batch=w.B)
+    w.groups = 1
+    w.name = "C2"
+    w.description = ("C2: one ESSID, one EAPOL keyver-2 line (mp 0x80, planted NC +3 LE), 100M-word synthetic "
+                     "dictionary resident in HBM, PHP nonce window nc=8 (21 attempts)")
+    w.extra = {"dict_words": n}
+
+    def load(i, hs):
+        first = (i % w.nbatches) * w.B
+        cnt = min(w.B, n - first)
+        w.scan.load_dict(w.dict.off.ptr, w.dict.data.ptr, first, cnt, 8, 63, hs)
+        return cnt
+
+    def check(hits):
+        return any(h["cand"] == w.plant and h["nc"] == 3 and h["endian"] == "LE" and h["pmk"] == S.pmk(w.psk, w.essid)
+                   for h in hits)
+    w.load, w.check, w.plant_batch = load, check, w.plant // w.B
+    return w
+
+
+def build_c4(args, local, S, Scan, Dictionary):
+    """configs[3]: 8-digit numeric keyspace 00000000..99999999 generated in-kernel, one ESSID (PMKID line)."""
+    import random
+    w = Workload()
+    n = 10 ** 8
+    w.plant = 73019412
+    rng = random.Random(3)
+    w.essid, ap, sta, an, sn = S.random_net(rng, essid_len=8)
+    w.line = S.pmkid_line(b"%08d" % w.plant, w.essid, ap, sta)
+    w.B = (args.batch + 63) & ~63
+    w.nbatches = (n + w.B - 1) // w.B
+    w.scan = Scan([w.line], device=local, nc=NC, nc_mode=0, batch=w.B)
+    w.groups = 1
+    w.name = "C4"
+    w.description = "C4: 8-digit numeric keyspace (10^8) generated on the GPU, one ESSID, PMKID line"
+    w.extra = {"keyspace": n}
+
+    def load(i, hs):
+        first = (i % w.nbatches) * w.B
+        cnt = min(w.B, n - first)
+        w.scan.load_numeric(first, cnt, 8, hs)
+        return cnt
+
+    def check(hits):
+        return any(h["cand"] == w.plant and h["pmk"] == S.pmk(b"%08d" % w.plant, w.essid) for h in hits)
+    w.load, w.check, w.plant_batch = load, check, w.plant // w.B
+    return w
+
+
+def build_c3(args, local, S, Scan, Dictionary):
+    """configs[2]: 10k-word dictionary x WPA rule set amplified on the GPU, across E ESSIDs with 1-4 lines each;
+    each PMK is derived once per ESSID x candidate and tested against every line of that ESSID."""
+    import random
+    from dwpa_amd.rulesets import wpa_rules
+    from dwpa_amd.device import dictionary_arrays
+    import dwpa_amd
+    w = Workload()
+    rng = random.Random(4)
+    base = [S.random_psk(rng, 6, 12) for _ in range(10000)]
+    rules = wpa_rules()
+    picks = [(rng.randrange(len(base)), rng.randrange(len(rules))) for _ in range(4 * args.essids)]
+    expanded = dwpa_amd.rules_expand("\n".join(rules), [base[wi] for wi, _ in picks], device=local)
+    w.off, w.data = dictionary_arrays(base)
+    w.dict = Dictionary(w.off, w.data, device=local)
+    lines, w.plants = [], []
+    for e in range(args.essids):
+        essid, ap, sta, an, sn = S.random_net(rng)
+        for k in range(rng.randint(1, 4)):
+            wi, ri = picks[4 * e + k]
+            psk = expanded[4 * e + k][ri]
+            if not psk or not 8 <= len(psk) <= 63:
+                psk = b"not-in-keyspace-%d" % k
+            elif e == 0 and k == 0:
+                w.plants.append((len(lines), wi * len(rules) + ri, essid, psk))
+            if k % 2:
+                lines.append(S.pmkid_line(psk, essid, rng.randbytes(6), sta))
+            else:
+                lines.append(S.eapol_line(psk, essid, ap, sta, an, sn, 2, rng.randint(-3, 3), "LE", rng=rng))
+    w.B = (args.batch + 63) & ~63
+    w.scan = Scan(lines, device=local, nc=NC, nc_mode=0, batch=w.B)
+    w.nrules = w.scan.set_rules("\n".join(rules))
+    w.words_per_step = max(1, w.B // w.nrules)
+    w.nbatches = (len(base) + w.words_per_step - 1) // w.words_per_step
+    w.groups = w.scan.groups
+    w.name = "C3"
+    w.description = (f"C3: 10k-word dictionary x {w.nrules} WPA rules amplified on the GPU (8..63 filter), "
+                     f"{w.groups} ESSIDs x 1-4 lines, one PMK per ESSID x candidate")
+    w.extra = {"essids": w.groups, "lines": len(lines), "rules": w.nrules}
+
+    def load(i, hs):
+        first = (i % w.nbatches) * w.words_per_step
+        nw = min(w.words_per_step, len(base) - first)
+        w.scan.load_rules(w.dict.off.ptr, w.dict.data.ptr, first, nw, hs)
+        return w.scan.loaded(hs) * w.groups
+
+    def check(hits):
+        return all(any(h["line"] == li and h["pmk"] == S.pmk(psk, essid) for h in hits)
+                   for li, cand, essid, psk in w.plants)
+    w.load, w.check = load, check
+    w.plant_batch = (w.plants[0][1] // w.nrules) // w.words_per_step if w.plants else 0
+    return w
 
 
 def main():
@@ -78,38 +204,24 @@ def main():
     from dwpa_amd.device import Dictionary, Event, Stream
     from dwpa_amd.shard import batch_ids, reduce_timing
 
-    n = args.dict_words
-    plant = min(PLANT_INDEX, n - 1)
-    off, data = make_dictionary(n)
-    psk = data[int(off[plant]):int(off[plant + 1])].tobytes()
-    import random
-    rng = random.Random(1)
-    essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
-    line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rng)
-
-    d = Dictionary(off, data, device=local)
-    B = (args.batch + 63) & ~63
-    nbatches = (n + B - 1) // B
+    build = {"c2": build_c2, "c3": build_c3, "c4": build_c4}[args.workload]
+    w = build(args, local, S, dwpa_amd.Scan, Dictionary)
     stream = Stream(local)
     hs = stream.handle
-    sc = dwpa_amd.Scan([line], device=local, nc=NC, nc_mode=0, batch=B)
-
-    def batch_range(i):
-        first = (i % nbatches) * B
-        return first, min(B, n - first)
+    sc = w.scan
 
     def step(i, ev=None):
-        first, cnt = batch_range(i)
-        sc.load_dict(d.off.ptr, d.data.ptr, first, cnt, 8, 63, hs)
-        if ev is not None:
-            ev[0].record(stream)
-        sc.pbkdf2(0, hs)
-        if ev is not None:
-            ev[1].record(stream)
-        sc.verify(0, hs)
+        cnt = w.load(i, hs)
+        for g in range(w.groups):
+            if ev is not None and g == 0:
+                ev[0].record(stream)
+            sc.pbkdf2(g, hs)
+            if ev is not None and g == 0:
+                ev[1].record(stream)
+            sc.verify(g, hs)
         return cnt
 
-    for b in batch_ids(rank, world, 0, args.warmup, nbatches):
+    for b in batch_ids(rank, world, 0, args.warmup, w.nbatches):
         step(b)
     stream.synchronize()
     sc.hits(hs)  # drop warmup hits
@@ -121,7 +233,7 @@ def main():
     t0 = time.perf_counter()
     done = 0
     counts = []
-    for s, b in enumerate(batch_ids(rank, world, args.warmup, args.steps, nbatches)):
+    for s, b in enumerate(batch_ids(rank, world, args.warmup, args.steps, w.nbatches)):
         counts.append(step(b, kev[s]))
         done += counts[-1]
     stream.synchronize()
@@ -137,20 +249,19 @@ def main():
     else:
         total = float(done)
 
-    # correctness: the batch holding the planted PSK must report it with nc +3 LE and the right PMK (untimed)
-    step(plant // B)
-    hits = sc.hits(hs)
-    verified = any(h["cand"] == plant and h["nc"] == 3 and h["endian"] == "LE" and h["pmk"] == S.pmk(psk, essid)
-                   for h in hits)
+    # correctness: the batch holding the planted PSK(s) must report them (untimed)
+    step(w.plant_batch)
+    verified = bool(w.check(sc.hits(hs)))
 
-    pmk_per_launch = sum(counts) / len(counts)
-    kernel_pmk_s = sum(counts) / (sum(kms) * 1e-3)
+    per_launch = [c / w.groups for c in counts]
+    pmk_per_launch = sum(per_launch) / len(per_launch)
+    kernel_pmk_s = sum(per_launch) / (sum(kms) * 1e-3)
     achieved = kernel_pmk_s * COMPRESSIONS_PER_PMK
     if rank == 0:
         value = total / elapsed
         cpu = None
-        if not args.no_cpu_baseline:
-            cpu = cpu_baseline(line, data, off, plant, args.cpu_seconds)
+        if not args.no_cpu_baseline and args.workload == "c2":
+            cpu = cpu_baseline(w.line, w.data, w.off, w.plant, args.cpu_seconds)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -164,13 +275,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
-            "config": {
-                "workload": "C2: one ESSID, one EAPOL keyver-2 line (mp 0x80, planted NC +3 LE), 100M-word "
-                            "synthetic dictionary resident in HBM, PHP nonce window nc=8 (21 attempts)",
-                "dict_words": n,
-                "batch_per_step": B,
-                "parallelism": f"keyspace shards x{world}, no collective on the data path",
-            },
+            "config": dict({"workload": w.description, "batch_per_step": w.B,
+                            "parallelism": f"keyspace shards x{world}, no collective on the data path"}, **w.extra),
             "roofline": {
                 "bound": "valu",
                 "kernel": "k_pbkdf2",
@@ -188,7 +294,7 @@ def main():
                 "frac_nominal_ops": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION / PEAK_LANE_OPS, 4),
             },
             "cpu_baseline": cpu,
-            "hits_verified": bool(verified),
+            "hits_verified": verified,
             "rank0_local_s": round(elapsed_local, 4),
         }
         print(json.dumps(result), flush=True)

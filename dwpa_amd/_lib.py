@@ -82,6 +82,8 @@ SIGNATURES = {
     "dwpa_scan_line_status": ([_P, ctypes.c_size_t], ctypes.c_int),
     "dwpa_scan_load_dict": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _P],
                             ctypes.c_int),
+    "dwpa_scan_set_rules": ([_P, ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
+    "dwpa_scan_load_rules": ([_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, _P], ctypes.c_int),
     "dwpa_scan_load_numeric": ([_P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P], ctypes.c_int),
     "dwpa_scan_pbkdf2": ([_P, ctypes.c_int, _P], ctypes.c_int),
     "dwpa_scan_verify": ([_P, ctypes.c_int, _P], ctypes.c_int),

@@ -475,6 +475,7 @@ int scan_create(int device, const char* const* lines, const size_t* lens, size_t
 
 void scan_destroy(dwpa_scan* sc) {
     if (!sc) return;
+    scan_rules_drop(sc);
     hipSetDevice(sc->device);
     hipDeviceSynchronize();
     sc->lines.release(); sc->atts.release(); sc->pool.release(); sc->salt.release(); sc->segs.release();
@@ -572,6 +573,7 @@ void scan_mark_cracked(dwpa_scan* sc, uint32_t input_line) {
 }
 uint32_t scan_batch_cap(const dwpa_scan* sc) { return sc->batch_cap; }
 Batch& scan_batch_ref(dwpa_scan* sc) { return sc->batch; }
+int scan_device(const dwpa_scan* sc) { return sc->device; }
 
 // ---------------------------------------------------------------------------------------------------------
 // helpers for crack.cpp

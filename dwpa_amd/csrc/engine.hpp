@@ -44,5 +44,7 @@ void hit_to_public(const dwpa_scan* sc, const HitDev& h, dwpa_hit& o);
 void scan_mark_cracked(dwpa_scan* sc, uint32_t input_line);
 uint32_t scan_batch_cap(const dwpa_scan* sc);
 Batch& scan_batch_ref(dwpa_scan* sc);
+int scan_device(const dwpa_scan* sc);
+void scan_rules_drop(const dwpa_scan* scan);
 
 }  // namespace dwpa

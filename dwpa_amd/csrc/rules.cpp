@@ -7,6 +7,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <memory>
+#include <mutex>
 
 #include "engine.hpp"
 
@@ -183,7 +186,59 @@ void rules_release(DevRules* r) {
     r->device = -1;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// scan-level rules (device-resident candidates x rules)
+// ---------------------------------------------------------------------------------------------------------
+struct ScanRules {
+    RuleSet set;
+    DevRules dev;
+};
+static std::mutex g_rules_mu;
+static std::map<const dwpa_scan*, std::unique_ptr<ScanRules>> g_scan_rules;
+
+void scan_rules_drop(const dwpa_scan* scan) {
+    std::lock_guard<std::mutex> lk(g_rules_mu);
+    auto it = g_scan_rules.find(scan);
+    if (it != g_scan_rules.end()) {
+        rules_release(&it->second->dev);
+        g_scan_rules.erase(it);
+    }
+}
+
 }  // namespace dwpa
+
+extern "C" int dwpa_scan_set_rules(dwpa_scan* scan, const char* rules_text, size_t rules_len) {
+    using namespace dwpa;
+    if (!scan || (!rules_text && rules_len)) return DWPA_E_ARG;
+    scan_rules_drop(scan);
+    auto sr = std::make_unique<ScanRules>();
+    std::string cur;
+    for (size_t i = 0; i < rules_len; i++) {
+        if (rules_text[i] == '\n') { sr->set.add_line(cur); cur.clear(); }
+        else cur.push_back(rules_text[i]);
+    }
+    if (!cur.empty()) sr->set.add_line(cur);
+    if (sr->set.size() == 0) return DWPA_E_RULE;
+    int rc = rules_upload(scan_device(scan), sr->set, &sr->dev);
+    if (rc < 0) return rc;
+    const int n = (int)sr->set.size();
+    std::lock_guard<std::mutex> lk(g_rules_mu);
+    g_scan_rules[scan] = std::move(sr);
+    return n;
+}
+
+extern "C" int dwpa_scan_load_rules(dwpa_scan* scan, const uint64_t* d_offsets, const uint8_t* d_bytes,
+                                    uint64_t first_word, uint32_t nwords, void* hip_stream) {
+    using namespace dwpa;
+    ScanRules* sr = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_rules_mu);
+        auto it = g_scan_rules.find(scan);
+        if (it != g_scan_rules.end()) sr = it->second.get();
+    }
+    if (!sr) return DWPA_E_RULE;
+    return rules_load(scan, &sr->dev, d_offsets, d_bytes, first_word, nwords, (hipStream_t)hip_stream);
+}
 
 // ---------------------------------------------------------------------------------------------------------
 // C ABI: rule expansion on the GPU (replaces `hashcat --stdout -r rules` in help_crack.py:508,575)

@@ -201,6 +201,15 @@ class Scan:
         L.check(self._lib.dwpa_scan_load_dict(self._h, d_offsets, d_bytes, first, count, minlen, maxlen, stream),
                 "scan_load_dict")
 
+    def set_rules(self, rules_text) -> int:
+        t = _b(rules_text)
+        self.nrules = L.check(self._lib.dwpa_scan_set_rules(self._h, t, len(t)), "scan_set_rules")
+        return self.nrules
+
+    def load_rules(self, d_offsets: int, d_bytes: int, first_word: int, nwords: int, stream: int = 0):
+        L.check(self._lib.dwpa_scan_load_rules(self._h, d_offsets, d_bytes, first_word, nwords, stream),
+                "scan_load_rules")
+
     def load_numeric(self, first: int, count: int, digits: int = 8, stream: int = 0):
         L.check(self._lib.dwpa_scan_load_numeric(self._h, first, count, digits, stream), "scan_load_numeric")
 

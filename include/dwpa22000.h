@@ -160,6 +160,12 @@ int dwpa_scan_line_status(const dwpa_scan *scan, size_t line); /* 0 usable, or t
  * (hashcat m22000 accepts 8..63).  count <= batch. */
 int dwpa_scan_load_dict(dwpa_scan *scan, const uint64_t *d_offsets, const uint8_t *d_bytes, uint64_t first,
                         uint32_t count, uint32_t minlen, uint32_t maxlen, void *hip_stream);
+/* Rule amplification on the GPU: set the scan's rules once (hashcat rule syntax, one per line), then load
+ * words [first_word, first_word+nwords) x every rule; candidate id = word * nrules + rule, 8..63 filter applied.
+ * nwords * nrules must be <= batch.  Returns the number of rules that parsed (set) or 0 (load). */
+int dwpa_scan_set_rules(dwpa_scan *scan, const char *rules_text, size_t rules_len);
+int dwpa_scan_load_rules(dwpa_scan *scan, const uint64_t *d_offsets, const uint8_t *d_bytes, uint64_t first_word,
+                         uint32_t nwords, void *hip_stream);
 /* Decimal keyspace first..first+count-1, zero-padded to `digits` characters. */
 int dwpa_scan_load_numeric(dwpa_scan *scan, uint64_t first, uint32_t count, uint32_t digits, void *hip_stream);
 /* Stages 2 and 3 for ESSID group g (PMKs of the loaded batch, then every uncracked line of that ESSID). */

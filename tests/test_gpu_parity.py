@@ -193,3 +193,35 @@ def test_crack_files_rules_and_exhausted(tmp_path):
     assert len(recs) == 1
     plain = psk if all(0x20 <= c <= 0x7E and c != 0x3A for c in psk) else b"$HEX[" + psk.hex().encode() + b"]"
     assert recs[0].endswith(b":" + plain)
+
+
+def test_scan_rules_device_resident():
+    """configs[2] shape: words x rules amplified on the GPU, several ESSIDs, hits with word*nrules+rule ids."""
+    from dwpa_amd.device import Dictionary
+    rng = random.Random(8)
+    base = [S.random_psk(rng, 5, 12) for _ in range(2000)]
+    rules = wpa_rules()
+    d = Dictionary.from_words(base)
+    nets = [S.random_net(rng) for _ in range(3)]
+    plants = [(17, rules.index("$2 $0 $2 $4")), (1999, rules.index("u $1")), (500, rules.index("^e ^h ^t"))]
+    lines = []
+    for (wi, ri), (essid, ap, sta, an, sn) in zip(plants, nets):
+        psk = R.apply(R.parse(rules[ri]), base[wi])
+        lines.append(S.eapol_line(psk, essid, ap, sta, an, sn, 2, -1, "BE", rng=rng))
+    sc = dwpa_amd.Scan(lines, nc=8, batch=1 << 18)
+    assert sc.set_rules("\n".join(rules)) == len(rules)
+    per = (1 << 18) // len(rules)
+    hits = []
+    for first in range(0, len(base), per):
+        sc.load_rules(d.off.ptr, d.data.ptr, first, min(per, len(base) - first))
+        for g in range(sc.groups):
+            sc.pbkdf2(g)
+            sc.verify(g)
+        hits += sc.hits()
+    got = {(h["line"], h["nc"], h["endian"]) for h in hits}
+    assert got == {(0, -1, "BE"), (1, -1, "BE"), (2, -1, "BE")}
+    for h in hits:
+        wi, ri = divmod(h["cand"], len(rules))
+        essid = nets[h["line"]][0]
+        assert h["pmk"] == S.pmk(R.apply(R.parse(rules[ri]), base[wi]), essid)
+    sc.close()
