@@ -235,7 +235,7 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     int rc = 0;
     for (size_t k = 0; k < devs.size() && rc >= 0; k++) {
         work[k].device = devs[k];
-        hipSetDevice(devs[k]);
+        (void)hipSetDevice(devs[k]);
         if (hipStreamCreateWithFlags(&work[k].stream, hipStreamNonBlocking) != hipSuccess) rc = DWPA_E_HIP;
         if (rc >= 0) rc = scan_create(devs[k], lp.data(), ll.data(), lines.size(), nec, nc_mode, batch, &work[k].scan);
         if (rc >= 0 && rp) rc = rules_upload(devs[k], rules, &drules[k]);
@@ -274,11 +274,11 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     }
     for (size_t k = 0; k < work.size(); k++) {
         if (work[k].scan) scan_destroy(work[k].scan);
-        hipSetDevice(work[k].device);
+        (void)hipSetDevice(work[k].device);
         work[k].off.release();
         work[k].bytes.release();
         rules_release(&drules[k]);
-        if (work[k].stream) hipStreamDestroy(work[k].stream);
+        if (work[k].stream) (void)hipStreamDestroy(work[k].stream);
     }
     fclose(sh.out);
     if (rc < 0 || ioerr) return DWPA_RC_ERROR;

@@ -41,7 +41,7 @@ static thread_local hipError_t t_last_hip = hipSuccess;
 
 int DevBuf::ensure(size_t bytes) {
     if (n >= bytes && p) return 0;
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
     if (bytes == 0) bytes = 16;
@@ -50,7 +50,7 @@ int DevBuf::ensure(size_t bytes) {
     return 0;
 }
 void DevBuf::release() {
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
 }
@@ -476,8 +476,8 @@ int scan_create(int device, const char* const* lines, const size_t* lens, size_t
 void scan_destroy(dwpa_scan* sc) {
     if (!sc) return;
     scan_rules_drop(sc);
-    hipSetDevice(sc->device);
-    hipDeviceSynchronize();
+    (void)hipSetDevice(sc->device);
+    (void)hipDeviceSynchronize();
     sc->lines.release(); sc->atts.release(); sc->pool.release(); sc->salt.release(); sc->segs.release();
     sc->batch.mid.release(); sc->batch.pmk.release(); sc->batch.ids.release(); sc->batch.hits.release();
     sc->batch.counters.release();
@@ -627,13 +627,13 @@ void dwpa_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     for (auto& d : g_dev) {
         std::lock_guard<std::mutex> dl(d->mu);
-        hipSetDevice(d->id);
-        hipDeviceSynchronize();
+        (void)hipSetDevice(d->id);
+        (void)hipDeviceSynchronize();
         for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->salt, &d->koff, &d->kbytes, &d->idsup,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();
         d->batch.cap = d->batch.hitcap = 0;
-        if (d->stream) hipStreamDestroy(d->stream);
+        if (d->stream) (void)hipStreamDestroy(d->stream);
         d->stream = nullptr;
     }
     g_dev.clear();

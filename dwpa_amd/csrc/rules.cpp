@@ -179,9 +179,9 @@ int rules_load(dwpa_scan* scan, const DevRules* r, const uint64_t* off, const ui
 
 void rules_release(DevRules* r) {
     if (!r || r->device < 0) return;
-    hipSetDevice(r->device);
-    if (r->offs) hipFree(r->offs);
-    if (r->code) hipFree(r->code);
+    (void)hipSetDevice(r->device);
+    if (r->offs) (void)hipFree(r->offs);
+    if (r->code) (void)hipFree(r->code);
     r->offs = r->code = nullptr;
     r->device = -1;
 }
@@ -287,7 +287,7 @@ extern "C" int dwpa_rules_expand(int device, const char* rules_text, size_t rule
     if (!rc && (hipMemcpy(out, d_out, ncand * 256, hipMemcpyDeviceToHost) ||
                 hipMemcpy(out_len, d_len, ncand * 4, hipMemcpyDeviceToHost)))
         rc = DWPA_E_HIP;
-    hipFree(d_off); hipFree(d_bytes); hipFree(d_out); hipFree(d_len);
+    (void)hipFree(d_off); (void)hipFree(d_bytes); (void)hipFree(d_out); (void)hipFree(d_len);
     rules_release(&dr);
     return rc;
 }
