@@ -6,7 +6,10 @@ SRC := dwpa_amd/csrc
 OBJ := build/obj
 LIB := dwpa_amd/lib/libdwpa22000.so
 HDRS := $(wildcard $(SRC)/*.hpp) include/dwpa22000.h
-OBJS := $(OBJ)/kernels.o $(OBJ)/rules_dev.o $(OBJ)/engine.o $(OBJ)/m22000_host.o $(OBJ)/crack.o $(OBJ)/rules.o
+OBJS := $(OBJ)/kernels.o $(OBJ)/rules_dev.o $(OBJ)/engine.o $(OBJ)/m22000_host.o $(OBJ)/crack.o $(OBJ)/rules.o \
+        $(OBJ)/pbkdf2_module.o $(OBJ)/pbkdf2_hsaco.o
+LLVM := /opt/rocm/lib/llvm/bin
+ISSUE_RULE ?= before_half
 
 all: $(LIB) oracle
 
@@ -17,6 +20,25 @@ $(OBJ)/%.o: $(SRC)/%.hip $(HDRS)
 $(OBJ)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) --offload-arch=$(ARCH) $(CXXFLAGS) -Iinclude -c $< -o $@
+
+# product PBKDF2 kernel: hipcc -> gfx950 asm -> VALU issue pass -> code object -> embedded byte array
+build/pbkdf2/pbkdf2_gfx950.s: $(SRC)/pbkdf2_gfx950.hip $(SRC)/pbkdf2_dev.hpp $(SRC)/crypto_dev.hpp
+	@mkdir -p build/pbkdf2
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 --cuda-device-only -S $< -o $@
+
+build/pbkdf2/pbkdf2_issue.s: build/pbkdf2/pbkdf2_gfx950.s $(SRC)/gen/issue_pass.py
+	python3 $(SRC)/gen/issue_pass.py $< $@ k_pbkdf2_gfx950 $(ISSUE_RULE)
+
+build/pbkdf2/pbkdf2_gfx950.hsaco: build/pbkdf2/pbkdf2_issue.s
+	$(LLVM)/clang -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c $< -o build/pbkdf2/pbkdf2_issue.o
+	$(LLVM)/ld.lld -shared build/pbkdf2/pbkdf2_issue.o -o $@
+
+build/pbkdf2/pbkdf2_hsaco.cpp: build/pbkdf2/pbkdf2_gfx950.hsaco $(SRC)/gen/embed.py
+	python3 $(SRC)/gen/embed.py $< $@ pbkdf2_gfx950_hsaco
+
+$(OBJ)/pbkdf2_hsaco.o: build/pbkdf2/pbkdf2_hsaco.cpp
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
 	@mkdir -p dwpa_amd/lib

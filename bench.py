@@ -295,6 +295,8 @@ def main():
             },
             "cpu_baseline": cpu,
             "hits_verified": verified,
+            "pbkdf2_kernel": "k_pbkdf2 (hipcc schedule)" if os.environ.get("DWPA_PBKDF2_PLAIN", "0") not in ("", "0")
+                             else "k_pbkdf2_gfx950 (gfx950 VALU issue pass)",
             "rank0_local_s": round(elapsed_local, 4),
         }
         print(json.dumps(result), flush=True)

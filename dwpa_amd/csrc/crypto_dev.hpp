@@ -137,7 +137,15 @@ __device__ __forceinline__ uint32_t sched84(const uint32_t w[16]) {
     }
 }
 
-template <int T>
+// Issue-slot spacer.  On gfx950 a wave whose VALU stream mixes 4-cycle ops (alignbit, add3) with 2-cycle ops
+// (xor, bitop3, add) issues every VALU at the 4-cycle rate; a scalar s_nop between them restores near-additive
+// issue (tools/valu_mix*, profiles/).  NOP selects where spacers go in the SHA-1 rounds (0 = none).
+template <int NOP, int WHERE>
+__device__ __forceinline__ void spacer() {
+    if constexpr ((NOP & WHERE) != 0) asm volatile("s_nop 0");
+}
+
+template <int T, int NOP = 0>
 __device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[16]) {
     uint32_t f;
     if constexpr (T < 20) f = DWPA_SHA1_CH(b, c, d);
@@ -152,28 +160,32 @@ __device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, ui
         if constexpr (T < 16) wt = w[T];
         else {
             wt = rotl(sched84<T>(w), 1);
+            spacer<NOP, 1>();
             w[T & 15] = wt;
         }
         t = rotl(a, 5) + f + e + sha1_k<T>() + wt;
     }
+    spacer<NOP, 2>();
     e = d; d = c; c = rotl(b, 30); b = a; a = t;
+    spacer<NOP, 4>();
 }
 
-template <int T0, int... Ts>
+template <int NOP, int T0, int... Ts>
 __device__ __forceinline__ void steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[16],
                                         std::integer_sequence<int, T0, Ts...>) {
-    step84<T0>(a, b, c, d, e, w);
-    if constexpr (sizeof...(Ts) > 0) steps84(a, b, c, d, e, w, std::integer_sequence<int, Ts...>{});
+    step84<T0, NOP>(a, b, c, d, e, w);
+    if constexpr (sizeof...(Ts) > 0) steps84<NOP>(a, b, c, d, e, w, std::integer_sequence<int, Ts...>{});
 }
-template <int Lo, int... Is>
+template <int Lo, int NOP, int... Is>
 __device__ __forceinline__ void run_steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
                                             uint32_t w[16], std::integer_sequence<int, Is...>) {
-    steps84(a, b, c, d, e, w, std::integer_sequence<int, (Lo + Is)...>{});
+    steps84<NOP>(a, b, c, d, e, w, std::integer_sequence<int, (Lo + Is)...>{});
 }
 
 // out <- SHA1_compress(M, in[0..4] || 0x80 || 0.. || bitlen(64+20)): the PBKDF2/HMAC inner-loop compression
 // (a 20-byte digest hashed after a 64-byte key pad block).  Rounds 0-1 come from the folded midstate invariants,
 // rounds 2-79 use the constant-folded message schedule above.
+template <int NOP = 0>
 __device__ __forceinline__ void sha1_84(const Sha1Mid& M, const uint32_t in[5], uint32_t out[5]) {
     uint32_t w[16];
     w[0] = in[0]; w[1] = in[1]; w[2] = in[2]; w[3] = in[3]; w[4] = in[4];
@@ -182,7 +194,7 @@ __device__ __forceinline__ void sha1_84(const Sha1Mid& M, const uint32_t in[5], 
     uint32_t a1 = M.c0 + w[0];
     uint32_t a2 = rotl(a1, 5) + M.c1 + w[1];
     uint32_t a = a2, b = a1, c = M.r0, d = M.r1, e = M.h2;
-    run_steps84<2>(a, b, c, d, e, w, std::make_integer_sequence<int, 78>{});
+    run_steps84<2, NOP>(a, b, c, d, e, w, std::make_integer_sequence<int, 78>{});
     out[0] = M.h0 + a; out[1] = M.h1 + b; out[2] = M.h2 + c; out[3] = M.h3 + d; out[4] = M.h4 + e;
 }
 

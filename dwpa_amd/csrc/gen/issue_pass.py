@@ -1,0 +1,91 @@
+"""gfx950 VALU issue pass: insert s_nop spacers into the main (4096-iteration) loop of a device assembly file.
+
+Why (measured on MI355X, tools/valu_mix*, tools/asm/asm_lab, profiles/r01/): a wave64 VALU stream that mixes 4-cycle
+ops (v_alignbit_b32, v_add3_u32, v_xad_u32, ...) with 2-cycle ops (v_xor_b32, v_bitop3_b32, v_add_u32) issues
+EVERY instruction at the 4-cycle rate, even with 8 waves per SIMD; homogeneous streams run at 2 / 4 cycles.  A
+scalar `s_nop 0` in front of each 4-cycle op restores near-additive issue: the PBKDF2 loop goes from 3.9 to ~3.4
+SIMD-cycles per VALU instruction (+15.7 % PMK/s) with the instruction stream otherwise unchanged.  Source-level
+`asm volatile("s_nop 0")` cannot do this -- LLVM hoists the register-only VALU ops over it -- hence the pass on
+the compiler's assembly.  The default rule for the product kernel is `before_half`.
+
+Rules (comma-separated, applied in the loop body only):
+  after_half      s_nop after every 4-cycle VALU (alignbit, add3, xad, bfi, ...)
+  after_full_h    s_nop after a 2-cycle VALU that follows a 4-cycle VALU
+  before_half     s_nop before every 4-cycle VALU
+  every=K         s_nop after every K-th VALU
+  after_alb       s_nop after every v_alignbit_b32
+  before_half_trans  s_nop before a 4-cycle VALU that follows a 2-cycle VALU
+  before_alb / before_ad3  s_nop before every alignbit / add3
+  before_full_trans  s_nop before a 2-cycle VALU that follows a 4-cycle VALU
+  nop1            use s_nop 1 instead of s_nop 0
+  none            copy through
+"""
+import re
+import sys
+
+HALF = ("v_alignbit_b32", "v_add3_u32", "v_xad_u32", "v_bfi_b32", "v_lshl_add_u32", "v_lshl_or_b32",
+        "v_lshlrev_b32", "v_perm_b32", "v_or3_b32", "v_and_or_b32", "v_add_co_u32", "v_alignbyte_b32")
+
+
+def main_loop_range(lines, kernel):
+    start = next(i for i, l in enumerate(lines) if l.startswith(kernel + ":"))
+    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    best = None
+    for h in range(start, end):
+        if "Loop Header" in lines[h]:
+            lab = lines[h].split(":")[0].strip()
+            if not lab.startswith(".LBB"):
+                lab = lines[h - 1].split(":")[0].strip()
+            e = next(n for n in range(h + 1, end) if "s_cbranch" in lines[n] and lines[n].split()[-1] == lab)
+            nv = sum(1 for l in lines[h:e] if re.match(r"\s+v_", l))
+            if best is None or nv > best[2]:
+                best = (h, e, nv)
+    return best
+
+
+def nopify(lines, kernel, rules):
+    h, e, nv = main_loop_range(lines, kernel)
+    out = lines[:h + 1]
+    k = 0
+    prev_half = False
+    every = [int(r.split("=")[1]) for r in rules if r.startswith("every=")]
+    for l in lines[h + 1:e]:
+        m = re.match(r"\s+(v_\w+)", l)
+        if not m:
+            out.append(l)
+            continue
+        op = m.group(1).replace("_e32", "").replace("_e64", "")
+        half = op in HALF
+        nopw = "\ts_nop 1" if "nop1" in rules else "\ts_nop 0"
+        if "before_half" in rules and half:
+            out.append(nopw)
+        elif "before_half_trans" in rules and half and not prev_half:
+            out.append(nopw)
+        elif "before_alb" in rules and op == "v_alignbit_b32":
+            out.append(nopw)
+        elif "before_ad3" in rules and op == "v_add3_u32":
+            out.append(nopw)
+        elif "before_full_trans" in rules and not half and prev_half:
+            out.append(nopw)
+        out.append(l)
+        k += 1
+        ins = False
+        if "after_half" in rules and half:
+            ins = True
+        if "after_full_h" in rules and not half and prev_half:
+            ins = True
+        if "after_alb" in rules and op == "v_alignbit_b32":
+            ins = True
+        if every and k % every[0] == 0:
+            ins = True
+        if ins:
+            out.append("\ts_nop 0")
+        prev_half = half
+    out += lines[e:]
+    return out
+
+
+if __name__ == "__main__":
+    src, dst, kernel, rules = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4].split(",")
+    lines = open(src).read().split("\n")
+    open(dst, "w").write("\n".join(nopify(lines, kernel, rules) if rules != ["none"] else lines))

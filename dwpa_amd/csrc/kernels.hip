@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include "crypto_dev.hpp"
+#include "pbkdf2_dev.hpp"
 #include "prep_dev.hpp"
 #include "tables.hpp"
 #include "kernels.hpp"
@@ -73,53 +74,14 @@ __global__ __launch_bounds__(256) void k_prep_numeric(uint64_t first, uint32_t c
 }
 
 // ------------------------------------------------------------------------------------------------
-// stage 2: PBKDF2-HMAC-SHA1, 4096 iterations, one (candidate, output block) per lane.
-// blockIdx.y selects the output block T_1 (PMK bytes 0..19) or T_2 (bytes 20..31).  The salt blocks
-// (ESSID || INT(i) || SHA1 padding, pre-padded on the host) are wave-uniform -> scalar loads.
+// stage 2: PBKDF2-HMAC-SHA1 x4096 (body in pbkdf2_dev.hpp).  This is the plain hipcc-scheduled build, kept as the
+// A/B reference; the product launch uses k_pbkdf2_gfx950 after the gfx950 issue pass (pbkdf2_module.cpp).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pbkdf2(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base,
                                                 uint32_t count, const uint32_t* __restrict__ counter,
                                                 const uint32_t* __restrict__ salt, uint32_t nsalt,
                                                 uint32_t* __restrict__ pmk) {
-    const uint32_t blk = blockIdx.y;
-    const uint32_t s = base + blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = counter ? min(*counter, cap) : min(base + count, cap);
-    if (s >= n) return;
-    uint32_t hi[5], ho[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        hi[k] = mid[(size_t)k * cap + s];
-        ho[k] = mid[(size_t)(5 + k) * cap + s];
-    }
-    // U_1 = HMAC(P, S || INT(blk+1))
-    uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
-    const uint32_t* sb = salt + (size_t)blk * nsalt * 16;
-    for (uint32_t b = 0; b < nsalt; b++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) m[j] = sb[b * 16 + j];
-        sha1_compress(st, m);
-    }
-    const Sha1Mid MI = sha1_mid(hi);
-    const Sha1Mid MO = sha1_mid(ho);
-    uint32_t u[5], x[5], t[5];
-    sha1_84(MO, st, u);
-#pragma unroll
-    for (int k = 0; k < 5; k++) t[k] = u[k];
-#pragma unroll 1
-    for (int it = 1; it < 4096; it++) {
-        sha1_84(MI, u, x);
-        sha1_84(MO, x, u);
-#pragma unroll
-        for (int k = 0; k < 5; k++) t[k] ^= u[k];
-    }
-    if (blk == 0) {
-#pragma unroll
-        for (int k = 0; k < 5; k++) pmk[(size_t)k * cap + s] = t[k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 3; k++) pmk[(size_t)(5 + k) * cap + s] = t[k];
-    }
+    pbkdf2_body(mid, cap, base, count, counter, salt, nsalt, pmk);
 }
 
 // Caller-supplied PMK for one slot (check_key_m22000's $pmk argument, common.php:157,178).
@@ -359,8 +321,9 @@ hipError_t launch_prep_numeric(uint64_t first, uint32_t count, uint32_t digits, 
     return hipGetLastError();
 }
 
-hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
-                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s) {
+hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count,
+                               const uint32_t* counter, const uint32_t* salt, uint32_t nsalt, uint32_t* pmk,
+                               hipStream_t s) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pbkdf2, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, base, count, counter, salt, nsalt,
                        pmk);

@@ -12,8 +12,13 @@ hipError_t launch_prep_dict(const uint64_t* off, const uint8_t* bytes, uint64_t 
                             bool compact, hipStream_t s);
 hipError_t launch_prep_numeric(uint64_t first, uint32_t count, uint32_t digits, uint32_t* mid, uint64_t* ids,
                                uint32_t cap, hipStream_t s);
+// product launch: issue-pass code object (pbkdf2_module.cpp); DWPA_PBKDF2_PLAIN=1 -> launch_pbkdf2_plain
 hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
                          const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s);
+hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count,
+                               const uint32_t* counter, const uint32_t* salt, uint32_t nsalt, uint32_t* pmk,
+                               hipStream_t s);
+const char* pbkdf2_variant();
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s);
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,

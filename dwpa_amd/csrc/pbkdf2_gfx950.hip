@@ -1,0 +1,14 @@
+// pbkdf2_gfx950.hip -- the product PBKDF2 kernel.  Compiled device-only to gfx950 assembly, passed through the
+// VALU issue pass (gen/issue_pass.py, rule before_half), assembled to a code object and embedded in
+// libdwpa22000.so (see Makefile); launched with hipModuleLaunchKernel (pbkdf2_module.cpp).
+#include <hip/hip_runtime.h>
+
+#include "pbkdf2_dev.hpp"
+
+extern "C" __global__ __launch_bounds__(256) void k_pbkdf2_gfx950(const uint32_t* __restrict__ mid, uint32_t cap,
+                                                                  uint32_t base, uint32_t count,
+                                                                  const uint32_t* __restrict__ counter,
+                                                                  const uint32_t* __restrict__ salt, uint32_t nsalt,
+                                                                  uint32_t* __restrict__ pmk) {
+    dwpa::pbkdf2_body(mid, cap, base, count, counter, salt, nsalt, pmk);
+}

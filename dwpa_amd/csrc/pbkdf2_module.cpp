@@ -1,0 +1,58 @@
+// pbkdf2_module.cpp -- loads the issue-pass PBKDF2 code object (embedded at build time) on each device and launches
+// it.  DWPA_PBKDF2_PLAIN=1 selects the hipcc-scheduled k_pbkdf2 instead (A/B reference; identical results).
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include <map>
+#include <mutex>
+
+#include "kernels.hpp"
+
+namespace dwpa {
+
+extern const uint8_t pbkdf2_gfx950_hsaco[];
+extern const size_t pbkdf2_gfx950_hsaco_size;
+
+static std::mutex g_mod_mu;
+static std::map<int, hipFunction_t> g_fn;
+
+static bool use_plain() {
+    static const bool plain = [] {
+        const char* e = getenv("DWPA_PBKDF2_PLAIN");
+        return e && *e && *e != '0';
+    }();
+    return plain;
+}
+
+static hipError_t tuned_function(hipFunction_t* fn) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(g_mod_mu);
+    auto it = g_fn.find(dev);
+    if (it != g_fn.end()) {
+        *fn = it->second;
+        return hipSuccess;
+    }
+    hipModule_t mod;
+    if ((e = hipModuleLoadData(&mod, pbkdf2_gfx950_hsaco)) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(fn, mod, "k_pbkdf2_gfx950")) != hipSuccess) return e;
+    g_fn[dev] = *fn;
+    return hipSuccess;
+}
+
+hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
+                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (use_plain()) return launch_pbkdf2_plain(mid, cap, base, count, counter, salt, nsalt, pmk, s);
+    hipFunction_t fn;
+    hipError_t e = tuned_function(&fn);
+    if (e != hipSuccess) return e;
+    void* args[] = {(void*)&mid, (void*)&cap, (void*)&base, (void*)&count, (void*)&counter,
+                    (void*)&salt, (void*)&nsalt, (void*)&pmk};
+    return hipModuleLaunchKernel(fn, (count + 255) / 256, 2, 1, 256, 1, 1, 0, s, args, nullptr);
+}
+
+const char* pbkdf2_variant() { return use_plain() ? "k_pbkdf2 (hipcc schedule)" : "k_pbkdf2_gfx950 (issue pass)"; }
+
+}  // namespace dwpa
