@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--dict-words", type=int, default=DICT_WORDS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2",
-                    help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs")
+    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs; "
+                         "c1/c5 = the FFI check path (host buffers, PCIe-inclusive)")
     ap.add_argument("--essids", type=int, default=8, help="c3: number of ESSIDs (BASELINE: 1000)")
     return ap.parse_args()
 
@@ -194,6 +195,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload in ("c1", "c5"):
+        return main_ffi(args, world, rank, local)
     if world > 1:
         # control plane only (barrier, max-over-ranks time, sum of PMKs): the data path shards the keyspace and
         # never exchanges data, so there is no RCCL collective on the GPU.
@@ -306,6 +309,106 @@ def main():
         dist.destroy_process_group()
     if rank == 0 and not verified:
         sys.exit(3)
+
+
+def main_ffi(args, world, rank, local):
+    """C1 / C5 legs: the server-side FFI call (dwpa_check_m22000 / dwpa_check_batch) on host buffers, as PHP
+    makes it (common.php:157, :902).  A step = one call over the whole config: C1 = 10k keys x 1 PMKID line,
+    C5 = 1,010 mixed jobs x 202 keys at nc=128 (261 NC attempts).  The rate includes parsing, the key upload
+    and the result download (PCIe-inclusive, unlike the HBM-resident C2 line).  N>1 runs N replicas."""
+    import ctypes
+    import torch.distributed as dist
+    import dwpa_amd
+    from dwpa_amd import _lib as L
+    from dwpa_amd import synth as S
+    from dwpa_amd.shard import reduce_timing
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    cfg = L.Config(ctypes.sizeof(L.Config), 1 << local, 0, 0)
+    L.check(L.load().dwpa_init(ctypes.byref(cfg)), "init")
+    if args.workload == "c1":
+        line, keys, psk = S.c1_workload()
+        jobs = [(line, keys, False, 128)]
+        desc = "C1: 10,000 PSKs (1 % $HEX[]) vs one PMKID line, dwpa_check_m22000 per step (FFI, host buffers)"
+    else:
+        jobs = S.c5_jobs()
+        desc = ("C5: 250 PMKID + 250 x keyver 1/2/3 EAPOL lines (NC offsets 0..+-8, LE/BE) + 10 zero-PMK jobs, "
+                "202 keys per job, nc=128 (261 attempts), dwpa_check_batch per step (FFI, host buffers)")
+    batch = dwpa_amd.BatchJobs(jobs)
+    for _ in range(args.warmup):
+        batch.run()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.run()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        elapsed, total = reduce_timing(dist, time.perf_counter() - t0, float(batch.nkeys * args.steps))
+    else:
+        total = float(batch.nkeys * args.steps)
+    got = batch.results()
+    if args.workload == "c1":
+        verified = bool(got[0]) and got[0][0] == psk and got[0][3] == S.pmk(psk, bytes.fromhex(line.split(b"*")[5].decode()))
+    else:
+        verified = sum(1 for g in got if g) >= 0.85 * len(jobs)
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline_jobs(jobs, args.cpu_seconds)
+        print(json.dumps({
+            "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": desc, "jobs": len(jobs), "keys_per_step": batch.nkeys,
+                       "parallelism": f"replicas x{world}"},
+            "roofline": None, "cpu_baseline": cpu, "hits_verified": verified,
+            "hits": sum(1 for g in got if g)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0 and not verified:
+        sys.exit(3)
+
+
+def cpu_baseline_jobs(jobs, seconds):
+    """The PHP path for the same jobs: check_key_m22000 per job on the OpenSSL restatement (oracle/), jobs in
+    parallel on up to 16 host threads, over a bounded prefix of the job list."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    if len(jobs) == 1:
+        line, keys, pmk, nc = jobs[0]
+        probe = keys[-threads * 32:]
+        t0 = time.perf_counter()
+        O.c_check_many(line, probe, nc, threads)
+        rate = len(probe) / (time.perf_counter() - t0)
+        sample = keys[-int(max(len(probe), min(len(keys), rate * seconds))):]
+        t0 = time.perf_counter()
+        idx, _ = O.c_check_many(line, sample, nc, threads)
+        dt = time.perf_counter() - t0
+        one = keys[-max(8, int(rate / threads * seconds / 4)):]
+        t1 = time.perf_counter()
+        O.c_check_many(line, one, nc, 1)
+        dt1 = time.perf_counter() - t1
+        return {"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+                "sample": f"last {len(sample)} keys (ending at the true PSK), one check per key, {dt:.1f} s",
+                "found_planted": idx == len(sample) - 1,
+                "one_php_request": {"value": round(len(one) / dt1, 1), "cores": 1,
+                                    "sample": f"last {len(one)} keys on one thread, {dt1:.1f} s"}}
+    done, nkeys = 0, 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while done < len(jobs) and time.perf_counter() - t0 < seconds:
+            chunk = jobs[done:done + threads]
+            list(ex.map(lambda j: O.c_check_key_m22000(*j), chunk))
+            done += len(chunk)
+            nkeys += sum(len(j[1]) for j in chunk)
+    dt = time.perf_counter() - t0
+    return {"value": round(nkeys / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} jobs ({nkeys} keys), check_key_m22000 per job, {dt:.1f} s"}
 
 
 def cpu_baseline(line, data, off, plant, seconds):

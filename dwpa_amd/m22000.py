@@ -96,35 +96,49 @@ def check_key_m22000(hashline, keys, pmk=False, nc: int = 128):
     return _result(keys, res)
 
 
+class BatchJobs:
+    """A dwpa_check_batch argument block built once (ctypes job/key arrays) and run any number of times."""
+
+    def __init__(self, jobs):
+        jobs = list(jobs)
+        self.n = n = len(jobs)
+        self.carr = (L.Job * max(1, n))()
+        self._keep = []
+        self.key_lists = []
+        for i, (line, keys, pmk, nc) in enumerate(jobs):
+            h = _b(line)
+            keys = list(keys)
+            arr, k = L.bytes_array([None if x is None else _b(x) for x in keys])
+            pm = bytes(pmk) if pmk else None
+            self._keep += [h, arr, k, pm]
+            self.key_lists.append(keys)
+            c = self.carr[i]
+            c.line, c.line_len = h, len(h)
+            c.keys, c.nkeys = ctypes.cast(arr, ctypes.POINTER(L.Bytes)), len(keys)
+            c.pmk, c.nc = pm, int(nc)
+        self.nkeys = sum(len(k) for k in self.key_lists)
+        self.out = (L.Result * max(1, n))()
+        self.rcs = (ctypes.c_int * max(1, n))()
+
+    def run(self) -> None:
+        L.check(L.load().dwpa_check_batch(self.carr, self.n, self.out, self.rcs), "check_batch")
+
+    def results(self) -> list:
+        res = []
+        for i in range(self.n):
+            if self.rcs[i] == L.DWPA_HIT:
+                res.append(_result(self.key_lists[i], self.out[i]))
+            else:
+                L.check(self.rcs[i], "check_batch job")
+                res.append(False)
+        return res
+
+
 def check_batch(jobs):
     """jobs: iterable of (hashline, keys, pmk_or_False, nc).  Returns a list of check_key_m22000 results."""
-    jobs = list(jobs)
-    n = len(jobs)
-    carr = (L.Job * max(1, n))()
-    keep = []
-    key_lists = []
-    for i, (line, keys, pmk, nc) in enumerate(jobs):
-        h = _b(line)
-        keys = list(keys)
-        arr, k = L.bytes_array([None if x is None else _b(x) for x in keys])
-        keep += [h, arr, k]
-        key_lists.append(keys)
-        pm = bytes(pmk) if pmk else None
-        keep.append(pm)
-        carr[i].line, carr[i].line_len = h, len(h)
-        carr[i].keys, carr[i].nkeys = ctypes.cast(arr, ctypes.POINTER(L.Bytes)), len(keys)
-        carr[i].pmk, carr[i].nc = pm, int(nc)
-    out = (L.Result * max(1, n))()
-    rcs = (ctypes.c_int * max(1, n))()
-    L.check(L.load().dwpa_check_batch(carr, n, out, rcs), "check_batch")
-    res = []
-    for i in range(n):
-        if rcs[i] == L.DWPA_HIT:
-            res.append(_result(key_lists[i], out[i]))
-        else:
-            L.check(rcs[i], "check_batch job")
-            res.append(False)
-    return res
+    b = BatchJobs(jobs)
+    b.run()
+    return b.results()
 
 
 def pbkdf2_pmk(keys, essid) -> list:

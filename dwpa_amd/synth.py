@@ -133,3 +133,63 @@ CHALLENGE_LINES = [
     b"0000000000000000000000000000000000000000000000000000000000000000"
     b"00001830160100000fac020100000fac040100000fac023c000000*00",
 ]
+
+
+def fast_psk(rng: random.Random, lo: int = 8, hi: int = 63) -> bytes:
+    """Printable-ASCII PSK, length U[lo, hi] (same distribution family as random_psk, cheaper to draw in bulk)."""
+    return bytes(0x20 + b % 95 for b in rng.randbytes(rng.randint(lo, hi)))
+
+
+def c1_workload(seed: int = 0, n: int = 10_000):
+    """BASELINE configs[0] / SURVEY.md 8(d) C1: n PSKs (length U[8,63], printable, ~1 % `$HEX[..]`) against one
+    PMKID line (ESSID 10 B, random MACs, seed 1); the true PSK is the last key.  Returns (line, keys, psk)."""
+    rng = random.Random(seed)
+    keys = []
+    for _ in range(n):
+        k = fast_psk(rng)
+        if rng.random() < 0.01:
+            k = b"$HEX[" + k.hex().encode() + b"]"
+        keys.append(k)
+    net = random.Random(1)
+    essid, ap, sta, _, _ = random_net(net, essid_len=10)
+    psk = keys[-1]
+    raw = bytes.fromhex(psk[5:-1].decode()) if psk.startswith(b"$HEX[") else psk
+    return pmkid_line(raw, essid, ap, sta), keys, raw
+
+
+def c5_jobs(seed: int = 5, per_kind: int = 250, keys_per_job: int = 202, essids: int = 200, nc: int = 128,
+            hit_rate: float = 0.9, zero_pmk: int = 10):
+    """per_kind PMKID + keyver 1/2/3 EAPOL lines (nonce offsets uniform in {0, +-1..+-8} x
+    {LE, BE}) plus zero_pmk zero-PMK jobs (common.php:592), keys_per_job candidates per job (the put_work cap,
+    common.php:937), the true PSK planted at a random index in hit_rate of the jobs.  ESSIDs are drawn from a
+    pool of `essids` networks so the batch path groups lines.  Returns [(line, keys, pmk, nc)]."""
+    rng = random.Random(seed)
+    nets = [random_net(rng) for _ in range(essids)]
+    jobs = []
+    for kind in ("pmkid", 1, 2, 3):
+        for _ in range(per_kind):
+            essid, ap, sta, an, sn = nets[rng.randrange(essids)]
+            ap, sta = rng.randbytes(6), rng.randbytes(6)
+            psk = fast_psk(rng)
+            if kind == "pmkid":
+                line = pmkid_line(psk, essid, ap, sta)
+            else:
+                line = eapol_line(psk, essid, ap, sta, rng.randbytes(32), rng.randbytes(32), kind,
+                                  rng.randint(-8, 8), rng.choice(["LE", "BE"]), mp=rng.choice([0, 0x80, 0x02]),
+                                  eapol_len=rng.choice([121, 123, 151, 187]), rng=rng)
+            keys = [fast_psk(rng) for _ in range(keys_per_job - 1)]
+            if rng.random() < hit_rate:
+                keys.insert(rng.randrange(keys_per_job), psk)
+            else:
+                keys.append(fast_psk(rng))
+            jobs.append((line, keys, False, nc))
+    zpmk = b"\0" * 32
+    for i in range(zero_pmk):
+        essid, ap, sta, an, sn = nets[rng.randrange(essids)]
+        if i % 2:
+            line = pmkid_line(b"", essid, ap, sta, the_pmk=zpmk)
+        else:
+            line = eapol_line(b"", essid, ap, sta, rng.randbytes(32), rng.randbytes(32), 2 + i % 4 // 2,
+                              rng.randint(-8, 8), "BE", the_pmk=zpmk, rng=rng)
+        jobs.append((line, [b""], zpmk, nc))
+    return jobs

@@ -1,0 +1,55 @@
+"""GPU parity at the BASELINE.json sizes of the FFI-shaped configs.
+
+C1 = 10,000 PSKs against one PMKID line through dwpa_check_m22000 (the PHP FFI call, common.php:157).
+C5 = 1,010 mixed jobs x 202 keys through dwpa_check_batch, PHP nonce window nc=128 (261 attempts).
+
+The oracle is checked on the *prefix* of each job's key list up to the key the GPU reported (all keys for a
+miss).  check_key_m22000 returns the first key in input order that verifies (common.php:169-306), so the prefix
+decides the result by itself: the GPU tuple is correct iff the oracle returns the same tuple on that prefix.
+This keeps the whole C5 batch checked bit-exact in the full [key, nc, endian, PMK] tuple at about half the
+oracle cost of a full re-check.
+"""
+import os
+from concurrent.futures import ThreadPoolExecutor
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import dwpa_amd  # noqa: E402
+from dwpa_amd import synth as S  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _prefix_oracle(job, got):
+    line, keys, pmk, nc = job
+    if got is False:
+        return O.c_check_key_m22000(line, keys, pmk, nc) is False
+    # the GPU names the key by value; find its first occurrence (the oracle returns the first hit, too)
+    k = next(i for i, key in enumerate(keys) if key is not None and O.hc_unhex(key) == got[0])
+    return O.c_check_key_m22000(line, keys[:k + 1], pmk, nc) == got
+
+
+def test_c1_pmkid_10k_keys():
+    line, keys, psk = S.c1_workload()
+    got = dwpa_amd.check_key_m22000(line, keys)
+    assert got and got[0] == psk and got[1] is None and got[2] is None
+    idx, exp = O.c_check_many(line, keys, 128, THREADS)
+    assert idx == len(keys) - 1
+    assert got == exp
+
+
+def test_c5_mixed_batch_full_size():
+    jobs = S.c5_jobs()
+    assert len(jobs) == 1010 and sum(len(j[1]) for j in jobs) == 1000 * 202 + 10
+    got = dwpa_amd.check_batch(jobs)
+    hits = sum(1 for g in got if g)
+    assert hits >= 0.85 * len(jobs)
+    # every EAPOL hit carries an NC and endian inside the planted window
+    assert all(g[1] is not None and abs(g[1]) <= 8 for g, j in zip(got, jobs) if g and j[0][4:6] == b"02")
+    with ThreadPoolExecutor(THREADS) as ex:
+        ok = list(ex.map(_prefix_oracle, jobs, got))
+    bad = [i for i, o in enumerate(ok) if not o]
+    assert not bad, [(i, jobs[i][0][:40], got[i]) for i in bad[:3]]
