@@ -13,6 +13,8 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
+#include <unordered_map>
 #include <thread>
 #include <vector>
 
@@ -64,6 +66,7 @@ struct Device {
     std::mutex mu;
     Batch batch;
     DevBuf lines, atts, pool, segs, salt, koff, kbytes, idsup;
+    DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
 };
 
 static std::mutex g_mu;
@@ -165,54 +168,70 @@ static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
     RCHK(d.batch.reserve(n, n));
-    // keys -> offsets/bytes (packed back to back: k_prep_dict derives len = off[i+1] - off[i])
-    std::vector<uint64_t> off(n + 1);
-    std::string bytes;
+    // Unique (ESSID, key) pairs are derived once, all ESSIDs in one launch (server batches fan one key out to
+    // every net of an ESSID, common.php:879-902); each slot then gathers its PMK from them or from the caller's
+    // $pmk.  Slots arrive sorted by ESSID, so duplicates are found within each ESSID run.
+    std::vector<uint32_t> src(n), sref, spool, cpmk;
+    std::vector<const std::string*> ukeys;
+    std::unordered_map<std::string_view, uint32_t> seen;
+    const std::string* cur = nullptr;
+    uint32_t cur_ref = 0;
     for (uint32_t i = 0; i < n; i++) {
-        off[i] = bytes.size();
-        bytes += *slots[b + i].key;
+        const Slot& sl = slots[b + i];
+        if (!sl.pbkdf2) {
+            const uint8_t* p = job_pmk[sl.job];
+            src[i] = GATHER_CALLER | (uint32_t)(cpmk.size() / 8);
+            for (int k = 0; k < 8; k++)
+                cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 | (uint32_t)p[4 * k + 2] << 8 |
+                               p[4 * k + 3]);
+            continue;
+        }
+        if (!cur || *sl.essid != *cur) {
+            cur = sl.essid;
+            seen.clear();
+            std::vector<uint32_t> sb;
+            const uint32_t nb = build_salt_blocks(*cur, sb);
+            cur_ref = (uint32_t)spool.size();
+            spool.push_back(nb);
+            spool.insert(spool.end(), sb.begin(), sb.end());
+        }
+        auto ins = seen.try_emplace(std::string_view(*sl.key), (uint32_t)ukeys.size());
+        if (ins.second) {
+            ukeys.push_back(sl.key);
+            sref.push_back(cur_ref);
+        }
+        src[i] = ins.first->second;
     }
-    off[n] = bytes.size();
-    bytes.append(8, '\0');
-    std::vector<uint8_t> bv(bytes.begin(), bytes.end());
-    RCHK(upload(d.koff, off, s));
-    RCHK(upload(d.kbytes, bv, s));
-    HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, n, 0, 0xffffffffu,
-                            (uint32_t*)d.batch.mid.p, nullptr, nullptr, d.batch.cap, false, s));
+    const uint32_t nu = (uint32_t)ukeys.size();
+    RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
+    if (nu) {
+        // unique keys -> offsets/bytes (back to back: k_prep_dict derives len = off[i+1] - off[i])
+        std::vector<uint64_t> off(nu + 1);
+        std::string bytes;
+        for (uint32_t u = 0; u < nu; u++) {
+            off[u] = bytes.size();
+            bytes += *ukeys[u];
+        }
+        off[nu] = bytes.size();
+        bytes.append(8, '\0');
+        std::vector<uint8_t> bv(bytes.begin(), bytes.end());
+        RCHK(upload(d.koff, off, s));
+        RCHK(upload(d.kbytes, bv, s));
+        RCHK(upload(d.salt, spool, s));
+        RCHK(upload(d.sref, sref, s));
+        HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, nu, 0, 0xffffffffu,
+                                (uint32_t*)d.batch.mid.p, nullptr, nullptr, d.batch.cap, false, s));
+        HIPCHK(launch_pbkdf2_ms((const uint32_t*)d.batch.mid.p, d.batch.cap, nu, (const uint32_t*)d.salt.p,
+                                (const uint32_t*)d.sref.p, (uint32_t*)d.upmk.p, s));
+    }
+    RCHK(upload(d.cpmk, cpmk, s));
+    RCHK(upload(d.src, src, s));
+    HIPCHK(launch_gather_pmk((const uint32_t*)d.upmk.p, d.batch.cap, (const uint32_t*)d.cpmk.p,
+                             (const uint32_t*)d.src.p, n, (uint32_t*)d.batch.pmk.p, d.batch.cap, s));
     // ids = key ordinals (selects the PHP attempt list of each key)
     std::vector<uint64_t> ids(n);
     for (uint32_t i = 0; i < n; i++) ids[i] = slots[b + i].ordinal;
     HIPCHK(hipMemcpyAsync(d.batch.ids.p, ids.data(), n * 8, hipMemcpyHostToDevice, s));
-
-    // PBKDF2 per ESSID run
-    std::vector<uint32_t> salts;
-    struct Run { uint32_t b, e, salt_off, nsalt; };
-    std::vector<Run> runs;
-    for (uint32_t i = 0; i < n;) {
-        uint32_t j = i;
-        while (j < n && *slots[b + j].essid == *slots[b + i].essid && slots[b + j].pbkdf2) j++;
-        if (j > i) {
-            std::vector<uint32_t> sb;
-            uint32_t nb = build_salt_blocks(*slots[b + i].essid, sb);
-            runs.push_back({i, j, (uint32_t)salts.size(), nb});
-            salts.insert(salts.end(), sb.begin(), sb.end());
-            i = j;
-        } else {
-            i++;  // caller-supplied PMK
-        }
-    }
-    RCHK(upload(d.salt, salts, s));
-    for (const Run& r : runs)
-        HIPCHK(launch_pbkdf2((const uint32_t*)d.batch.mid.p, d.batch.cap, r.b, r.e - r.b, nullptr,
-                             (const uint32_t*)d.salt.p + r.salt_off, r.nsalt, (uint32_t*)d.batch.pmk.p, s));
-    for (uint32_t i = 0; i < n; i++)
-        if (!slots[b + i].pbkdf2) {
-            const uint8_t* p = job_pmk[slots[b + i].job];
-            uint32_t w[8];
-            for (int k = 0; k < 8; k++)
-                w[k] = (uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 | (uint32_t)p[4 * k + 2] << 8 | p[4 * k + 3];
-            HIPCHK(launch_set_pmk((uint32_t*)d.batch.pmk.p, d.batch.cap, i, w, s));
-        }
 
     if (pmk_out) {
         std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
@@ -630,6 +649,7 @@ void dwpa_shutdown(void) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
         for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->salt, &d->koff, &d->kbytes, &d->idsup,
+                          &d->upmk, &d->sref, &d->src, &d->cpmk,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();
         d->batch.cap = d->batch.hitcap = 0;

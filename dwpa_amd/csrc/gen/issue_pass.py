@@ -45,6 +45,7 @@ def main_loop_range(lines, kernel):
 
 def nopify(lines, kernel, rules):
     h, e, nv = main_loop_range(lines, kernel)
+    sys.stderr.write(f"issue_pass: {kernel}: main loop {nv} VALU, rules {','.join(rules)}\n")
     out = lines[:h + 1]
     k = 0
     prev_half = False
@@ -88,4 +89,7 @@ def nopify(lines, kernel, rules):
 if __name__ == "__main__":
     src, dst, kernel, rules = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4].split(",")
     lines = open(src).read().split("\n")
-    open(dst, "w").write("\n".join(nopify(lines, kernel, rules) if rules != ["none"] else lines))
+    if rules != ["none"]:
+        for k in kernel.split("+"):  # several kernels may share one .s
+            lines = nopify(lines, k, rules)
+    open(dst, "w").write("\n".join(lines))

@@ -84,6 +84,31 @@ __global__ __launch_bounds__(256) void k_pbkdf2(const uint32_t* __restrict__ mid
     pbkdf2_body(mid, cap, base, count, counter, salt, nsalt, pmk);
 }
 
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_ms(
+    const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
+    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk) {
+    pbkdf2_body_ms(mid, cap, count, pool, sref, pmk);
+}
+
+// Slot PMKs from the derived unique (ESSID, key) PMKs or from caller-supplied PMKs:
+// src[i] = u -> upmk[.][u];  src[i] = GATHER_CALLER | c -> cpmk[c][0..7] (check_key_m22000's $pmk, common.php:178).
+__global__ __launch_bounds__(256) void k_gather_pmk(const uint32_t* __restrict__ upmk, uint32_t ucap,
+                                                    const uint32_t* __restrict__ cpmk,
+                                                    const uint32_t* __restrict__ src, uint32_t n,
+                                                    uint32_t* __restrict__ pmk, uint32_t cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t r = src[i];
+    if (r & GATHER_CALLER) {
+        const uint32_t* c = cpmk + 8 * (size_t)(r & ~GATHER_CALLER);
+#pragma unroll
+        for (int k = 0; k < 8; k++) pmk[(size_t)k * cap + i] = c[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) pmk[(size_t)k * cap + i] = upmk[(size_t)k * ucap + r];
+    }
+}
+
 // Caller-supplied PMK for one slot (check_key_m22000's $pmk argument, common.php:157,178).
 __global__ void k_set_pmk(uint32_t* __restrict__ pmk, uint32_t cap, uint32_t slot, uint4 lo, uint4 hi) {
     if (threadIdx.x == 0) {
@@ -327,6 +352,20 @@ hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base,
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pbkdf2, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, base, count, counter, salt, nsalt,
                        pmk);
+    return hipGetLastError();
+}
+
+hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
+                                  const uint32_t* sref, uint32_t* pmk, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pbkdf2_ms, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, count, pool, sref, pmk);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t* cpmk, const uint32_t* src,
+                             uint32_t n, uint32_t* pmk, uint32_t cap, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_pmk, dim3(cdiv(n, 256)), dim3(256), 0, s, upmk, ucap, cpmk, src, n, pmk, cap);
     return hipGetLastError();
 }
 

@@ -19,6 +19,14 @@ hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base,
                                const uint32_t* counter, const uint32_t* salt, uint32_t nsalt, uint32_t* pmk,
                                hipStream_t s);
 const char* pbkdf2_variant();
+// many ESSIDs per launch: slot s uses the salt entry pool + sref[s] = {nsalt, [2][nsalt][16] words}
+hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
+                            const uint32_t* sref, uint32_t* pmk, hipStream_t s);
+hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
+                                  const uint32_t* sref, uint32_t* pmk, hipStream_t s);
+constexpr uint32_t GATHER_CALLER = 0x80000000u;
+hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t* cpmk, const uint32_t* src,
+                             uint32_t n, uint32_t* pmk, uint32_t cap, hipStream_t s);
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s);
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,

@@ -13,23 +13,11 @@
 
 namespace dwpa {
 
-__device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base,
-                                            uint32_t count, const uint32_t* __restrict__ counter,
-                                            const uint32_t* __restrict__ salt, uint32_t nsalt,
-                                            uint32_t* __restrict__ pmk) {
-    const uint32_t blk = blockIdx.y;
-    const uint32_t s = base + blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = counter ? min(*counter, cap) : min(base + count, cap);
-    if (s >= n) return;
-    uint32_t hi[5], ho[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        hi[k] = mid[(size_t)k * cap + s];
-        ho[k] = mid[(size_t)(5 + k) * cap + s];
-    }
-    // U_1 = HMAC(P, S || INT(blk+1))
+// One lane's PBKDF2 output block: T = U_1 ^ ... ^ U_4096 with U_1 = HMAC(P, S || INT(blk+1)).  `sb` points at
+// the nsalt pre-padded 16-word salt blocks of this output block.
+__device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
+                                            uint32_t nsalt, uint32_t t[5]) {
     uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
-    const uint32_t* sb = salt + (size_t)blk * nsalt * 16;
     for (uint32_t b = 0; b < nsalt; b++) {
         uint32_t m[16];
 #pragma unroll
@@ -38,7 +26,7 @@ __device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, ui
     }
     const Sha1Mid MI = sha1_mid(hi);
     const Sha1Mid MO = sha1_mid(ho);
-    uint32_t u[5], x[5], t[5];
+    uint32_t u[5], x[5];
     sha1_84(MO, st, u);
 #pragma unroll
     for (int k = 0; k < 5; k++) t[k] = u[k];
@@ -49,6 +37,19 @@ __device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, ui
 #pragma unroll
         for (int k = 0; k < 5; k++) t[k] ^= u[k];
     }
+}
+
+__device__ __forceinline__ void load_mid(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t s, uint32_t hi[5],
+                                         uint32_t ho[5]) {
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        hi[k] = mid[(size_t)k * cap + s];
+        ho[k] = mid[(size_t)(5 + k) * cap + s];
+    }
+}
+
+__device__ __forceinline__ void store_block(uint32_t* __restrict__ pmk, uint32_t cap, uint32_t s, uint32_t blk,
+                                            const uint32_t t[5]) {
     if (blk == 0) {
 #pragma unroll
         for (int k = 0; k < 5; k++) pmk[(size_t)k * cap + s] = t[k];
@@ -56,6 +57,38 @@ __device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, ui
 #pragma unroll
         for (int k = 0; k < 3; k++) pmk[(size_t)(5 + k) * cap + s] = t[k];
     }
+}
+
+// One ESSID for the whole launch: salt = [2 blocks][nsalt][16] words, read with scalar loads.
+__device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base,
+                                            uint32_t count, const uint32_t* __restrict__ counter,
+                                            const uint32_t* __restrict__ salt, uint32_t nsalt,
+                                            uint32_t* __restrict__ pmk) {
+    const uint32_t blk = blockIdx.y;
+    const uint32_t s = base + blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = counter ? min(*counter, cap) : min(base + count, cap);
+    if (s >= n) return;
+    uint32_t hi[5], ho[5], t[5];
+    load_mid(mid, cap, s, hi, ho);
+    pbkdf2_lane(hi, ho, salt + (size_t)blk * nsalt * 16, nsalt, t);
+    store_block(pmk, cap, s, blk, t);
+}
+
+// Many ESSIDs in one launch (server batches, common.php:902): slot s derives with the salt entry at
+// pool + sref[s] = {nsalt, [2 blocks][nsalt][16] words}.  Only the U_1 blocks differ per lane; the 4096 loop is
+// the same code as pbkdf2_body's.
+__device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
+                                               const uint32_t* __restrict__ pool,
+                                               const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk) {
+    const uint32_t blk = blockIdx.y;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= min(count, cap)) return;
+    uint32_t hi[5], ho[5], t[5];
+    load_mid(mid, cap, s, hi, ho);
+    const uint32_t* e = pool + sref[s];
+    const uint32_t nsalt = e[0];
+    pbkdf2_lane(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
+    store_block(pmk, cap, s, blk, t);
 }
 
 }  // namespace dwpa

@@ -12,3 +12,11 @@ extern "C" __global__ __launch_bounds__(256) void k_pbkdf2_gfx950(const uint32_t
                                                                   uint32_t* __restrict__ pmk) {
     dwpa::pbkdf2_body(mid, cap, base, count, counter, salt, nsalt, pmk);
 }
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_ms(const uint32_t* __restrict__ mid, uint32_t cap,
+                                                                     uint32_t count,
+                                                                     const uint32_t* __restrict__ pool,
+                                                                     const uint32_t* __restrict__ sref,
+                                                                     uint32_t* __restrict__ pmk) {
+    dwpa::pbkdf2_body_ms(mid, cap, count, pool, sref, pmk);
+}

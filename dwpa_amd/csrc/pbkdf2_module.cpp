@@ -13,8 +13,11 @@ namespace dwpa {
 extern const uint8_t pbkdf2_gfx950_hsaco[];
 extern const size_t pbkdf2_gfx950_hsaco_size;
 
+struct Fns {
+    hipFunction_t one, ms;  // k_pbkdf2_gfx950 (one ESSID per launch), k_pbkdf2_gfx950_ms (per-slot salt)
+};
 static std::mutex g_mod_mu;
-static std::map<int, hipFunction_t> g_fn;
+static std::map<int, Fns> g_fn;
 
 static bool use_plain() {
     static const bool plain = [] {
@@ -24,7 +27,7 @@ static bool use_plain() {
     return plain;
 }
 
-static hipError_t tuned_function(hipFunction_t* fn) {
+static hipError_t tuned_functions(Fns* fn) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -36,7 +39,8 @@ static hipError_t tuned_function(hipFunction_t* fn) {
     }
     hipModule_t mod;
     if ((e = hipModuleLoadData(&mod, pbkdf2_gfx950_hsaco)) != hipSuccess) return e;
-    if ((e = hipModuleGetFunction(fn, mod, "k_pbkdf2_gfx950")) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(&fn->one, mod, "k_pbkdf2_gfx950")) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(&fn->ms, mod, "k_pbkdf2_gfx950_ms")) != hipSuccess) return e;
     g_fn[dev] = *fn;
     return hipSuccess;
 }
@@ -45,12 +49,23 @@ hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint3
                          const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s) {
     if (count == 0) return hipSuccess;
     if (use_plain()) return launch_pbkdf2_plain(mid, cap, base, count, counter, salt, nsalt, pmk, s);
-    hipFunction_t fn;
-    hipError_t e = tuned_function(&fn);
+    Fns fn;
+    hipError_t e = tuned_functions(&fn);
     if (e != hipSuccess) return e;
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&base, (void*)&count, (void*)&counter,
                     (void*)&salt, (void*)&nsalt, (void*)&pmk};
-    return hipModuleLaunchKernel(fn, (count + 255) / 256, 2, 1, 256, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(fn.one, (count + 255) / 256, 2, 1, 256, 1, 1, 0, s, args, nullptr);
+}
+
+hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
+                            const uint32_t* sref, uint32_t* pmk, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (use_plain()) return launch_pbkdf2_ms_plain(mid, cap, count, pool, sref, pmk, s);
+    Fns fn;
+    hipError_t e = tuned_functions(&fn);
+    if (e != hipSuccess) return e;
+    void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk};
+    return hipModuleLaunchKernel(fn.ms, (count + 255) / 256, 2, 1, 256, 1, 1, 0, s, args, nullptr);
 }
 
 const char* pbkdf2_variant() { return use_plain() ? "k_pbkdf2 (hipcc schedule)" : "k_pbkdf2_gfx950 (issue pass)"; }

@@ -53,3 +53,42 @@ def test_c5_mixed_batch_full_size():
         ok = list(ex.map(_prefix_oracle, jobs, got))
     bad = [i for i, o in enumerate(ok) if not o]
     assert not bad, [(i, jobs[i][0][:40], got[i]) for i in bad[:3]]
+
+
+def test_batch_fanout_dedup_and_mixed_salt_lengths():
+    """put_work shape (common.php:879-902): one submitted key checked against every net of an ESSID, plus PMK
+    re-use jobs (:919) -- the engine derives each (ESSID, key) once.  ESSIDs of 1..60 bytes put 1- and 2-block
+    salts into the same multi-salt launch."""
+    import random
+    rng = random.Random(77)
+    jobs = []
+    for essid_len in (1, 7, 32, 51, 52, 60):
+        essid = bytes(rng.randrange(0x20, 0x7f) for _ in range(essid_len))
+        psk = S.fast_psk(rng)
+        shared = [S.fast_psk(rng) for _ in range(5)] + [psk]
+        pmk = S.pmk(psk, essid)
+        for k in range(24):
+            ap, sta = rng.randbytes(6), rng.randbytes(6)
+            right = k % 3 != 2
+            the = pmk if right else S.pmk(b"other-" + psk, essid)
+            if k % 2:
+                line = S.pmkid_line(psk, essid, ap, sta, the_pmk=the)
+            else:
+                line = S.eapol_line(psk, essid, ap, sta, rng.randbytes(32), rng.randbytes(32), 1 + k % 3,
+                                    rng.randint(-4, 4), rng.choice(["LE", "BE"]), the_pmk=the, rng=rng)
+            jobs.append((line, [psk], False, 128))
+            jobs.append((line, shared, False, 16))
+            jobs.append((line, [b""], pmk, 9))  # PMK re-use: caller PMK, no derivation
+    got = dwpa_amd.check_batch(jobs)
+    with ThreadPoolExecutor(THREADS) as ex:
+        exp = list(ex.map(lambda j: O.c_check_key_m22000(*j), jobs))
+    bad = [i for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    assert not bad, [(i, got[i], exp[i]) for i in bad[:3]]
+    assert sum(1 for e in exp if e) >= len(jobs) // 2
+
+
+def test_pbkdf2_pmk_duplicate_keys():
+    keys = [b"password", b"password", b"12345678", b"password", b"x" * 63, b"12345678"]
+    essid = b"linksys"
+    got = dwpa_amd.pbkdf2_pmk(keys, essid)
+    assert got == [O.c_pbkdf2(k, essid) for k in keys]
