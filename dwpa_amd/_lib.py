@@ -87,6 +87,7 @@ SIGNATURES = {
     "dwpa_scan_load_numeric": ([_P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P], ctypes.c_int),
     "dwpa_scan_pbkdf2": ([_P, ctypes.c_int, _P], ctypes.c_int),
     "dwpa_scan_verify": ([_P, ctypes.c_int, _P], ctypes.c_int),
+    "dwpa_scan_run": ([_P, _P], ctypes.c_int),
     "dwpa_scan_hits": ([_P, ctypes.POINTER(Hit), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), _P], ctypes.c_int),
     "dwpa_scan_loaded": ([_P, ctypes.POINTER(ctypes.c_uint32), _P], ctypes.c_int),
     "dwpa_scan_destroy": ([_P], None),

@@ -138,7 +138,6 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
         hipMemcpyAsync(w.bytes.p, c.bytes.data() + c.off[b], nbytes, hipMemcpyHostToDevice, w.stream) != hipSuccess)
         return DWPA_E_HIP;
     const uint32_t cap = scan_batch_cap(w.scan);
-    const int ngroups = dwpa_scan_num_groups(w.scan);
     const size_t words = e - b;
     const uint64_t nrules = rules ? rules->size() : 1;
     const uint64_t total = words * nrules;
@@ -152,10 +151,7 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
         else
             r = scan_load_dict(w.scan, (const uint64_t*)w.off.p, (const uint8_t*)w.bytes.p, wb, nw, 8, 63, w.stream);
         if (r < 0) return r;
-        for (int g = 0; g < ngroups; g++) {
-            if ((r = scan_pbkdf2(w.scan, g, w.stream)) < 0) return r;
-            if ((r = scan_verify(w.scan, g, w.stream)) < 0) return r;
-        }
+        if ((r = scan_run(w.scan, w.stream)) < 0) return r;  // all ESSID groups, grouped per launch
         std::vector<HitDev> hits;
         if ((r = scan_hits_raw(w.scan, hits, w.stream)) < 0) return r;
         if (hits.empty()) continue;

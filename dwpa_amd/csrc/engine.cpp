@@ -437,6 +437,15 @@ struct dwpa_scan {
     dwpa::DevBuf lines, atts, pool, salt, segs;
     dwpa::Batch batch;
     uint32_t batch_cap = 0;
+    // scan_run (many ESSID groups per PBKDF2 launch): rebuilt when the set of uncracked lines changes
+    struct Chunk {
+        uint32_t g0, ngroups, list0, nlines;
+    };
+    bool mg_dirty = true;
+    uint32_t mg_per = 0;                   // groups per launch
+    std::vector<Chunk> mg_chunks;
+    std::vector<uint32_t> mg_gsalt_h, mg_list_h, mg_poff_h;
+    dwpa::DevBuf mg_pmk, mg_gsalt, mg_list, mg_poff;
 };
 
 namespace dwpa {
@@ -498,6 +507,7 @@ void scan_destroy(dwpa_scan* sc) {
     (void)hipSetDevice(sc->device);
     (void)hipDeviceSynchronize();
     sc->lines.release(); sc->atts.release(); sc->pool.release(); sc->salt.release(); sc->segs.release();
+    sc->mg_pmk.release(); sc->mg_gsalt.release(); sc->mg_list.release(); sc->mg_poff.release();
     sc->batch.mid.release(); sc->batch.pmk.release(); sc->batch.ids.release(); sc->batch.hits.release();
     sc->batch.counters.release();
     delete sc;
@@ -558,6 +568,70 @@ int scan_verify(dwpa_scan* sc, int group, void* stream) {
     return 0;
 }
 
+// Candidate slots per multi-group PBKDF2 launch (x2 lanes for the two output blocks): 4M slots fill all 1024 SIMDs
+// at 8 waves with room to spare, and bound the group-major PMK buffer at 128 MiB.
+constexpr uint64_t MG_SLOTS = 1u << 22;
+
+static int scan_mg_rebuild(dwpa_scan* sc, hipStream_t s) {
+    const uint32_t cap = sc->batch_cap;
+    HIPCHK(hipStreamSynchronize(s));  // the previous tables may still be read by queued launches
+    sc->mg_per = (uint32_t)std::max<uint64_t>(1, MG_SLOTS / cap);
+    sc->mg_chunks.clear();
+    sc->mg_gsalt_h.clear();
+    sc->mg_list_h.clear();
+    sc->mg_poff_h.assign(std::max<size_t>(sc->tb.lines.size(), 1), 0);
+    uint32_t in_chunk = 0, most = 0;
+    for (const ScanGroup& g : sc->groups) {
+        bool any = false;
+        for (uint32_t l = g.line_begin; l < g.line_end; l++) any |= !sc->cracked[l];
+        if (!any) continue;
+        if (in_chunk == 0)
+            sc->mg_chunks.push_back({(uint32_t)sc->mg_gsalt_h.size() / 2, 0, (uint32_t)sc->mg_list_h.size(), 0});
+        dwpa_scan::Chunk& ch = sc->mg_chunks.back();
+        sc->mg_gsalt_h.push_back(g.salt_off);
+        sc->mg_gsalt_h.push_back(g.nsalt);
+        for (uint32_t l = g.line_begin; l < g.line_end; l++) {
+            if (sc->cracked[l]) continue;
+            sc->mg_list_h.push_back(l);
+            sc->mg_poff_h[l] = in_chunk * cap;
+        }
+        ch.ngroups++;
+        ch.nlines = (uint32_t)sc->mg_list_h.size() - ch.list0;
+        most = std::max(most, ch.ngroups);
+        if (++in_chunk == sc->mg_per) in_chunk = 0;
+    }
+    if (most) RCHK(sc->mg_pmk.ensure((size_t)PMK_WORDS * most * cap * 4));
+    RCHK(upload(sc->mg_gsalt, sc->mg_gsalt_h, s));
+    RCHK(upload(sc->mg_list, sc->mg_list_h, s));
+    RCHK(upload(sc->mg_poff, sc->mg_poff_h, s));
+    sc->mg_dirty = false;
+    return 0;
+}
+
+int scan_run(dwpa_scan* sc, void* stream) {
+    if (!sc) return DWPA_E_ARG;
+    HIPCHK(hipSetDevice(sc->device));
+    hipStream_t s = as_stream(stream);
+    if (sc->mg_dirty) RCHK(scan_mg_rebuild(sc, s));
+    const uint32_t cap = sc->batch_cap;
+    const uint32_t pstride = sc->mg_per * cap;
+    for (const dwpa_scan::Chunk& ch : sc->mg_chunks) {
+        HIPCHK(launch_pbkdf2_mg((const uint32_t*)sc->batch.mid.p, cap, (const uint32_t*)sc->batch.counters.p,
+                                ch.ngroups, (const uint32_t*)sc->salt.p, (const uint32_t*)sc->mg_gsalt.p + 2 * ch.g0,
+                                (uint32_t*)sc->mg_pmk.p, pstride, s));
+        for (uint32_t l = 0; l < ch.nlines; l += 65535u) {
+            const uint32_t nl = std::min<uint32_t>(65535u, ch.nlines - l);
+            HIPCHK(launch_verify((const uint32_t*)sc->mg_pmk.p, cap, (const uint64_t*)sc->batch.ids.p,
+                                 (const uint32_t*)sc->batch.counters.p, nullptr, cap / 64, ch.list0 + l, nl,
+                                 (const LineDev*)sc->lines.p, (const uint32_t*)sc->pool.p, (const AttDev*)sc->atts.p,
+                                 (HitDev*)sc->batch.hits.p, (uint32_t*)sc->batch.counters.p + 1, sc->batch.hitcap,
+                                 sc->tb.any_aes, s, (const uint32_t*)sc->mg_list.p, (const uint32_t*)sc->mg_poff.p,
+                                 pstride));
+        }
+    }
+    return 0;
+}
+
 int scan_hits_raw(dwpa_scan* sc, std::vector<HitDev>& out, void* stream) {
     HIPCHK(hipSetDevice(sc->device));
     hipStream_t s = as_stream(stream);
@@ -588,7 +662,10 @@ void hit_to_public(const dwpa_scan* sc, const HitDev& h, dwpa_hit& o) {
 }
 
 void scan_mark_cracked(dwpa_scan* sc, uint32_t input_line) {
-    if (input_line < sc->status.size() && sc->status[input_line] == 0) sc->cracked[sc->line_of[input_line]] = 1;
+    if (input_line < sc->status.size() && sc->status[input_line] == 0 && !sc->cracked[sc->line_of[input_line]]) {
+        sc->cracked[sc->line_of[input_line]] = 1;
+        sc->mg_dirty = true;
+    }
 }
 uint32_t scan_batch_cap(const dwpa_scan* sc) { return sc->batch_cap; }
 Batch& scan_batch_ref(dwpa_scan* sc) { return sc->batch; }
@@ -732,6 +809,7 @@ int dwpa_scan_load_numeric(dwpa_scan* scan, uint64_t first, uint32_t count, uint
 }
 int dwpa_scan_pbkdf2(dwpa_scan* scan, int group, void* hip_stream) { return scan_pbkdf2(scan, group, hip_stream); }
 int dwpa_scan_verify(dwpa_scan* scan, int group, void* hip_stream) { return scan_verify(scan, group, hip_stream); }
+int dwpa_scan_run(dwpa_scan* scan, void* hip_stream) { return scan_run(scan, hip_stream); }
 int dwpa_scan_hits(dwpa_scan* scan, dwpa_hit* out, size_t cap, size_t* nhits, void* hip_stream) {
     if (!scan || !nhits || (!out && cap)) return DWPA_E_ARG;
     std::vector<HitDev> raw;

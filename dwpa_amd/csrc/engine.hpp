@@ -39,6 +39,7 @@ int scan_load_dict(dwpa_scan* sc, const uint64_t* off, const uint8_t* bytes, uin
 int scan_load_numeric(dwpa_scan* sc, uint64_t first, uint32_t count, uint32_t digits, void* stream);
 int scan_pbkdf2(dwpa_scan* sc, int group, void* stream);
 int scan_verify(dwpa_scan* sc, int group, void* stream);
+int scan_run(dwpa_scan* sc, void* stream);
 int scan_hits_raw(dwpa_scan* sc, std::vector<HitDev>& out, void* stream);
 void hit_to_public(const dwpa_scan* sc, const HitDev& h, dwpa_hit& o);
 void scan_mark_cracked(dwpa_scan* sc, uint32_t input_line);

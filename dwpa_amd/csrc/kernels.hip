@@ -90,6 +90,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     pbkdf2_body_ms(mid, cap, count, pool, sref, pmk);
 }
 
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_mg(const uint32_t* __restrict__ mid, uint32_t cap,
+                                                   const uint32_t* __restrict__ counter, uint32_t ngroups,
+                                                   const uint32_t* __restrict__ salt,
+                                                   const uint32_t* __restrict__ gsalt, uint32_t* __restrict__ pmk,
+                                                   uint32_t pstride) {
+    pbkdf2_body_mg(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride);
+}
+
 // Slot PMKs from the derived unique (ESSID, key) PMKs or from caller-supplied PMKs:
 // src[i] = u -> upmk[.][u];  src[i] = GATHER_CALLER | c -> cpmk[c][0..7] (check_key_m22000's $pmk, common.php:178).
 __global__ __launch_bounds__(256) void k_gather_pmk(const uint32_t* __restrict__ upmk, uint32_t ucap,
@@ -158,6 +166,8 @@ __device__ __forceinline__ void sha1_outer20(const uint32_t opad[5], const uint3
 __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk, uint32_t cap,
                                                 const uint64_t* __restrict__ ids, const uint32_t* __restrict__ counter,
                                                 const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t line_base,
+                                                const uint32_t* __restrict__ line_list,
+                                                const uint32_t* __restrict__ line_poff, uint32_t pstride,
                                                 const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                 uint32_t* __restrict__ hitcnt, uint32_t hitcap, uint32_t use_aes) {
@@ -172,8 +182,8 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
     if (segi >= nsegs) return;
     SegDev sg;
     if (segs) sg = segs[segi];
-    else {  // implicit: every 64-slot chunk of the batch against line line_base + blockIdx.y
-        sg.line = line_base + blockIdx.y;
+    else {  // implicit: every 64-slot chunk of the batch against line line_base + blockIdx.y (or line_list[y])
+        sg.line = line_list ? line_list[line_base + blockIdx.y] : line_base + blockIdx.y;
         sg.slot = segi * 64;
         sg.count = 64;
     }
@@ -182,10 +192,12 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
     const bool active = lane < sg.count && slot < n;
     if (!__any(active)) return;
     const LineDev L = lines[sg.line];
+    // PMKs of multi-group launches: the line's ESSID group owns slots [poff, poff + cap) of a pstride-wide array
+    const uint32_t poff = line_poff ? line_poff[sg.line] : 0u;
 
     uint32_t p[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) p[k] = active ? pmk[(size_t)k * cap + slot] : 0u;
+    for (int k = 0; k < 8; k++) p[k] = active ? pmk[(size_t)k * pstride + poff + slot] : 0u;
     const uint64_t cand = active ? (ids ? ids[slot] : (uint64_t)slot) : 0ull;
 
     uint32_t kb[16];
@@ -378,10 +390,22 @@ hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,
                          const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt, uint32_t hitcap,
-                         bool use_aes, hipStream_t s) {
+                         bool use_aes, hipStream_t s, const uint32_t* line_list, const uint32_t* line_poff,
+                         uint32_t pstride) {
     if (nsegs == 0 || nlines == 0) return hipSuccess;
+    if (!pstride) pstride = cap;
     hipLaunchKernelGGL(k_verify, dim3(cdiv(nsegs, 4), segs ? 1 : nlines), dim3(256), 0, s, pmk, cap, ids, counter, segs,
-                       nsegs, line_base, lines, pool, atts, hits, hitcnt, hitcap, use_aes ? 1u : 0u);
+                       nsegs, line_base, line_list, line_poff, pstride, lines, pool, atts, hits, hitcnt, hitcap,
+                       use_aes ? 1u : 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_pbkdf2_mg_plain(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
+                                  const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
+                                  hipStream_t s) {
+    if (ngroups == 0 || cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pbkdf2_mg, dim3(cdiv((uint64_t)ngroups * cap, 256), 2), dim3(256), 0, s, mid, cap, counter,
+                       ngroups, salt, gsalt, pmk, pstride);
     return hipGetLastError();
 }
 

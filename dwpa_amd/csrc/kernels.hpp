@@ -24,6 +24,14 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
                             const uint32_t* sref, uint32_t* pmk, hipStream_t s);
 hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                   const uint32_t* sref, uint32_t* pmk, hipStream_t s);
+// many ESSID groups x one batch per launch (cap % 64 == 0): gsalt[c] = {salt word offset, nsalt} of chunk group c,
+// PMK word k of (c, slot) at pmk[k * pstride + c * cap + slot]
+hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
+                            const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
+                            hipStream_t s);
+hipError_t launch_pbkdf2_mg_plain(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
+                                  const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
+                                  hipStream_t s);
 constexpr uint32_t GATHER_CALLER = 0x80000000u;
 hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t* cpmk, const uint32_t* src,
                              uint32_t n, uint32_t* pmk, uint32_t cap, hipStream_t s);
@@ -31,6 +39,7 @@ hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,
                          const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt, uint32_t hitcap,
-                         bool use_aes, hipStream_t s);
+                         bool use_aes, hipStream_t s, const uint32_t* line_list = nullptr,
+                         const uint32_t* line_poff = nullptr, uint32_t pstride = 0);
 
 }  // namespace dwpa

@@ -91,4 +91,24 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
     store_block(pmk, cap, s, blk, t);
 }
 
+// Many ESSID groups x one candidate batch in one launch (scan work units with many ESSIDs):
+// lane i -> chunk group c = i / cap, slot s = i % cap.  cap is a multiple of 64, so c is wave-uniform and the
+// salt entry is read with scalar loads.  gsalt[c] = {word offset of the group's [2][nsalt][16] salt blocks, nsalt};
+// PMK word k of (c, s) lands at pmk[k * pstride + c * cap + s].
+__device__ __forceinline__ void pbkdf2_body_mg(const uint32_t* __restrict__ mid, uint32_t cap,
+                                               const uint32_t* __restrict__ counter, uint32_t ngroups,
+                                               const uint32_t* __restrict__ salt, const uint32_t* __restrict__ gsalt,
+                                               uint32_t* __restrict__ pmk, uint32_t pstride) {
+    const uint32_t blk = blockIdx.y;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(i / cap);
+    const uint32_t s = i - c * cap;
+    if (c >= ngroups || s >= min(*counter, cap)) return;
+    uint32_t hi[5], ho[5], t[5];
+    load_mid(mid, cap, s, hi, ho);
+    const uint32_t off = gsalt[2 * c], nsalt = gsalt[2 * c + 1];
+    pbkdf2_lane(hi, ho, salt + off + (size_t)blk * nsalt * 16, nsalt, t);
+    store_block(pmk + (size_t)c * cap, pstride, s, blk, t);
+}
+
 }  // namespace dwpa

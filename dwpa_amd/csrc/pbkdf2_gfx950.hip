@@ -20,3 +20,12 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                                                                      uint32_t* __restrict__ pmk) {
     dwpa::pbkdf2_body_ms(mid, cap, count, pool, sref, pmk);
 }
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_mg(const uint32_t* __restrict__ mid, uint32_t cap,
+                                                                     const uint32_t* __restrict__ counter,
+                                                                     uint32_t ngroups,
+                                                                     const uint32_t* __restrict__ salt,
+                                                                     const uint32_t* __restrict__ gsalt,
+                                                                     uint32_t* __restrict__ pmk, uint32_t pstride) {
+    dwpa::pbkdf2_body_mg(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride);
+}

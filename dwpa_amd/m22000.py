@@ -233,6 +233,11 @@ class Scan:
     def verify(self, group: int = 0, stream: int = 0):
         L.check(self._lib.dwpa_scan_verify(self._h, group, stream), "scan_verify")
 
+    def run(self, stream: int = 0):
+        """PBKDF2 + verify of the loaded batch for every ESSID group with an uncracked line, many groups per
+        launch (dwpa_scan_run)."""
+        L.check(self._lib.dwpa_scan_run(self._h, stream), "scan_run")
+
     def loaded(self, stream: int = 0) -> int:
         c = ctypes.c_uint32(0)
         L.check(self._lib.dwpa_scan_loaded(self._h, ctypes.byref(c), stream), "scan_loaded")

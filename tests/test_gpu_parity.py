@@ -225,3 +225,46 @@ def test_scan_rules_device_resident():
         essid = nets[h["line"]][0]
         assert h["pmk"] == S.pmk(R.apply(R.parse(rules[ri]), base[wi]), essid)
     sc.close()
+
+
+def test_scan_run_many_essids_matches_per_group():
+    """dwpa_scan_run: many ESSID groups per PBKDF2 launch (1- and 2-block salts in one launch, several launches
+    when groups x batch exceeds 4M slots) gives exactly the per-group path's hits, and every hit's PMK is the
+    oracle's."""
+    from dwpa_amd.device import Dictionary
+    rng = random.Random(12)
+    words = [S.random_psk(rng, 8, 24) for _ in range(3000)]
+    d = Dictionary.from_words(words)
+    lines, plants = [], []
+    for e in range(12):
+        essid = bytes(rng.randrange(0x21, 0x7f) for _ in range((1, 9, 32, 52, 60)[e % 5]))
+        _, ap, sta, an, sn = S.random_net(rng)
+        for k in range(1 + e % 3):
+            wi = rng.randrange(len(words))
+            kind = (e + k) % 4
+            if kind == 0:
+                lines.append(S.pmkid_line(words[wi], essid, rng.randbytes(6), sta))
+            else:
+                lines.append(S.eapol_line(words[wi], essid, ap, sta, an, sn, kind, rng.randint(-5, 5),
+                                          rng.choice(["LE", "BE"]), rng=rng))
+            plants.append((len(lines) - 1, wi, essid))
+    lines.append(S.pmkid_line(b"not-in-the-dictionary", b"lonely", rng.randbytes(6), rng.randbytes(6)))
+    results = []
+    for mode in ("run", "per_group"):
+        sc = dwpa_amd.Scan(lines, nc=8, batch=1 << 20)  # 4M-slot launches hold 4 groups: 3 launches for 13
+        assert sc.groups == 13
+        sc.load_dict(d.off.ptr, d.data.ptr, 0, len(words))
+        if mode == "run":
+            sc.run()
+        else:
+            for g in range(sc.groups):
+                sc.pbkdf2(g)
+                sc.verify(g)
+        results.append(sorted((h["line"], h["cand"], h["nc"], h["endian"], h["pmk"]) for h in sc.hits()))
+        sc.close()
+    assert results[0] == results[1]
+    found = {(h[0], h[1]) for h in results[0]}
+    assert {(li, wi) for li, wi, _ in plants} <= found
+    for li, cand, nc, endian, pmk in results[0]:
+        essid = next(e for l, _, e in plants if l == li)
+        assert pmk == O.c_pbkdf2(words[cand], essid)
