@@ -5,16 +5,20 @@
 // contiguous keyspace shards, no collective -- shards never exchange data; hits are gathered on the host).
 // bench.py instead runs one process per GPU (torch.distributed launch) and uses the scan API on its own device.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
 #include <string_view>
 #include <unordered_map>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -26,6 +30,19 @@
 namespace dwpa {
 
 static thread_local hipError_t t_last_hip = hipSuccess;
+
+// DWPA_TRACE=1: host phase timings of the check path on stderr (what the PCIe-inclusive FFI rate is made of).
+struct PhaseTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t;
+    PhaseTrace() : on(getenv("DWPA_TRACE") && *getenv("DWPA_TRACE") == '1'), t(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[dwpa] %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    }
+};
 
 #define HIPCHK(x)                                                                                            \
     do {                                                                                                     \
@@ -153,7 +170,7 @@ static void pmk_bytes(const uint32_t w[8], uint8_t out[32]) {
 // explicit keys -> slots (server-side check path and dwpa_pbkdf2_pmk)
 // ---------------------------------------------------------------------------------------------------------
 struct Slot {
-    const std::string* key;   // bytes hashed (after hc_unhex)
+    std::string_view key;     // bytes hashed (after hc_unhex): the caller's buffer or a decoded copy
     uint32_t job;
     uint32_t ordinal;         // index among the job's non-null keys
     const std::string* essid;
@@ -165,6 +182,7 @@ struct Slot {
 static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
                      const std::vector<const uint8_t*>& job_pmk, const std::vector<uint32_t>& job_line,
                      const TableBuilder* tb, bool verify, std::vector<HitDev>& hits_out, uint8_t* pmk_out) {
+    PhaseTrace tr;
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
     RCHK(d.batch.reserve(n, n));
@@ -172,7 +190,7 @@ static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t
     // every net of an ESSID, common.php:879-902); each slot then gathers its PMK from them or from the caller's
     // $pmk.  Slots arrive sorted by ESSID, so duplicates are found within each ESSID run.
     std::vector<uint32_t> src(n), sref, spool, cpmk;
-    std::vector<const std::string*> ukeys;
+    std::vector<std::string_view> ukeys;
     std::unordered_map<std::string_view, uint32_t> seen;
     const std::string* cur = nullptr;
     uint32_t cur_ref = 0;
@@ -195,7 +213,7 @@ static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t
             spool.push_back(nb);
             spool.insert(spool.end(), sb.begin(), sb.end());
         }
-        auto ins = seen.try_emplace(std::string_view(*sl.key), (uint32_t)ukeys.size());
+        auto ins = seen.try_emplace(sl.key, (uint32_t)ukeys.size());
         if (ins.second) {
             ukeys.push_back(sl.key);
             sref.push_back(cur_ref);
@@ -203,36 +221,68 @@ static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t
         src[i] = ins.first->second;
     }
     const uint32_t nu = (uint32_t)ukeys.size();
+    tr.mark("  dedup (ESSID, key)");
     RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
-    if (nu) {
+    // Host staging first: a hipMemcpyAsync from pageable memory queued behind a running kernel blocks the host
+    // until that kernel ends, so every upload goes ahead of the launches.
+    std::vector<uint64_t> off(nu + 1);
+    std::vector<uint8_t> bv;
+    {
         // unique keys -> offsets/bytes (back to back: k_prep_dict derives len = off[i+1] - off[i])
-        std::vector<uint64_t> off(nu + 1);
-        std::string bytes;
+        size_t total = 0;
+        for (uint32_t u = 0; u < nu; u++) total += ukeys[u].size();
+        bv.resize(total + 8, 0);
+        size_t pos = 0;
         for (uint32_t u = 0; u < nu; u++) {
-            off[u] = bytes.size();
-            bytes += *ukeys[u];
+            off[u] = pos;
+            memcpy(bv.data() + pos, ukeys[u].data(), ukeys[u].size());
+            pos += ukeys[u].size();
         }
-        off[nu] = bytes.size();
-        bytes.append(8, '\0');
-        std::vector<uint8_t> bv(bytes.begin(), bytes.end());
+        off[nu] = pos;
+    }
+    // ids = key ordinals (selects the PHP attempt list of each key)
+    std::vector<uint64_t> ids(n);
+    for (uint32_t i = 0; i < n; i++) ids[i] = slots[b + i].ordinal;
+    // segments: runs of consecutive slots of one job, <= 64 each.  EAPOL lines with wide nonce windows go to the
+    // attempt-parallel kernel (a wave per key, lanes = attempts), the rest to the key-parallel one.
+    std::vector<SegDev> segs;
+    size_t nkey = 0;
+    if (verify) {
+        for (int pass = 0; pass < 2; pass++) {
+            for (uint32_t i = 0; i < n;) {
+                uint32_t j = i;
+                const uint32_t job = slots[b + i].job;
+                while (j < n && slots[b + j].job == job && j - i < 64) j++;
+                const uint32_t li = job_line[job];
+                const LineDev& L = tb->lines[li];
+                const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
+                if (!tb->never[li] && att == (pass == 1)) segs.push_back({li, i, j - i, 0});
+                i = j;
+            }
+            if (pass == 0) nkey = segs.size();
+        }
+    }
+    if (nu) {
         RCHK(upload(d.koff, off, s));
         RCHK(upload(d.kbytes, bv, s));
         RCHK(upload(d.salt, spool, s));
         RCHK(upload(d.sref, sref, s));
+    }
+    RCHK(upload(d.cpmk, cpmk, s));
+    RCHK(upload(d.src, src, s));
+    HIPCHK(hipMemcpyAsync(d.batch.ids.p, ids.data(), n * 8, hipMemcpyHostToDevice, s));
+    if (!segs.empty()) RCHK(upload(d.segs, segs, s));
+    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
+    tr.mark("  stage+upload");
+
+    if (nu) {
         HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, nu, 0, 0xffffffffu,
                                 (uint32_t*)d.batch.mid.p, nullptr, nullptr, d.batch.cap, false, s));
         HIPCHK(launch_pbkdf2_ms((const uint32_t*)d.batch.mid.p, d.batch.cap, nu, (const uint32_t*)d.salt.p,
                                 (const uint32_t*)d.sref.p, (uint32_t*)d.upmk.p, s));
     }
-    RCHK(upload(d.cpmk, cpmk, s));
-    RCHK(upload(d.src, src, s));
     HIPCHK(launch_gather_pmk((const uint32_t*)d.upmk.p, d.batch.cap, (const uint32_t*)d.cpmk.p,
                              (const uint32_t*)d.src.p, n, (uint32_t*)d.batch.pmk.p, d.batch.cap, s));
-    // ids = key ordinals (selects the PHP attempt list of each key)
-    std::vector<uint64_t> ids(n);
-    for (uint32_t i = 0; i < n; i++) ids[i] = slots[b + i].ordinal;
-    HIPCHK(hipMemcpyAsync(d.batch.ids.p, ids.data(), n * 8, hipMemcpyHostToDevice, s));
-
     if (pmk_out) {
         std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
         HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, s));
@@ -243,34 +293,24 @@ static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t
             pmk_bytes(pw, pmk_out + 32 * (size_t)(b + i));
         }
     }
-    if (!verify) {
+    if (!verify || segs.empty()) {
         HIPCHK(hipStreamSynchronize(s));  // host staging vectors die with this frame
         return 0;
     }
-
-    // segments: runs of consecutive slots of one job, <= 64 each
-    std::vector<SegDev> segs;
-    for (uint32_t i = 0; i < n;) {
-        uint32_t j = i;
-        const uint32_t job = slots[b + i].job;
-        while (j < n && slots[b + j].job == job && j - i < 64) j++;
-        if (!tb->never[job_line[job]]) segs.push_back({job_line[job], i, j - i, 0});
-        i = j;
-    }
-    if (segs.empty()) {
-        HIPCHK(hipStreamSynchronize(s));
-        return 0;
-    }
-    RCHK(upload(d.segs, segs, s));
-    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
     uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
     HIPCHK(launch_verify((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, nullptr,
-                         (const SegDev*)d.segs.p, (uint32_t)segs.size(), 0, 1, (const LineDev*)d.lines.p,
+                         (const SegDev*)d.segs.p, (uint32_t)nkey, 0, 1, (const LineDev*)d.lines.p,
                          (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt,
                          d.batch.hitcap, tb->any_aes, s));
+    HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p,
+                             (const SegDev*)d.segs.p + nkey, (uint32_t)(segs.size() - nkey),
+                             (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p,
+                             (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, tb->any_aes, s));
+    tr.mark("  launches queued");
     uint32_t nh = 0;
     HIPCHK(hipMemcpyAsync(&nh, hitcnt, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    tr.mark("  device wait");
     if (nh > d.batch.hitcap) return DWPA_E_OVERFLOW;
     size_t old = hits_out.size();
     hits_out.resize(old + nh);
@@ -303,11 +343,13 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     HIPCHK(hipSetDevice(d.id));
     RCHK(device_stream(d));
 
+    PhaseTrace tr;
     TableBuilder tb;
     std::vector<ParsedLine> parsed(njobs);
     std::vector<uint32_t> job_line(njobs, 0);
     std::vector<const uint8_t*> job_pmk(njobs, nullptr);
-    std::vector<std::vector<std::string>> keys(njobs);
+    std::vector<std::vector<std::string_view>> keys(njobs);
+    std::deque<std::string> unhexed;  // decoded $HEX[] keys (stable addresses)
     std::vector<std::vector<uint32_t>> key_index(njobs);
     std::vector<Slot> slots;
     for (size_t j = 0; j < njobs; j++) {
@@ -322,9 +364,12 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         for (size_t k = 0; k < jobs[j].nkeys; k++) {
             const dwpa_bytes& kb = jobs[j].keys[k];
             if (!kb.ptr) continue;  // is_null($key): skipped (common.php:172,240)
-            std::string key((const char*)kb.ptr, kb.len);
-            if (starts_hex(kb.ptr, kb.len)) key = hc_unhex(key);
-            keys[j].push_back(std::move(key));
+            std::string_view key((const char*)kb.ptr, kb.len);
+            if (starts_hex(kb.ptr, kb.len)) {
+                unhexed.push_back(hc_unhex(std::string(key)));
+                key = unhexed.back();
+            }
+            keys[j].push_back(key);
             key_index[j].push_back((uint32_t)k);
         }
         rcs[j] = DWPA_MISS;
@@ -333,17 +378,26 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         job_pmk[j] = jobs[j].pmk;
         if (tb.never[job_line[j]]) continue;
     }
+    tr.mark("parse+keys+tables");
+    // slots grouped by ESSID (jobs in input order within an ESSID, keys in order within a job): the unique
+    // (ESSID, key) pairs of run_slots are found per ESSID run
+    std::unordered_map<std::string_view, uint32_t> essid_id;
+    std::vector<std::vector<uint32_t>> by_essid;
+    size_t nslots = 0;
     for (size_t j = 0; j < njobs; j++) {
         if (rcs[j] != DWPA_MISS || keys[j].empty() || tb.never[job_line[j]]) continue;
-        for (uint32_t o = 0; o < keys[j].size(); o++)
-            slots.push_back({&keys[j][o], (uint32_t)j, o, &parsed[j].essid, !(o == 0 && job_pmk[j])});
+        auto ins = essid_id.try_emplace(std::string_view(parsed[j].essid), (uint32_t)by_essid.size());
+        if (ins.second) by_essid.emplace_back();
+        by_essid[ins.first->second].push_back((uint32_t)j);
+        nslots += keys[j].size();
     }
-    if (slots.empty()) return 0;
-    std::stable_sort(slots.begin(), slots.end(), [](const Slot& a, const Slot& b) {
-        int c = a.essid->compare(*b.essid);
-        if (c) return c < 0;
-        return a.pbkdf2 > b.pbkdf2;
-    });
+    if (!nslots) return 0;
+    slots.reserve(nslots);
+    for (const auto& js : by_essid)
+        for (uint32_t j : js)
+            for (uint32_t o = 0; o < keys[j].size(); o++)
+                slots.push_back({keys[j][o], j, o, &parsed[j].essid, !(o == 0 && job_pmk[j])});
+    tr.mark("slots");
     hipStream_t s = d.stream;
     RCHK(upload(d.lines, tb.lines, s));
     RCHK(upload(d.atts, tb.atts, s));
@@ -353,6 +407,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     const size_t chunk = default_batch();
     for (size_t b = 0; b < slots.size(); b += chunk)
         RCHK(run_slots(d, slots, b, std::min(slots.size(), b + chunk), job_pmk, job_line, &tb, true, hits, nullptr));
+    tr.mark("device (run_slots)");
 
     // first key in input order wins, then the first attempt in PHP order (common.php:186,280-289)
     std::map<uint32_t, size_t> line_job;
@@ -403,7 +458,7 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
     std::vector<Slot> slots(nkeys);
     for (size_t i = 0; i < nkeys; i++) {
         if (keys[i].ptr) ks[i].assign((const char*)keys[i].ptr, keys[i].len);
-        slots[i] = {&ks[i], 0, (uint32_t)i, &es, true};
+        slots[i] = {std::string_view(ks[i]), 0, (uint32_t)i, &es, true};
     }
     std::vector<HitDev> hits;
     const size_t chunk = default_batch();
@@ -442,7 +497,7 @@ struct dwpa_scan {
         uint32_t g0, ngroups, list0, nlines;
     };
     bool mg_dirty = true;
-    uint32_t mg_per = 0;                   // groups per launch
+    uint32_t mg_stride = 0;                // PMK SoA stride = (most groups in one launch) x batch_cap
     std::vector<Chunk> mg_chunks;
     std::vector<uint32_t> mg_gsalt_h, mg_list_h, mg_poff_h;
     dwpa::DevBuf mg_pmk, mg_gsalt, mg_list, mg_poff;
@@ -568,39 +623,49 @@ int scan_verify(dwpa_scan* sc, int group, void* stream) {
     return 0;
 }
 
-// Candidate slots per multi-group PBKDF2 launch (x2 lanes for the two output blocks): 4M slots fill all 1024 SIMDs
-// at 8 waves with room to spare, and bound the group-major PMK buffer at 128 MiB.
-constexpr uint64_t MG_SLOTS = 1u << 22;
+// Candidate slots per multi-group PBKDF2 launch (x2 lanes for the two output blocks).  The 1024 SIMDs hold 512K
+// lanes at 8 waves, and every lane runs the same 4096 iterations, so a launch takes ceil(lanes / 512K) wave
+// rounds: 16M slots = 64 rounds keeps a partial last round under ~2 %, and bounds the group-major PMK buffer
+// at 512 MiB of the 288 GB.
+constexpr uint64_t MG_SLOTS = 1u << 24;
 
 static int scan_mg_rebuild(dwpa_scan* sc, hipStream_t s) {
     const uint32_t cap = sc->batch_cap;
     HIPCHK(hipStreamSynchronize(s));  // the previous tables may still be read by queued launches
-    sc->mg_per = (uint32_t)std::max<uint64_t>(1, MG_SLOTS / cap);
+    const uint32_t per = (uint32_t)std::max<uint64_t>(1, MG_SLOTS / cap);
+    std::vector<const ScanGroup*> act;
+    for (const ScanGroup& g : sc->groups) {
+        bool any = false;
+        for (uint32_t l = g.line_begin; l < g.line_end; l++) any |= !sc->cracked[l];
+        if (any) act.push_back(&g);
+    }
+    // spread the active groups evenly over the launches: sizes differ by at most one (no small last launch)
+    const uint32_t nact = (uint32_t)act.size();
+    const uint32_t launches = (nact + per - 1) / per;
     sc->mg_chunks.clear();
     sc->mg_gsalt_h.clear();
     sc->mg_list_h.clear();
     sc->mg_poff_h.assign(std::max<size_t>(sc->tb.lines.size(), 1), 0);
-    uint32_t in_chunk = 0, most = 0;
-    for (const ScanGroup& g : sc->groups) {
-        bool any = false;
-        for (uint32_t l = g.line_begin; l < g.line_end; l++) any |= !sc->cracked[l];
-        if (!any) continue;
-        if (in_chunk == 0)
-            sc->mg_chunks.push_back({(uint32_t)sc->mg_gsalt_h.size() / 2, 0, (uint32_t)sc->mg_list_h.size(), 0});
-        dwpa_scan::Chunk& ch = sc->mg_chunks.back();
-        sc->mg_gsalt_h.push_back(g.salt_off);
-        sc->mg_gsalt_h.push_back(g.nsalt);
-        for (uint32_t l = g.line_begin; l < g.line_end; l++) {
-            if (sc->cracked[l]) continue;
-            sc->mg_list_h.push_back(l);
-            sc->mg_poff_h[l] = in_chunk * cap;
+    uint32_t most = 0, next = 0;
+    for (uint32_t c = 0; c < launches; c++) {
+        const uint32_t size = nact / launches + (c < nact % launches ? 1u : 0u);
+        dwpa_scan::Chunk ch{(uint32_t)sc->mg_gsalt_h.size() / 2, size, (uint32_t)sc->mg_list_h.size(), 0};
+        for (uint32_t k = 0; k < size; k++) {
+            const ScanGroup& g = *act[next++];
+            sc->mg_gsalt_h.push_back(g.salt_off);
+            sc->mg_gsalt_h.push_back(g.nsalt);
+            for (uint32_t l = g.line_begin; l < g.line_end; l++) {
+                if (sc->cracked[l]) continue;
+                sc->mg_list_h.push_back(l);
+                sc->mg_poff_h[l] = k * cap;
+            }
         }
-        ch.ngroups++;
         ch.nlines = (uint32_t)sc->mg_list_h.size() - ch.list0;
-        most = std::max(most, ch.ngroups);
-        if (++in_chunk == sc->mg_per) in_chunk = 0;
+        most = std::max(most, size);
+        sc->mg_chunks.push_back(ch);
     }
-    if (most) RCHK(sc->mg_pmk.ensure((size_t)PMK_WORDS * most * cap * 4));
+    sc->mg_stride = most * cap;
+    if (most) RCHK(sc->mg_pmk.ensure((size_t)PMK_WORDS * sc->mg_stride * 4));
     RCHK(upload(sc->mg_gsalt, sc->mg_gsalt_h, s));
     RCHK(upload(sc->mg_list, sc->mg_list_h, s));
     RCHK(upload(sc->mg_poff, sc->mg_poff_h, s));
@@ -614,8 +679,10 @@ int scan_run(dwpa_scan* sc, void* stream) {
     hipStream_t s = as_stream(stream);
     if (sc->mg_dirty) RCHK(scan_mg_rebuild(sc, s));
     const uint32_t cap = sc->batch_cap;
-    const uint32_t pstride = sc->mg_per * cap;
+    const uint32_t pstride = sc->mg_stride;
     for (const dwpa_scan::Chunk& ch : sc->mg_chunks) {
+        // every (group, slot) PMK of this launch must land inside mg_pmk: [8][pstride] words
+        if ((uint64_t)ch.ngroups * cap > pstride || sc->mg_pmk.n < (size_t)PMK_WORDS * pstride * 4) return DWPA_E_ARG;
         HIPCHK(launch_pbkdf2_mg((const uint32_t*)sc->batch.mid.p, cap, (const uint32_t*)sc->batch.counters.p,
                                 ch.ngroups, (const uint32_t*)sc->salt.p, (const uint32_t*)sc->mg_gsalt.p + 2 * ch.g0,
                                 (uint32_t*)sc->mg_pmk.p, pstride, s));

@@ -163,6 +163,156 @@ __device__ __forceinline__ void sha1_outer20(const uint32_t opad[5], const uint3
     sha1_compress(out, m);
 }
 
+// Block b of an attempt's PRF stream: shared words with the attempt's two patched words substituted
+// (LineDev.patch_w0/_w1; NO_PATCH never matches, so explicit per-attempt blocks pass through unchanged).
+__device__ __forceinline__ void att_block(const uint32_t* __restrict__ w, uint32_t b, uint32_t pw0, uint32_t pw1,
+                                          uint32_t v0, uint32_t v1, uint32_t m[16]) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const uint32_t idx = b * 16 + j;
+        uint32_t x = w[idx];
+        x = idx == pw0 ? v0 : x;
+        x = idx == pw1 ? v1 : x;
+        m[j] = x;
+    }
+}
+
+// Everything of an EAPOL check that depends on the PMK but not on the nonce-correction attempt.
+struct EapolKey {
+    uint32_t op1[5], pre1[5];  // keyver 1/2: HMAC-SHA1(PMK) opad midstate, inner state after the shared PRF prefix
+    uint32_t op2[8], pre2[8];  // keyver 3: same for HMAC-SHA256
+};
+
+__device__ __forceinline__ void eapol_key(const LineDev& L, const uint32_t* __restrict__ pool, const uint32_t p[8],
+                                          EapolKey& K) {
+    uint32_t kb[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
+    if (L.keyver != 3) {
+        uint32_t ip1[5];
+        sha1_hmac_mid(kb, ip1, K.op1);
+#pragma unroll
+        for (int k = 0; k < 5; k++) K.pre1[k] = ip1[k];
+        sha1_blocks(K.pre1, pool + L.pre_off, L.pre_nblk);
+    } else {
+        uint32_t ip2[8];
+        sha256_hmac_mid(kb, ip2, K.op2);
+#pragma unroll
+        for (int k = 0; k < 8; k++) K.pre2[k] = ip2[k];
+        sha256_blocks(K.pre2, pool + L.pre_off, L.pre_nblk);
+    }
+}
+
+// MIC of one nonce-correction attempt (common.php:250-300): PRF-512 (keyver 1/2: HMAC-SHA1, first 20 bytes;
+// keyver 3: KDF-SHA256) -> KCK -> HMAC-MD5 (1), HMAC-SHA1 (2) or AES-128-CMAC (3) over the EAPOL frame.
+__device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __restrict__ pool, const EapolKey& K,
+                                          const AttDev& at, const uint32_t* te, uint32_t mic[4]) {
+    const uint32_t* aw = pool + at.blk_off;
+    if (L.keyver != 3) {
+        uint32_t st[5], ptk[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) st[k] = K.pre1[k];
+        for (uint32_t b = 0; b < at.nblk; b++) {
+            uint32_t m[16];
+            att_block(aw, b, L.patch_w0, L.patch_w1, at.v0, at.v1, m);
+            sha1_compress(st, m);
+        }
+        sha1_outer20(K.op1, st, ptk);  // PTK[0..19]; KCK = PTK[0..15]
+        if (L.keyver == 2) {
+            uint32_t k2[16], mi[5], mo[5];
+#pragma unroll
+            for (int k = 0; k < 16; k++) k2[k] = k < 4 ? ptk[k] : 0u;
+            sha1_hmac_mid(k2, mi, mo);
+            sha1_blocks(mi, pool + L.mic_off, L.mic_nblk);
+            uint32_t o[5];
+            sha1_outer20(mo, mi, o);
+            mic[0] = o[0]; mic[1] = o[1]; mic[2] = o[2]; mic[3] = o[3];
+        } else {
+            uint32_t k1[16], mi[4], mo[4];
+#pragma unroll
+            for (int k = 0; k < 16; k++) k1[k] = k < 4 ? bswap32(ptk[k]) : 0u;
+            md5_hmac_mid(k1, mi, mo);
+            md5_blocks(mi, pool + L.mic_off, L.mic_nblk);
+            uint32_t m[16] = {mi[0], mi[1], mi[2], mi[3], 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 640u, 0};
+            md5_compress(mo, m);
+            mic[0] = mo[0]; mic[1] = mo[1]; mic[2] = mo[2]; mic[3] = mo[3];
+        }
+    } else {
+        uint32_t st[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) st[k] = K.pre2[k];
+        for (uint32_t b = 0; b < at.nblk; b++) {
+            uint32_t m[16];
+            att_block(aw, b, L.patch_w0, L.patch_w1, at.v0, at.v1, m);
+            sha256_compress(st, m);
+        }
+        uint32_t m[16] = {st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7],
+                          0x80000000u, 0, 0, 0, 0, 0, 0, 768u};
+        uint32_t ptk[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) ptk[k] = K.op2[k];
+        sha256_compress(ptk, m);
+        // AES-128-CMAC(KCK = PTK[0..15], EAPOL)  (common.php:72-112)
+        uint32_t rk[44];
+        aes128_expand(te, ptk, rk);
+        uint32_t Lb[4] = {0, 0, 0, 0}, K1[4], K2[4];
+        aes128_encrypt(te, rk, Lb);
+        cmac_dbl(Lb, K1);
+        cmac_dbl(K1, K2);
+        uint32_t c[4] = {0, 0, 0, 0};
+        const uint32_t* eb = pool + L.mic_off;
+        for (uint32_t b = 0; b < L.mic_nblk; b++) {
+            const bool last = b + 1 == L.mic_nblk;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                uint32_t v = eb[4 * b + k];
+                if (last) v ^= L.cmac_complete ? K1[k] : K2[k];
+                c[k] ^= v;
+            }
+            aes128_encrypt(te, rk, c);
+        }
+        mic[0] = c[0]; mic[1] = c[1]; mic[2] = c[2]; mic[3] = c[3];
+    }
+}
+
+__device__ __forceinline__ bool mic_match(const LineDev& L, const uint32_t mic[4]) {
+    return mic[0] == L.target[0] && mic[1] == L.target[1] && mic[2] == L.target[2] && mic[3] == L.target[3];
+}
+
+// hit reporting: one ballot, one atomic per wave, append to the small hit buffer
+__device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t cand, uint32_t line, uint32_t att,
+                                            const uint32_t p[8], HitDev* __restrict__ hits,
+                                            uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
+    const uint64_t m = __ballot(found);
+    if (!m) return;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(hitcnt, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)leader);
+    if (found) {
+        const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (idx < hitcap) {
+            HitDev h;
+            h.cand = cand;
+            h.line = line;
+            h.attempt = att;
+#pragma unroll
+            for (int k = 0; k < 8; k++) h.pmk[k] = p[k];
+            hits[idx] = h;
+        }
+    }
+}
+
+__device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te, uint32_t use_aes) {
+    if (use_aes) {
+        for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) te[k] = AES_TABLES.te0[k];
+        __syncthreads();
+    }
+    return te;
+}
+
+// Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
+// wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
 __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk, uint32_t cap,
                                                 const uint64_t* __restrict__ ids, const uint32_t* __restrict__ counter,
                                                 const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t line_base,
@@ -171,11 +321,8 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
                                                 const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                 uint32_t* __restrict__ hitcnt, uint32_t hitcap, uint32_t use_aes) {
-    __shared__ uint32_t te[256];
-    if (use_aes) {
-        for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) te[k] = AES_TABLES.te0[k];
-        __syncthreads();
-    }
+    __shared__ uint32_t te_lds[256];
+    const uint32_t* te = aes_table_lds(te_lds, use_aes);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t segi = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -200,14 +347,13 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
     for (int k = 0; k < 8; k++) p[k] = active ? pmk[(size_t)k * pstride + poff + slot] : 0u;
     const uint64_t cand = active ? (ids ? ids[slot] : (uint64_t)slot) : 0ull;
 
-    uint32_t kb[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
-
     bool found = false;
     uint32_t found_att = 0;
 
     if (L.kind == LINE_PMKID) {
+        uint32_t kb[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
         uint32_t ip[5], op[5], st[5], out[5];
         sha1_hmac_mid(kb, ip, op);
 #pragma unroll
@@ -217,21 +363,8 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
         found = active && out[0] == L.target[0] && out[1] == L.target[1] && out[2] == L.target[2] &&
                 out[3] == L.target[3];
     } else {
-        // PMK-keyed PRF midstates + the attempt-invariant PRF prefix
-        uint32_t ip1[5], op1[5], pre1[5];
-        uint32_t ip2[8], op2[8], pre2[8];
-        const bool kv3 = L.keyver == 3;
-        if (!kv3) {
-            sha1_hmac_mid(kb, ip1, op1);
-#pragma unroll
-            for (int k = 0; k < 5; k++) pre1[k] = ip1[k];
-            sha1_blocks(pre1, pool + L.pre_off, L.pre_nblk);
-        } else {
-            sha256_hmac_mid(kb, ip2, op2);
-#pragma unroll
-            for (int k = 0; k < 8; k++) pre2[k] = ip2[k];
-            sha256_blocks(pre2, pool + L.pre_off, L.pre_nblk);
-        }
+        EapolKey K;
+        eapol_key(L, pool, p, K);
         // PHP mutates $n across keys (common.php:255-259): list k serves the k-th non-null key, the last list the rest
         const uint32_t sel = active ? (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1)) : 0xffffffffu;
         uint32_t lo = sel, hi = active ? sel : 0u;
@@ -246,93 +379,61 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
             if (!__any(mine)) continue;
             const AttDev* al = atts + L.list_off + list * L.natt;
             for (uint32_t a = 0; a < L.natt; a++) {
-                const AttDev at = al[a];
                 uint32_t mic[4];
-                if (!kv3) {
-                    uint32_t st[5], ptk[5];
-#pragma unroll
-                    for (int k = 0; k < 5; k++) st[k] = pre1[k];
-                    sha1_blocks(st, pool + at.blk_off, at.nblk);
-                    sha1_outer20(op1, st, ptk);  // PTK[0..19]; KCK = PTK[0..15]
-                    if (L.keyver == 2) {
-                        uint32_t k2[16], mi[5], mo[5];
-#pragma unroll
-                        for (int k = 0; k < 16; k++) k2[k] = k < 4 ? ptk[k] : 0u;
-                        sha1_hmac_mid(k2, mi, mo);
-                        sha1_blocks(mi, pool + L.mic_off, L.mic_nblk);
-                        uint32_t o[5];
-                        sha1_outer20(mo, mi, o);
-                        mic[0] = o[0]; mic[1] = o[1]; mic[2] = o[2]; mic[3] = o[3];
-                    } else {
-                        uint32_t k1[16], mi[4], mo[4];
-#pragma unroll
-                        for (int k = 0; k < 16; k++) k1[k] = k < 4 ? bswap32(ptk[k]) : 0u;
-                        md5_hmac_mid(k1, mi, mo);
-                        md5_blocks(mi, pool + L.mic_off, L.mic_nblk);
-                        uint32_t m[16] = {mi[0], mi[1], mi[2], mi[3], 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 640u, 0};
-                        md5_compress(mo, m);
-                        mic[0] = mo[0]; mic[1] = mo[1]; mic[2] = mo[2]; mic[3] = mo[3];
-                    }
-                } else {
-                    uint32_t st[8];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) st[k] = pre2[k];
-                    sha256_blocks(st, pool + at.blk_off, at.nblk);
-                    uint32_t m[16] = {st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7],
-                                      0x80000000u, 0, 0, 0, 0, 0, 0, 768u};
-                    uint32_t ptk[8];
-#pragma unroll
-                    for (int k = 0; k < 8; k++) ptk[k] = op2[k];
-                    sha256_compress(ptk, m);
-                    // AES-128-CMAC(KCK = PTK[0..15], EAPOL)  (common.php:72-112)
-                    uint32_t rk[44];
-                    aes128_expand(te, ptk, rk);
-                    uint32_t Lb[4] = {0, 0, 0, 0}, K1[4], K2[4];
-                    aes128_encrypt(te, rk, Lb);
-                    cmac_dbl(Lb, K1);
-                    cmac_dbl(K1, K2);
-                    uint32_t c[4] = {0, 0, 0, 0};
-                    const uint32_t* eb = pool + L.mic_off;
-                    for (uint32_t b = 0; b < L.mic_nblk; b++) {
-                        const bool last = b + 1 == L.mic_nblk;
-#pragma unroll
-                        for (int k = 0; k < 4; k++) {
-                            uint32_t v = eb[4 * b + k];
-                            if (last) v ^= L.cmac_complete ? K1[k] : K2[k];
-                            c[k] ^= v;
-                        }
-                        aes128_encrypt(te, rk, c);
-                    }
-                    mic[0] = c[0]; mic[1] = c[1]; mic[2] = c[2]; mic[3] = c[3];
-                }
-                const bool match = mine && !found && mic[0] == L.target[0] && mic[1] == L.target[1] &&
-                                   mic[2] == L.target[2] && mic[3] == L.target[3];
-                if (match) {
+                eapol_mic(L, pool, K, al[a], te, mic);
+                if (mine && !found && mic_match(L, mic)) {
                     found = true;
                     found_att = a;
                 }
             }
         }
     }
+    report_hits(found, lane, cand, sg.line, found_att, p, hits, hitcnt, hitcap);
+}
 
-    // hit reporting: one ballot, one atomic per wave, append to the small hit buffer
-    const uint64_t m = __ballot(found);
-    if (m) {
-        const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(hitcnt, (uint32_t)__popcll(m));
-        base = __shfl(base, (int)leader);
-        if (found) {
-            const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-            if (idx < hitcap) {
-                HitDev h;
-                h.cand = cand;
-                h.line = sg.line;
-                h.attempt = found_att;
+// Attempt-parallel verification (server checks with wide nonce windows, e.g. nc=128 -> 261 attempts,
+// common.php:250-300): one wave = one (key slot, EAPOL line) pair, lane = attempt, 64 attempts per pass in PHP
+// order.  The first pass with a match yields the earliest attempt (lowest lane), exactly the attempt PHP
+// returns.  Segment s expands to 64 waves, wave k handling slot segs[s].slot + k.
+__global__ __launch_bounds__(256) void k_verify_att(const uint32_t* __restrict__ pmk, uint32_t cap,
+                                                    const uint64_t* __restrict__ ids,
+                                                    const SegDev* __restrict__ segs, uint32_t nsegs,
+                                                    const LineDev* __restrict__ lines,
+                                                    const uint32_t* __restrict__ pool,
+                                                    const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
+                                                    uint32_t* __restrict__ hitcnt, uint32_t hitcap, uint32_t use_aes) {
+    __shared__ uint32_t te_lds[256];
+    const uint32_t* te = aes_table_lds(te_lds, use_aes);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint32_t segi = gw >> 6, k = gw & 63;
+    if (segi >= nsegs) return;
+    const SegDev sg = segs[segi];
+    if (k >= sg.count) return;
+    const uint32_t slot = sg.slot + k;
+    const LineDev L = lines[sg.line];
+    uint32_t p[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) h.pmk[k] = p[k];
-                hits[idx] = h;
-            }
+    for (int w = 0; w < 8; w++) p[w] = pmk[(size_t)w * cap + slot];
+    const uint64_t cand = ids ? ids[slot] : (uint64_t)slot;
+    EapolKey K;
+    eapol_key(L, pool, p, K);
+    const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
+    const AttDev* al = atts + L.list_off + sel * L.natt;
+    for (uint32_t a0 = 0; a0 < L.natt; a0 += 64) {
+        const uint32_t a = a0 + lane;
+        bool match = false;
+        if (a < L.natt) {
+            uint32_t mic[4];
+            eapol_mic(L, pool, K, al[a], te, mic);
+            match = mic_match(L, mic);
+        }
+        const uint64_t m = __ballot(match);
+        if (m) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(m);
+            report_hits(lane == first, lane, cand, sg.line, a0 + first, p, hits, hitcnt, hitcap);
+            return;
         }
     }
 }
@@ -397,6 +498,15 @@ hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids,
     hipLaunchKernelGGL(k_verify, dim3(cdiv(nsegs, 4), segs ? 1 : nlines), dim3(256), 0, s, pmk, cap, ids, counter, segs,
                        nsegs, line_base, line_list, line_poff, pstride, lines, pool, atts, hits, hitcnt, hitcap,
                        use_aes ? 1u : 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
+                             uint32_t nsegs, const LineDev* lines, const uint32_t* pool, const AttDev* atts,
+                             HitDev* hits, uint32_t* hitcnt, uint32_t hitcap, bool use_aes, hipStream_t s) {
+    if (nsegs == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_verify_att, dim3(cdiv((uint64_t)nsegs * 64, 4)), dim3(256), 0, s, pmk, cap, ids, segs, nsegs,
+                       lines, pool, atts, hits, hitcnt, hitcap, use_aes ? 1u : 0u);
     return hipGetLastError();
 }
 

@@ -184,6 +184,90 @@ uint32_t build_salt_blocks(const std::string& essid, std::vector<uint32_t>& out)
 // ---------------------------------------------------------------------------------------------------------
 // table builder
 // ---------------------------------------------------------------------------------------------------------
+namespace {
+struct NcAtt {
+    bool big;     // 'N' (big-endian) correction word, else 'V' (little-endian)
+    int64_t off;
+};
+}  // namespace
+
+// The 4 bytes one nonce-correction attempt writes into $n (common.php:255-259, pack('N'|'V', corr + off)).
+static std::string nc_raw(const NcAtt& a, int64_t corrV, int64_t corrN) {
+    const uint32_t v = (uint32_t)(uint64_t)((a.big ? corrN : corrV) + a.off);
+    std::string r(4, '\0');
+    for (int i = 0; i < 4; i++) r[i] = (char)(a.big ? v >> (24 - 8 * i) : v >> (8 * i));
+    return r;
+}
+
+// Explicit attempt lists, used when an attempt can change the length of $n (short ANONCE: PHP's substr_replace
+// then appends, and the state of $n carries over from key to key, common.php:255-259).  lists[k][a] = full PRF
+// message of attempt a for the k-th non-null key; every attempt gets its own pre-padded blocks.
+static void add_explicit_attempts(TableBuilder& tb, LineDev& L, const std::vector<NcAtt>& order, const std::string& n0,
+                                  const std::string& pre, const std::string& post, size_t patch, int nc_mode,
+                                  int64_t corrV, int64_t corrN) {
+    std::vector<std::vector<std::string>> lists;
+    if (nc_mode == DWPA_NC_HASHCAT) {
+        std::vector<std::string> lst;
+        for (const NcAtt& a : order) {
+            std::string nn = n0;
+            php_substr_replace(nn, nc_raw(a, corrV, corrN), patch, 4);
+            lst.push_back(pre + nn + post);
+        }
+        lists.push_back(std::move(lst));
+    } else {
+        std::string ns = n0;  // PHP's $n, carried across attempts and keys
+        std::vector<std::string> starts;
+        for (int q = 0; q < 256; q++) {
+            starts.push_back(ns);
+            std::vector<std::string> lst;
+            for (const NcAtt& a : order) {
+                php_substr_replace(ns, nc_raw(a, corrV, corrN), patch, 4);
+                lst.push_back(pre + ns + post);
+            }
+            lists.push_back(std::move(lst));
+            if (ns == starts.back()) break;  // fixed point: every later key sees this list again
+        }
+        while (lists.size() >= 2 && lists[lists.size() - 2] == lists.back()) lists.pop_back();
+    }
+
+    // pre-pad every attempt; share the leading blocks common to all of them
+    std::vector<std::vector<std::vector<uint32_t>>> streams(lists.size());
+    size_t minblk = SIZE_MAX;
+    for (size_t k = 0; k < lists.size(); k++)
+        for (const std::string& msg : lists[k]) {
+            streams[k].push_back(md_stream_be(msg, 64));
+            minblk = std::min(minblk, streams[k].back().size() / 16);
+        }
+    const std::vector<uint32_t>& ref = streams[0][0];
+    size_t prefix = 0;
+    while (prefix + 1 < minblk) {
+        bool same = true;
+        for (auto& lst : streams)
+            for (auto& w : lst)
+                if (!std::equal(w.begin() + 16 * prefix, w.begin() + 16 * (prefix + 1), ref.begin() + 16 * prefix)) same = false;
+        if (!same) break;
+        prefix++;
+    }
+    L.pre_off = (uint32_t)tb.pool.size();
+    L.pre_nblk = (uint32_t)prefix;
+    tb.pool.insert(tb.pool.end(), ref.begin(), ref.begin() + 16 * prefix);
+    L.list_off = (uint32_t)tb.atts.size();
+    L.nlists = (uint32_t)lists.size();
+    for (size_t k = 0; k < lists.size(); k++)
+        for (size_t a = 0; a < order.size(); a++) {
+            const std::vector<uint32_t>& w = streams[k][a];
+            AttDev at;
+            memset(&at, 0, sizeof(at));
+            at.blk_off = (uint32_t)tb.pool.size();
+            at.nblk = (uint32_t)(w.size() / 16 - prefix);
+            at.nc = a == 0 ? 0 : (int32_t)order[a].off;
+            at.endian = a == 0 ? 0u : (order[a].big ? 1u : 2u);
+            tb.pool.insert(tb.pool.end(), w.begin() + 16 * prefix, w.end());
+            tb.atts.push_back(at);
+        }
+
+}
+
 uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int nec) {
     LineDev L;
     memset(&L, 0, sizeof(L));
@@ -215,8 +299,7 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
         corrV = le32(p.nonce_ap, 28);
         corrN = be32(p.nonce_ap, 28);
     }
-    struct Att { bool big; int64_t off; };
-    std::vector<Att> order;
+    std::vector<NcAtt> order;
     order.push_back({true, 0});
     if (nc_mode == DWPA_NC_HASHCAT) {
         const uint8_t mp = p.mp.empty() ? 0 : (uint8_t)p.mp[0];
@@ -239,74 +322,52 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
     const std::string post = kv3 ? std::string("\x80\x01", 2) : std::string("\0", 1);
     const size_t patch = swap ? 28 : 60;
 
-    auto raw_of = [&](const Att& a) {
-        const uint32_t v = (uint32_t)(uint64_t)((a.big ? corrN : corrV) + a.off);
-        std::string r(4, '\0');
-        for (int i = 0; i < 4; i++) r[i] = (char)(a.big ? v >> (24 - 8 * i) : v >> (8 * i));
-        return r;
-    };
-
-    // lists[k][a] = full PRF message of attempt a for the k-th non-null key
-    std::vector<std::vector<std::string>> lists;
-    if (nc_mode == DWPA_NC_HASHCAT) {
-        std::vector<std::string> lst;
-        for (const Att& a : order) {
-            std::string nn = n0;
-            php_substr_replace(nn, raw_of(a), patch, 4);
-            lst.push_back(pre + nn + post);
-        }
-        lists.push_back(std::move(lst));
-    } else {
-        std::string ns = n0;  // PHP's $n, carried across attempts and keys
-        std::vector<std::string> starts;
-        for (int q = 0; q < 256; q++) {
-            starts.push_back(ns);
-            std::vector<std::string> lst;
-            for (const Att& a : order) {
-                php_substr_replace(ns, raw_of(a), patch, 4);
-                lst.push_back(pre + ns + post);
-            }
-            lists.push_back(std::move(lst));
-            if (ns == starts.back()) break;  // fixed point: every later key sees this list again
-        }
-        while (lists.size() >= 2 && lists[lists.size() - 2] == lists.back()) lists.pop_back();
-    }
-
-    // pre-pad every attempt; share the leading blocks common to all of them
-    std::vector<std::vector<std::vector<uint32_t>>> streams(lists.size());
-    size_t minblk = SIZE_MAX;
-    for (size_t k = 0; k < lists.size(); k++)
-        for (const std::string& msg : lists[k]) {
-            streams[k].push_back(md_stream_be(msg, 64));
-            minblk = std::min(minblk, streams[k].back().size() / 16);
-        }
-    const std::vector<uint32_t>& ref = streams[0][0];
-    size_t prefix = 0;
-    while (prefix + 1 < minblk) {
-        bool same = true;
-        for (auto& lst : streams)
-            for (auto& w : lst)
-                if (!std::equal(w.begin() + 16 * prefix, w.begin() + 16 * (prefix + 1), ref.begin() + 16 * prefix)) same = false;
-        if (!same) break;
-        prefix++;
-    }
-    L.pre_off = (uint32_t)pool.size();
-    L.pre_nblk = (uint32_t)prefix;
-    pool.insert(pool.end(), ref.begin(), ref.begin() + 16 * prefix);
-    L.list_off = (uint32_t)atts.size();
-    L.nlists = (uint32_t)lists.size();
+    L.patch_w0 = L.patch_w1 = NO_PATCH;
     L.natt = (uint32_t)order.size();
-    for (size_t k = 0; k < lists.size(); k++)
+    if (n0.size() >= patch + 4) {
+        // Every attempt rewrites exactly bytes [patch, patch+4) of $n (common.php:255-259) and never changes its
+        // length, so all attempts of all keys share one message apart from those 4 bytes: one list, one shared
+        // block stream, two patched words per attempt.
+        const std::string base = pre + n0 + post;
+        const size_t o = pre.size() + patch;  // first correction byte in the PRF message
+        const std::vector<uint32_t> w = md_stream_be(base, 64);
+        const uint32_t W0 = (uint32_t)(o >> 2), W1 = (uint32_t)((o + 3) >> 2);
+        const uint32_t prefix = W0 / 16;
+        L.pre_off = (uint32_t)pool.size();
+        L.pre_nblk = prefix;
+        pool.insert(pool.end(), w.begin(), w.begin() + 16 * prefix);
+        const uint32_t blk_off = (uint32_t)pool.size();
+        pool.insert(pool.end(), w.begin() + 16 * prefix, w.end());
+        L.patch_w0 = W0 - 16 * prefix;
+        L.patch_w1 = W1 - 16 * prefix;
+        L.list_off = (uint32_t)atts.size();
+        L.nlists = 1;
         for (size_t a = 0; a < order.size(); a++) {
-            const std::vector<uint32_t>& w = streams[k][a];
+            const NcAtt& na = order[a];
+            const uint32_t cv = (uint32_t)(uint64_t)((na.big ? corrN : corrV) + na.off);
+            uint8_t r[4];
+            for (int i = 0; i < 4; i++) r[i] = (uint8_t)(na.big ? cv >> (24 - 8 * i) : cv >> (8 * i));
+            uint32_t v[2] = {w[W0], w[W1]};
+            for (int k = 0; k < 4; k++) {
+                const size_t q = o + k;
+                const int sh = 24 - 8 * (int)(q & 3);
+                uint32_t& x = v[(q >> 2) == W0 ? 0 : 1];
+                x = (x & ~(0xffu << sh)) | (uint32_t)r[k] << sh;
+            }
+            if (W0 == W1) v[1] = v[0];
             AttDev at;
-            at.blk_off = (uint32_t)pool.size();
+            memset(&at, 0, sizeof(at));
+            at.blk_off = blk_off;
             at.nblk = (uint32_t)(w.size() / 16 - prefix);
             at.nc = a == 0 ? 0 : (int32_t)order[a].off;
             at.endian = a == 0 ? 0u : (order[a].big ? 1u : 2u);
-            pool.insert(pool.end(), w.begin() + 16 * prefix, w.end());
+            at.v0 = v[0];
+            at.v1 = v[1];
             atts.push_back(at);
         }
+    } else {
+        add_explicit_attempts(*this, L, order, n0, pre, post, patch, nc_mode, corrV, corrN);
+    }
 
     // MIC input
     L.mic_off = (uint32_t)pool.size();

@@ -26,15 +26,28 @@ struct LineDev {
     uint32_t mic_off;     // EAPOL: HMAC inner blocks of the EAPOL frame (keyver 1/2), or CMAC blocks (keyver 3)
     uint32_t mic_nblk;
     uint32_t cmac_complete;  // keyver 3: 1 if the last EAPOL block is complete (XOR K1), else padded (XOR K2)
+    // Attempt patching: in the usual case every attempt's PRF message differs from the others only in the 4
+    // nonce-correction bytes, so all attempts share one block stream (AttDev.blk_off) and each attempt carries
+    // just the two big-endian words that hold those bytes (words patch_w0/patch_w1 of the stream; equal when the
+    // bytes are word-aligned).  NO_PATCH: every attempt has its own pre-padded blocks (short ANONCE, where PHP's
+    // substr_replace grows $n).
+    uint32_t patch_w0;
+    uint32_t patch_w1;
+    uint32_t pad0, pad1;
 };
 static_assert(sizeof(LineDev) % 16 == 0, "LineDev must stay 16-byte aligned");
+constexpr uint32_t NO_PATCH = 0xffffffffu;
 
 struct AttDev {
     uint32_t blk_off;     // word offset of this attempt's PRF blocks after the shared prefix
     uint32_t nblk;
     int32_t nc;           // signed correction reported on a hit (0 for the first attempt)
     uint32_t endian;      // 0 none (exact), 1 BE ('N'), 2 LE ('V')
+    uint32_t v0, v1;      // values of stream words patch_w0 / patch_w1 for this attempt (LineDev.patch_w0 != NO_PATCH)
+    uint32_t pad0, pad1;
 };
+// attempt-parallel verification (one wave = one key x 64 attempts) pays off once a list has this many attempts
+constexpr uint32_t ATT_PARALLEL_MIN = 64;
 
 // One wave (64 lanes) verifies up to 64 consecutive candidate slots against one line.
 struct SegDev {

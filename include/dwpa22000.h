@@ -172,7 +172,7 @@ int dwpa_scan_load_numeric(dwpa_scan *scan, uint64_t first, uint32_t count, uint
 int dwpa_scan_pbkdf2(dwpa_scan *scan, int group, void *hip_stream);
 int dwpa_scan_verify(dwpa_scan *scan, int group, void *hip_stream);
 /* Stages 2 and 3 for every ESSID group that still has an uncracked line: one PBKDF2 launch covers as many groups
- * x the loaded batch as fit 4M candidate slots (the ESSID salt is wave-uniform), followed by one verify launch
+ * x the loaded batch as fit 16M candidate slots (the ESSID salt is wave-uniform), followed by one verify launch
  * over all of their uncracked lines.  Hits are the same as the per-group calls'.  batch must be a multiple of
  * 64 (dwpa_scan_create rounds it up). */
 int dwpa_scan_run(dwpa_scan *scan, void *hip_stream);

@@ -229,7 +229,7 @@ def test_scan_rules_device_resident():
 
 def test_scan_run_many_essids_matches_per_group():
     """dwpa_scan_run: many ESSID groups per PBKDF2 launch (1- and 2-block salts in one launch, several launches
-    when groups x batch exceeds 4M slots) gives exactly the per-group path's hits, and every hit's PMK is the
+    when groups x batch exceeds 16M slots) gives exactly the per-group path's hits, and every hit's PMK is the
     oracle's."""
     from dwpa_amd.device import Dictionary
     rng = random.Random(12)
@@ -251,7 +251,7 @@ def test_scan_run_many_essids_matches_per_group():
     lines.append(S.pmkid_line(b"not-in-the-dictionary", b"lonely", rng.randbytes(6), rng.randbytes(6)))
     results = []
     for mode in ("run", "per_group"):
-        sc = dwpa_amd.Scan(lines, nc=8, batch=1 << 20)  # 4M-slot launches hold 4 groups: 3 launches for 13
+        sc = dwpa_amd.Scan(lines, nc=8, batch=1 << 22)  # 16M-slot launches hold 4 groups: 4+3+3+3 for 13 ESSIDs
         assert sc.groups == 13
         sc.load_dict(d.off.ptr, d.data.ptr, 0, len(words))
         if mode == "run":

@@ -5,11 +5,11 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out/traffic
+OUT=${OUT:-gpurun_out/traffic}
 mkdir -p $OUT
-BENCH="bench.py --dict-words 20000000 --steps 3 --warmup 1 --no-cpu-baseline"
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python3 $BENCH > $OUT/stats.log 2>&1
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $BENCH > $OUT/fetch.log 2>&1
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $BENCH > $OUT/write.log 2>&1
+BENCH="bench.py ${BENCH_ARGS:-}"  # default: the bench line itself (C2, 100M words)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/stats -o run --output-format csv -- python3 $BENCH > $OUT/stats.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- python3 $BENCH > $OUT/fetch.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- python3 $BENCH > $OUT/write.log 2>&1
 python3 tools/pmc_traffic.py $OUT > $OUT/traffic.json
 cat $OUT/traffic.json
