@@ -80,6 +80,8 @@ void DevBuf::release() {
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;   // check path: table uploads while PBKDF2 runs on `stream`
+    hipEvent_t side_done = nullptr;
     std::mutex mu;
     Batch batch;
     DevBuf lines, atts, pool, segs, salt, koff, kbytes, idsup;
@@ -131,6 +133,8 @@ static int device_stream(Device& d) {
     if (!d.stream) {
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&d.side_done, hipEventDisableTiming));
     }
     return 0;
 }
@@ -177,104 +181,111 @@ struct Slot {
     bool pbkdf2;              // false: PMK supplied by the caller
 };
 
-// Materialise, derive and (optionally) verify a list of slots sorted by (essid, !pbkdf2).
-// On return hits[] holds every hit of this chunk.
-static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
-                     const std::vector<const uint8_t*>& job_pmk, const std::vector<uint32_t>& job_line,
-                     const TableBuilder* tb, bool verify, std::vector<HitDev>& hits_out, uint8_t* pmk_out) {
+// 64-bit hash of a byte string (8-byte multiply-xor rounds) for the (ESSID run, key) dedup table.
+static uint64_t hash_bytes(const char* p, size_t n, uint64_t seed) {
+    uint64_t h = seed ^ (n * 0x9e3779b97f4a7c15ull);
+    for (; n >= 8; p += 8, n -= 8) {
+        uint64_t w;
+        memcpy(&w, p, 8);
+        h = (h ^ w) * 0xff51afd7ed558ccdull;
+        h ^= h >> 32;
+    }
+    uint64_t t = 0;
+    for (size_t k = 0; k < n; k++) t |= (uint64_t)(uint8_t)p[k] << (8 * k);
+    h = (h ^ t) * 0xc4ceb9fe1a85ec53ull;
+    return h ^ (h >> 29);
+}
+
+// Host staging of one derive step, kept alive until the stream that reads it is synchronised.
+struct DeriveStage {
+    std::vector<uint64_t> off, ids;
+    std::vector<uint8_t> bytes;
+    std::vector<uint32_t> src, sref, spool, cpmk;
+};
+
+// Derive the PMKs of slots [b, e) into batch.pmk (slot order) and their key ordinals into batch.ids.  Unique
+// (ESSID, key) pairs are derived once, all ESSIDs in one PBKDF2 launch (server batches fan one key out to every
+// net of an ESSID, common.php:879-902); each slot then gathers its PMK from them or from the caller's $pmk
+// (common.php:178).  Slots arrive grouped by ESSID.  The uploads are queued ahead of the launches: a pageable
+// upload queued behind a running kernel would block the host until that kernel ends.
+static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
+                        const std::vector<const uint8_t*>& job_pmk, DeriveStage& st) {
     PhaseTrace tr;
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
     RCHK(d.batch.reserve(n, n));
-    // Unique (ESSID, key) pairs are derived once, all ESSIDs in one launch (server batches fan one key out to
-    // every net of an ESSID, common.php:879-902); each slot then gathers its PMK from them or from the caller's
-    // $pmk.  Slots arrive sorted by ESSID, so duplicates are found within each ESSID run.
-    std::vector<uint32_t> src(n), sref, spool, cpmk;
+    st.src.assign(n, 0);
     std::vector<std::string_view> ukeys;
-    std::unordered_map<std::string_view, uint32_t> seen;
+    size_t tcap = 16;
+    while (tcap < 2 * (size_t)n) tcap <<= 1;
+    std::vector<uint32_t> table(tcap, UINT32_MAX);  // open addressing -> unique index
+    std::vector<uint64_t> uhash;
+    std::vector<uint32_t> urun;
     const std::string* cur = nullptr;
-    uint32_t cur_ref = 0;
+    uint32_t cur_ref = 0, run = 0;
     for (uint32_t i = 0; i < n; i++) {
         const Slot& sl = slots[b + i];
         if (!sl.pbkdf2) {
             const uint8_t* p = job_pmk[sl.job];
-            src[i] = GATHER_CALLER | (uint32_t)(cpmk.size() / 8);
+            st.src[i] = GATHER_CALLER | (uint32_t)(st.cpmk.size() / 8);
             for (int k = 0; k < 8; k++)
-                cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 | (uint32_t)p[4 * k + 2] << 8 |
-                               p[4 * k + 3]);
+                st.cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 |
+                                  (uint32_t)p[4 * k + 2] << 8 | p[4 * k + 3]);
             continue;
         }
-        if (!cur || *sl.essid != *cur) {
+        if (!cur || (sl.essid != cur && *sl.essid != *cur)) {
             cur = sl.essid;
-            seen.clear();
+            run++;
             std::vector<uint32_t> sb;
             const uint32_t nb = build_salt_blocks(*cur, sb);
-            cur_ref = (uint32_t)spool.size();
-            spool.push_back(nb);
-            spool.insert(spool.end(), sb.begin(), sb.end());
+            cur_ref = (uint32_t)st.spool.size();
+            st.spool.push_back(nb);
+            st.spool.insert(st.spool.end(), sb.begin(), sb.end());
         }
-        auto ins = seen.try_emplace(sl.key, (uint32_t)ukeys.size());
-        if (ins.second) {
+        const uint64_t h = hash_bytes(sl.key.data(), sl.key.size(), run);
+        size_t pos = h & (tcap - 1);
+        uint32_t u;
+        while ((u = table[pos]) != UINT32_MAX && !(uhash[u] == h && urun[u] == run && ukeys[u] == sl.key))
+            pos = (pos + 1) & (tcap - 1);
+        if (u == UINT32_MAX) {
+            u = (uint32_t)ukeys.size();
+            table[pos] = u;
             ukeys.push_back(sl.key);
-            sref.push_back(cur_ref);
+            uhash.push_back(h);
+            urun.push_back(run);
+            st.sref.push_back(cur_ref);
         }
-        src[i] = ins.first->second;
+        st.src[i] = u;
     }
     const uint32_t nu = (uint32_t)ukeys.size();
     tr.mark("  dedup (ESSID, key)");
-    RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
-    // Host staging first: a hipMemcpyAsync from pageable memory queued behind a running kernel blocks the host
-    // until that kernel ends, so every upload goes ahead of the launches.
-    std::vector<uint64_t> off(nu + 1);
-    std::vector<uint8_t> bv;
-    {
-        // unique keys -> offsets/bytes (back to back: k_prep_dict derives len = off[i+1] - off[i])
-        size_t total = 0;
-        for (uint32_t u = 0; u < nu; u++) total += ukeys[u].size();
-        bv.resize(total + 8, 0);
-        size_t pos = 0;
-        for (uint32_t u = 0; u < nu; u++) {
-            off[u] = pos;
-            memcpy(bv.data() + pos, ukeys[u].data(), ukeys[u].size());
-            pos += ukeys[u].size();
-        }
-        off[nu] = pos;
+    // unique keys -> offsets/bytes (back to back: k_prep_dict derives len = off[i+1] - off[i])
+    st.off.assign(nu + 1, 0);
+    size_t total = 0;
+    for (uint32_t u = 0; u < nu; u++) total += ukeys[u].size();
+    st.bytes.assign(total + 8, 0);
+    size_t pos = 0;
+    for (uint32_t u = 0; u < nu; u++) {
+        st.off[u] = pos;
+        memcpy(st.bytes.data() + pos, ukeys[u].data(), ukeys[u].size());
+        pos += ukeys[u].size();
     }
-    // ids = key ordinals (selects the PHP attempt list of each key)
-    std::vector<uint64_t> ids(n);
-    for (uint32_t i = 0; i < n; i++) ids[i] = slots[b + i].ordinal;
-    // segments: runs of consecutive slots of one job, <= 64 each.  EAPOL lines with wide nonce windows go to the
-    // attempt-parallel kernel (a wave per key, lanes = attempts), the rest to the key-parallel one.
-    std::vector<SegDev> segs;
-    size_t nkey = 0;
-    if (verify) {
-        for (int pass = 0; pass < 2; pass++) {
-            for (uint32_t i = 0; i < n;) {
-                uint32_t j = i;
-                const uint32_t job = slots[b + i].job;
-                while (j < n && slots[b + j].job == job && j - i < 64) j++;
-                const uint32_t li = job_line[job];
-                const LineDev& L = tb->lines[li];
-                const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
-                if (!tb->never[li] && att == (pass == 1)) segs.push_back({li, i, j - i, 0});
-                i = j;
-            }
-            if (pass == 0) nkey = segs.size();
-        }
-    }
-    if (nu) {
-        RCHK(upload(d.koff, off, s));
-        RCHK(upload(d.kbytes, bv, s));
-        RCHK(upload(d.salt, spool, s));
-        RCHK(upload(d.sref, sref, s));
-    }
-    RCHK(upload(d.cpmk, cpmk, s));
-    RCHK(upload(d.src, src, s));
-    HIPCHK(hipMemcpyAsync(d.batch.ids.p, ids.data(), n * 8, hipMemcpyHostToDevice, s));
-    if (!segs.empty()) RCHK(upload(d.segs, segs, s));
-    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
-    tr.mark("  stage+upload");
+    st.off[nu] = pos;
+    // ids = key ordinals (select the PHP attempt list of each key)
+    st.ids.resize(n);
+    for (uint32_t i = 0; i < n; i++) st.ids[i] = slots[b + i].ordinal;
 
+    RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
+    if (nu) {
+        RCHK(upload(d.koff, st.off, s));
+        RCHK(upload(d.kbytes, st.bytes, s));
+        RCHK(upload(d.salt, st.spool, s));
+        RCHK(upload(d.sref, st.sref, s));
+    }
+    RCHK(upload(d.cpmk, st.cpmk, s));
+    RCHK(upload(d.src, st.src, s));
+    HIPCHK(hipMemcpyAsync(d.batch.ids.p, st.ids.data(), n * 8, hipMemcpyHostToDevice, s));
+    tr.mark("  stage+upload");
     if (nu) {
         HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, nu, 0, 0xffffffffu,
                                 (uint32_t*)d.batch.mid.p, nullptr, nullptr, d.batch.cap, false, s));
@@ -283,30 +294,53 @@ static int run_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t
     }
     HIPCHK(launch_gather_pmk((const uint32_t*)d.upmk.p, d.batch.cap, (const uint32_t*)d.cpmk.p,
                              (const uint32_t*)d.src.p, n, (uint32_t*)d.batch.pmk.p, d.batch.cap, s));
-    if (pmk_out) {
-        std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
-        HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        for (uint32_t i = 0; i < n; i++) {
-            uint32_t pw[8];
-            for (int k = 0; k < 8; k++) pw[k] = w[(size_t)k * d.batch.cap + i];
-            pmk_bytes(pw, pmk_out + 32 * (size_t)(b + i));
+    return 0;
+}
+
+// Verify the derived slots [b, e) against their jobs' lines and append the hits.  The line tables go up on the
+// side stream (while PBKDF2 may still run) and d.stream waits for them.  EAPOL lines with wide nonce windows use
+// the attempt-parallel kernel (a wave per key, lanes = attempts), the rest the key-parallel one; segments are
+// runs of <= 64 consecutive slots of one job.
+static int verify_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
+                        const std::vector<uint32_t>& job_line, const TableBuilder& tb, bool upload_tables,
+                        std::vector<HitDev>& hits_out) {
+    PhaseTrace tr;
+    hipStream_t s = d.stream;
+    const uint32_t n = (uint32_t)(e - b);
+    std::vector<SegDev> segs;
+    size_t nkey = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        for (uint32_t i = 0; i < n;) {
+            uint32_t j = i;
+            const uint32_t job = slots[b + i].job;
+            while (j < n && slots[b + j].job == job && j - i < 64) j++;
+            const uint32_t li = job_line[job];
+            const LineDev& L = tb.lines[li];
+            const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
+            if (!tb.never[li] && att == (pass == 1)) segs.push_back({li, i, j - i, 0});
+            i = j;
         }
+        if (pass == 0) nkey = segs.size();
     }
-    if (!verify || segs.empty()) {
-        HIPCHK(hipStreamSynchronize(s));  // host staging vectors die with this frame
-        return 0;
+    if (upload_tables) {
+        RCHK(upload(d.lines, tb.lines, d.side));
+        RCHK(upload(d.atts, tb.atts, d.side));
+        RCHK(upload(d.pool, tb.pool, d.side));
     }
+    RCHK(upload(d.segs, segs, d.side));
+    HIPCHK(hipEventRecord(d.side_done, d.side));
+    HIPCHK(hipStreamWaitEvent(s, d.side_done, 0));
+    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
     uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
     HIPCHK(launch_verify((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, nullptr,
                          (const SegDev*)d.segs.p, (uint32_t)nkey, 0, 1, (const LineDev*)d.lines.p,
                          (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt,
-                         d.batch.hitcap, tb->any_aes, s));
+                         d.batch.hitcap, tb.any_aes, s));
     HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p,
                              (const SegDev*)d.segs.p + nkey, (uint32_t)(segs.size() - nkey),
                              (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p,
-                             (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, tb->any_aes, s));
-    tr.mark("  launches queued");
+                             (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, tb.any_aes, s));
+    tr.mark("  verify queued");
     uint32_t nh = 0;
     HIPCHK(hipMemcpyAsync(&nh, hitcnt, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -344,14 +378,12 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     RCHK(device_stream(d));
 
     PhaseTrace tr;
-    TableBuilder tb;
     std::vector<ParsedLine> parsed(njobs);
     std::vector<uint32_t> job_line(njobs, 0);
     std::vector<const uint8_t*> job_pmk(njobs, nullptr);
     std::vector<std::vector<std::string_view>> keys(njobs);
     std::deque<std::string> unhexed;  // decoded $HEX[] keys (stable addresses)
     std::vector<std::vector<uint32_t>> key_index(njobs);
-    std::vector<Slot> slots;
     for (size_t j = 0; j < njobs; j++) {
         out[j].key_index = -1;
         out[j].nc = 0;
@@ -361,6 +393,8 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         parsed[j] = parse_m22000(jobs[j].line, jobs[j].line_len);
         rcs[j] = parsed[j].status;
         if (parsed[j].status) continue;
+        rcs[j] = DWPA_MISS;
+        if (!line_can_match(parsed[j])) continue;  // PMKID/MIC shorter than 16 bytes never verifies
         for (size_t k = 0; k < jobs[j].nkeys; k++) {
             const dwpa_bytes& kb = jobs[j].keys[k];
             if (!kb.ptr) continue;  // is_null($key): skipped (common.php:172,240)
@@ -372,47 +406,50 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
             keys[j].push_back(key);
             key_index[j].push_back((uint32_t)k);
         }
-        rcs[j] = DWPA_MISS;
-        if (keys[j].empty()) continue;
-        job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
         job_pmk[j] = jobs[j].pmk;
-        if (tb.never[job_line[j]]) continue;
     }
-    tr.mark("parse+keys+tables");
-    // slots grouped by ESSID (jobs in input order within an ESSID, keys in order within a job): the unique
-    // (ESSID, key) pairs of run_slots are found per ESSID run
+    tr.mark("parse+keys");
+    // slots grouped by ESSID (jobs in input order within an ESSID, keys in order within a job)
     std::unordered_map<std::string_view, uint32_t> essid_id;
     std::vector<std::vector<uint32_t>> by_essid;
     size_t nslots = 0;
     for (size_t j = 0; j < njobs; j++) {
-        if (rcs[j] != DWPA_MISS || keys[j].empty() || tb.never[job_line[j]]) continue;
+        if (rcs[j] != DWPA_MISS || keys[j].empty()) continue;
         auto ins = essid_id.try_emplace(std::string_view(parsed[j].essid), (uint32_t)by_essid.size());
         if (ins.second) by_essid.emplace_back();
         by_essid[ins.first->second].push_back((uint32_t)j);
         nslots += keys[j].size();
     }
     if (!nslots) return 0;
+    std::vector<Slot> slots;
     slots.reserve(nslots);
     for (const auto& js : by_essid)
         for (uint32_t j : js)
             for (uint32_t o = 0; o < keys[j].size(); o++)
                 slots.push_back({keys[j][o], j, o, &parsed[j].essid, !(o == 0 && job_pmk[j])});
     tr.mark("slots");
-    hipStream_t s = d.stream;
-    RCHK(upload(d.lines, tb.lines, s));
-    RCHK(upload(d.atts, tb.atts, s));
-    RCHK(upload(d.pool, tb.pool, s));
 
+    // The first chunk's PBKDF2 is queued before the line tables exist: the host builds them while the GPU derives.
+    TableBuilder tb;
     std::vector<HitDev> hits;
     const size_t chunk = default_batch();
-    for (size_t b = 0; b < slots.size(); b += chunk)
-        RCHK(run_slots(d, slots, b, std::min(slots.size(), b + chunk), job_pmk, job_line, &tb, true, hits, nullptr));
-    tr.mark("device (run_slots)");
+    for (size_t b = 0; b < slots.size(); b += chunk) {
+        const size_t e = std::min(slots.size(), b + chunk);
+        DeriveStage st;
+        RCHK(derive_slots(d, slots, b, e, job_pmk, st));
+        if (b == 0) {
+            for (const auto& js : by_essid)
+                for (uint32_t j : js) job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
+            tr.mark("tables (overlapped)");
+        }
+        RCHK(verify_slots(d, slots, b, e, job_line, tb, b == 0, hits));
+    }
+    tr.mark("device");
 
     // first key in input order wins, then the first attempt in PHP order (common.php:186,280-289)
     std::map<uint32_t, size_t> line_job;
-    for (size_t j = 0; j < njobs; j++)
-        if (rcs[j] == DWPA_MISS && !keys[j].empty()) line_job[job_line[j]] = j;
+    for (const auto& js : by_essid)
+        for (uint32_t j : js) line_job[job_line[j]] = j;
     std::vector<int64_t> best(njobs, -1);
     std::vector<uint32_t> best_att(njobs, 0);
     std::vector<const HitDev*> best_hit(njobs, nullptr);
@@ -454,18 +491,25 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
     HIPCHK(hipSetDevice(d.id));
     RCHK(device_stream(d));
     std::string es((const char*)essid, essid_len);
-    std::vector<std::string> ks(nkeys);
     std::vector<Slot> slots(nkeys);
-    for (size_t i = 0; i < nkeys; i++) {
-        if (keys[i].ptr) ks[i].assign((const char*)keys[i].ptr, keys[i].len);
-        slots[i] = {std::string_view(ks[i]), 0, (uint32_t)i, &es, true};
-    }
-    std::vector<HitDev> hits;
+    for (size_t i = 0; i < nkeys; i++)
+        slots[i] = {keys[i].ptr ? std::string_view((const char*)keys[i].ptr, keys[i].len) : std::string_view(), 0,
+                    (uint32_t)i, &es, true};
     const size_t chunk = default_batch();
     std::vector<const uint8_t*> jp(1, nullptr);
-    std::vector<uint32_t> jl(1, 0);
-    for (size_t b = 0; b < nkeys; b += chunk)
-        RCHK(run_slots(d, slots, b, std::min(nkeys, b + chunk), jp, jl, nullptr, false, hits, out));
+    for (size_t b = 0; b < nkeys; b += chunk) {
+        const size_t e = std::min(nkeys, b + chunk);
+        DeriveStage st;
+        RCHK(derive_slots(d, slots, b, e, jp, st));
+        std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
+        HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(hipStreamSynchronize(d.stream));
+        for (size_t i = 0; i < e - b; i++) {
+            uint32_t pw[8];
+            for (int k = 0; k < 8; k++) pw[k] = w[(size_t)k * d.batch.cap + i];
+            pmk_bytes(pw, out + 32 * (b + i));
+        }
+    }
     return 0;
 }
 
@@ -798,7 +842,10 @@ void dwpa_shutdown(void) {
             b->release();
         d->batch.cap = d->batch.hitcap = 0;
         if (d->stream) (void)hipStreamDestroy(d->stream);
-        d->stream = nullptr;
+        if (d->side) (void)hipStreamDestroy(d->side);
+        if (d->side_done) (void)hipEventDestroy(d->side_done);
+        d->stream = d->side = nullptr;
+        d->side_done = nullptr;
     }
     g_dev.clear();
     g_init = false;

@@ -19,6 +19,11 @@ struct ParsedLine {
 };
 
 ParsedLine parse_m22000(const char* s, size_t n);
+// False when the line's PMKID / MIC is shorter than 16 bytes: strncmp over 16 bytes never matches
+// (common.php:186,280); TableBuilder marks such lines `never`.
+inline bool line_can_match(const ParsedLine& p) {
+    return (p.kind == LINE_PMKID ? p.pmkid.size() : p.keymic.size()) >= 16;
+}
 
 // hashcat $HEX[] decoding as web/common.php:3-25 (only applied to keys starting with "$HEX[")
 std::string hc_unhex(const std::string& k);
