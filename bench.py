@@ -33,6 +33,13 @@ COMPRESSIONS_PER_PMK = 16388
 C_MIN_CYCLES = 1887
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
+# HBM traffic of k_pbkdf2 per PMK, from the PMC passes of tools/profile_traffic.sh over this bench command
+# (profiles/r01/traffic/traffic.json, per 4,194,304-PMK launch): FETCH_SIZE 167,954,944 B, doubled as
+# MI355X_MICROARCH.md "HBM [CDNA4]" prescribes = 80 B/PMK (each of the two output-block lanes reads the 40-byte key
+# midstate once), plus WRITE_SIZE 134,217,728 B = 32 B/PMK.  Algorithmic bytes are the same 80 + 32 = 112 B/PMK.
+# PMC counters cannot be read inside a timed run, so the bench scales the measured per-PMK figure to its launches.
+TRAFFIC_BYTES_PER_PMK = (2 * 167954944 + 134217728) / 4194304
+ALGO_BYTES_PER_PMK = 80 + 32
 # Nominal all-ops-full-rate view (128 int32 lane-ops/clk/CU, 576.5 ops/compression): reported, not attainable.
 OPS_PER_COMPRESSION = 576.5
 PEAK_LANE_OPS = 256 * 128 * CLOCK_HZ
@@ -298,7 +305,10 @@ def main():
                 "peak": round(PEAK_COMPRESSIONS / 1e9, 3),
                 "unit": "G SHA-1 compressions/s",
                 "frac": round(achieved / PEAK_COMPRESSIONS, 4),
-                "traffic": None,
+                "traffic": round(TRAFFIC_BYTES_PER_PMK * pmk_per_launch),
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01/traffic)",
+                "algorithmic_bytes": ALGO_BYTES_PER_PMK * pmk_per_launch,
+                "hbm_gbs": round(TRAFFIC_BYTES_PER_PMK * pmk_per_launch / (kernel_ms * 1e-3) / 1e9, 3),
                 "kernel_ms": round(kernel_ms, 3),
                 "pmk_per_launch": pmk_per_launch,
                 "kernel_pmk_per_s": round(kernel_pmk_s, 1),
