@@ -307,21 +307,25 @@ static int verify_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     PhaseTrace tr;
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
-    std::vector<SegDev> segs;
-    size_t nkey = 0;
-    for (int pass = 0; pass < 2; pass++) {
-        for (uint32_t i = 0; i < n;) {
-            uint32_t j = i;
-            const uint32_t job = slots[b + i].job;
-            while (j < n && slots[b + j].job == job && j - i < 64) j++;
-            const uint32_t li = job_line[job];
-            const LineDev& L = tb.lines[li];
-            const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
-            if (!tb.never[li] && att == (pass == 1)) segs.push_back({li, i, j - i, 0});
-            i = j;
-        }
-        if (pass == 0) nkey = segs.size();
+    // bucket = mode * 4 + class index; mode 1 = attempt-parallel (EAPOL lines with >= ATT_PARALLEL_MIN attempts)
+    std::vector<SegDev> bucket[8];
+    for (uint32_t i = 0; i < n;) {
+        uint32_t j = i;
+        const uint32_t job = slots[b + i].job;
+        while (j < n && slots[b + j].job == job && j - i < 64) j++;
+        const uint32_t li = job_line[job];
+        const LineDev& L = tb.lines[li];
+        const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
+        if (!tb.never[li]) bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, i, j - i, 0});
+        i = j;
     }
+    std::vector<SegDev> segs;
+    size_t bstart[9];
+    for (int k = 0; k < 8; k++) {
+        bstart[k] = segs.size();
+        segs.insert(segs.end(), bucket[k].begin(), bucket[k].end());
+    }
+    bstart[8] = segs.size();
     if (upload_tables) {
         RCHK(upload(d.lines, tb.lines, d.side));
         RCHK(upload(d.atts, tb.atts, d.side));
@@ -332,14 +336,20 @@ static int verify_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     HIPCHK(hipStreamWaitEvent(s, d.side_done, 0));
     HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
     uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
-    HIPCHK(launch_verify((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, nullptr,
-                         (const SegDev*)d.segs.p, (uint32_t)nkey, 0, 1, (const LineDev*)d.lines.p,
-                         (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt,
-                         d.batch.hitcap, tb.any_aes, s));
-    HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p,
-                             (const SegDev*)d.segs.p + nkey, (uint32_t)(segs.size() - nkey),
-                             (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p,
-                             (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, tb.any_aes, s));
+    for (int k = 0; k < 8; k++) {
+        const uint32_t nb = (uint32_t)(bstart[k + 1] - bstart[k]), vc = 1u << (k & 3);
+        const SegDev* sg = (const SegDev*)d.segs.p + bstart[k];
+        if (!nb) continue;
+        if (k < 4)
+            HIPCHK(launch_verify((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, nullptr,
+                                 sg, nb, 0, 1, (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p,
+                                 (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc, s));
+        else
+            HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, sg,
+                                     nb, (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p,
+                                     (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc,
+                                     s));
+    }
     tr.mark("  verify queued");
     uint32_t nh = 0;
     HIPCHK(hipMemcpyAsync(&nh, hitcnt, 4, hipMemcpyDeviceToHost, s));
@@ -539,6 +549,7 @@ struct dwpa_scan {
     // scan_run (many ESSID groups per PBKDF2 launch): rebuilt when the set of uncracked lines changes
     struct Chunk {
         uint32_t g0, ngroups, list0, nlines;
+        uint32_t cls[5];  // the chunk's lines of verify class index c are list[list0 + cls[c], list0 + cls[c+1])
     };
     bool mg_dirty = true;
     uint32_t mg_stride = 0;                // PMK SoA stride = (most groups in one launch) x batch_cap
@@ -573,6 +584,11 @@ int scan_create(int device, const char* const* lines, const size_t* lens, size_t
         ScanGroup g;
         g.essid = kv.first;
         g.line_begin = (uint32_t)sc->tb.lines.size();
+        // lines of a group ordered by verify class, so that each class is one contiguous run (one kernel each)
+        auto cls = [&](size_t i) {
+            return parsed[i].kind == LINE_PMKID ? 0 : parsed[i].keyver;
+        };
+        std::stable_sort(kv.second.begin(), kv.second.end(), [&](size_t x, size_t y) { return cls(x) < cls(y); });
         for (size_t i : kv.second) {
             sc->line_of[i] = sc->tb.add_line(parsed[i], nc, nc_mode, nc);
             sc->input_of.push_back((uint32_t)i);
@@ -652,16 +668,17 @@ int scan_verify(dwpa_scan* sc, int group, void* stream) {
     HIPCHK(hipSetDevice(sc->device));
     const ScanGroup& g = sc->groups[group];
     const uint32_t nsegs = sc->batch_cap / 64;
-    // contiguous runs of uncracked lines -> implicit-segment launches
+    // contiguous runs of uncracked lines of one verify class -> implicit-segment launches
     for (uint32_t l = g.line_begin; l < g.line_end;) {
         if (sc->cracked[l]) { l++; continue; }
+        const uint32_t vc = verify_class(sc->tb.lines[l]);
         uint32_t e = l;
-        while (e < g.line_end && !sc->cracked[e]) e++;
+        while (e < g.line_end && !sc->cracked[e] && verify_class(sc->tb.lines[e]) == vc) e++;
         HIPCHK(launch_verify((const uint32_t*)sc->batch.pmk.p, sc->batch_cap, (const uint64_t*)sc->batch.ids.p,
                              (const uint32_t*)sc->batch.counters.p, nullptr, nsegs, l, e - l,
                              (const LineDev*)sc->lines.p, (const uint32_t*)sc->pool.p, (const AttDev*)sc->atts.p,
                              (HitDev*)sc->batch.hits.p, (uint32_t*)sc->batch.counters.p + 1, sc->batch.hitcap,
-                             sc->tb.any_aes, as_stream(stream)));
+                             vc, as_stream(stream)));
         l = e;
     }
     return 0;
@@ -693,18 +710,24 @@ static int scan_mg_rebuild(dwpa_scan* sc, hipStream_t s) {
     uint32_t most = 0, next = 0;
     for (uint32_t c = 0; c < launches; c++) {
         const uint32_t size = nact / launches + (c < nact % launches ? 1u : 0u);
-        dwpa_scan::Chunk ch{(uint32_t)sc->mg_gsalt_h.size() / 2, size, (uint32_t)sc->mg_list_h.size(), 0};
+        dwpa::ScanGroup const* const* grp = act.data() + next;
+        dwpa_scan::Chunk ch{(uint32_t)sc->mg_gsalt_h.size() / 2, size, (uint32_t)sc->mg_list_h.size(), 0, {}};
         for (uint32_t k = 0; k < size; k++) {
-            const ScanGroup& g = *act[next++];
-            sc->mg_gsalt_h.push_back(g.salt_off);
-            sc->mg_gsalt_h.push_back(g.nsalt);
-            for (uint32_t l = g.line_begin; l < g.line_end; l++) {
-                if (sc->cracked[l]) continue;
-                sc->mg_list_h.push_back(l);
-                sc->mg_poff_h[l] = k * cap;
-            }
+            sc->mg_gsalt_h.push_back(grp[k]->salt_off);
+            sc->mg_gsalt_h.push_back(grp[k]->nsalt);
         }
+        for (uint32_t c = 0; c < 4; c++) {
+            ch.cls[c] = (uint32_t)sc->mg_list_h.size() - ch.list0;
+            for (uint32_t k = 0; k < size; k++)
+                for (uint32_t l = grp[k]->line_begin; l < grp[k]->line_end; l++) {
+                    if (sc->cracked[l] || verify_class(sc->tb.lines[l]) != (1u << c)) continue;
+                    sc->mg_list_h.push_back(l);
+                    sc->mg_poff_h[l] = k * cap;
+                }
+        }
+        next += size;
         ch.nlines = (uint32_t)sc->mg_list_h.size() - ch.list0;
+        ch.cls[4] = ch.nlines;
         most = std::max(most, size);
         sc->mg_chunks.push_back(ch);
     }
@@ -730,15 +753,16 @@ int scan_run(dwpa_scan* sc, void* stream) {
         HIPCHK(launch_pbkdf2_mg((const uint32_t*)sc->batch.mid.p, cap, (const uint32_t*)sc->batch.counters.p,
                                 ch.ngroups, (const uint32_t*)sc->salt.p, (const uint32_t*)sc->mg_gsalt.p + 2 * ch.g0,
                                 (uint32_t*)sc->mg_pmk.p, pstride, s));
-        for (uint32_t l = 0; l < ch.nlines; l += 65535u) {
-            const uint32_t nl = std::min<uint32_t>(65535u, ch.nlines - l);
-            HIPCHK(launch_verify((const uint32_t*)sc->mg_pmk.p, cap, (const uint64_t*)sc->batch.ids.p,
-                                 (const uint32_t*)sc->batch.counters.p, nullptr, cap / 64, ch.list0 + l, nl,
-                                 (const LineDev*)sc->lines.p, (const uint32_t*)sc->pool.p, (const AttDev*)sc->atts.p,
-                                 (HitDev*)sc->batch.hits.p, (uint32_t*)sc->batch.counters.p + 1, sc->batch.hitcap,
-                                 sc->tb.any_aes, s, (const uint32_t*)sc->mg_list.p, (const uint32_t*)sc->mg_poff.p,
-                                 pstride));
-        }
+        for (uint32_t c = 0; c < 4; c++)  // one launch per verify class (grid.y <= 65535 lines)
+            for (uint32_t l = ch.cls[c]; l < ch.cls[c + 1]; l += 65535u) {
+                const uint32_t nl = std::min<uint32_t>(65535u, ch.cls[c + 1] - l);
+                HIPCHK(launch_verify((const uint32_t*)sc->mg_pmk.p, cap, (const uint64_t*)sc->batch.ids.p,
+                                     (const uint32_t*)sc->batch.counters.p, nullptr, cap / 64, ch.list0 + l, nl,
+                                     (const LineDev*)sc->lines.p, (const uint32_t*)sc->pool.p,
+                                     (const AttDev*)sc->atts.p, (HitDev*)sc->batch.hits.p,
+                                     (uint32_t*)sc->batch.counters.p + 1, sc->batch.hitcap, 1u << c, s,
+                                     (const uint32_t*)sc->mg_list.p, (const uint32_t*)sc->mg_poff.p, pstride));
+            }
     }
     return 0;
 }

@@ -183,18 +183,22 @@ struct EapolKey {
     uint32_t op2[8], pre2[8];  // keyver 3: same for HMAC-SHA256
 };
 
+// VC: the verify classes (VC_* in tables.hpp) a kernel instantiation handles; code for the others is not emitted,
+// so a launch over keyver-2 lines only carries neither the SHA-256/AES-CMAC nor the MD5 path's registers.
+template <uint32_t VC>
 __device__ __forceinline__ void eapol_key(const LineDev& L, const uint32_t* __restrict__ pool, const uint32_t p[8],
                                           EapolKey& K) {
+    constexpr bool has12 = (VC & (VC_KV1 | VC_KV2)) != 0, has3 = (VC & VC_KV3) != 0;
     uint32_t kb[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
-    if (L.keyver != 3) {
+    if (has12 && (!has3 || L.keyver != 3)) {
         uint32_t ip1[5];
         sha1_hmac_mid(kb, ip1, K.op1);
 #pragma unroll
         for (int k = 0; k < 5; k++) K.pre1[k] = ip1[k];
         sha1_blocks(K.pre1, pool + L.pre_off, L.pre_nblk);
-    } else {
+    } else if constexpr (has3) {
         uint32_t ip2[8];
         sha256_hmac_mid(kb, ip2, K.op2);
 #pragma unroll
@@ -205,10 +209,12 @@ __device__ __forceinline__ void eapol_key(const LineDev& L, const uint32_t* __re
 
 // MIC of one nonce-correction attempt (common.php:250-300): PRF-512 (keyver 1/2: HMAC-SHA1, first 20 bytes;
 // keyver 3: KDF-SHA256) -> KCK -> HMAC-MD5 (1), HMAC-SHA1 (2) or AES-128-CMAC (3) over the EAPOL frame.
+template <uint32_t VC>
 __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __restrict__ pool, const EapolKey& K,
                                           const AttDev& at, const uint32_t* te, uint32_t mic[4]) {
+    constexpr bool has1 = (VC & VC_KV1) != 0, has2 = (VC & VC_KV2) != 0, has3 = (VC & VC_KV3) != 0;
     const uint32_t* aw = pool + at.blk_off;
-    if (L.keyver != 3) {
+    if ((has1 || has2) && (!has3 || L.keyver != 3)) {
         uint32_t st[5], ptk[5];
 #pragma unroll
         for (int k = 0; k < 5; k++) st[k] = K.pre1[k];
@@ -218,16 +224,23 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
             sha1_compress(st, m);
         }
         sha1_outer20(K.op1, st, ptk);  // PTK[0..19]; KCK = PTK[0..15]
-        if (L.keyver == 2) {
-            uint32_t k2[16], mi[5], mo[5];
+        if (has2 && (!has1 || L.keyver == 2)) {
+            // HMAC-SHA1(KCK, EAPOL): the opad midstate is computed after the inner hash so that the two key-pad
+            // compressions are not live at the same time (keeps this class inside 64 VGPRs)
+            uint32_t blk[16], mi[5], mo[5];
 #pragma unroll
-            for (int k = 0; k < 16; k++) k2[k] = k < 4 ? ptk[k] : 0u;
-            sha1_hmac_mid(k2, mi, mo);
+            for (int k = 0; k < 16; k++) blk[k] = (k < 4 ? ptk[k] : 0u) ^ 0x36363636u;
+            sha1_iv(mi);
+            sha1_compress(mi, blk);
             sha1_blocks(mi, pool + L.mic_off, L.mic_nblk);
+#pragma unroll
+            for (int k = 0; k < 16; k++) blk[k] = (k < 4 ? ptk[k] : 0u) ^ 0x5c5c5c5cu;
+            sha1_iv(mo);
+            sha1_compress(mo, blk);
             uint32_t o[5];
             sha1_outer20(mo, mi, o);
             mic[0] = o[0]; mic[1] = o[1]; mic[2] = o[2]; mic[3] = o[3];
-        } else {
+        } else if constexpr (has1) {
             uint32_t k1[16], mi[4], mo[4];
 #pragma unroll
             for (int k = 0; k < 16; k++) k1[k] = k < 4 ? bswap32(ptk[k]) : 0u;
@@ -237,7 +250,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
             md5_compress(mo, m);
             mic[0] = mo[0]; mic[1] = mo[1]; mic[2] = mo[2]; mic[3] = mo[3];
         }
-    } else {
+    } else if constexpr (has3) {
         uint32_t st[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) st[k] = K.pre2[k];
@@ -280,8 +293,10 @@ __device__ __forceinline__ bool mic_match(const LineDev& L, const uint32_t mic[4
 }
 
 // hit reporting: one ballot, one atomic per wave, append to the small hit buffer
+// The PMK is re-read from `pw` (word k at pw[k * stride]) only for hit lanes, so it is not held in registers across
+// the attempt loop.
 __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t cand, uint32_t line, uint32_t att,
-                                            const uint32_t p[8], HitDev* __restrict__ hits,
+                                            const uint32_t* __restrict__ pw, size_t stride, HitDev* __restrict__ hits,
                                             uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
     const uint64_t m = __ballot(found);
     if (!m) return;
@@ -297,14 +312,15 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
             h.line = line;
             h.attempt = att;
 #pragma unroll
-            for (int k = 0; k < 8; k++) h.pmk[k] = p[k];
+            for (int k = 0; k < 8; k++) h.pmk[k] = pw[(size_t)k * stride];
             hits[idx] = h;
         }
     }
 }
 
-__device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te, uint32_t use_aes) {
-    if (use_aes) {
+template <uint32_t VC>
+__device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
+    if constexpr ((VC & VC_KV3) != 0) {
         for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) te[k] = AES_TABLES.te0[k];
         __syncthreads();
     }
@@ -313,16 +329,22 @@ __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te, uint32_t 
 
 // Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
 // wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
-__global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk, uint32_t cap,
+// Occupancy target per class (VGPR budget without scratch spills): PMKID and keyver 1 fit 64 VGPRs (8 waves/SIMD),
+// keyver 2 80 (6 waves), keyver 3 keeps 44 AES round-key registers (2 waves).
+constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? 2 : 8; }
+
+template <uint32_t VC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify(
+                                                const uint32_t* __restrict__ pmk, uint32_t cap,
                                                 const uint64_t* __restrict__ ids, const uint32_t* __restrict__ counter,
                                                 const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t line_base,
                                                 const uint32_t* __restrict__ line_list,
                                                 const uint32_t* __restrict__ line_poff, uint32_t pstride,
                                                 const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
-                                                uint32_t* __restrict__ hitcnt, uint32_t hitcap, uint32_t use_aes) {
+                                                uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
     __shared__ uint32_t te_lds[256];
-    const uint32_t* te = aes_table_lds(te_lds, use_aes);
+    const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t segi = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -350,7 +372,8 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
     bool found = false;
     uint32_t found_att = 0;
 
-    if (L.kind == LINE_PMKID) {
+    constexpr bool has_pmkid = (VC & VC_PMKID) != 0, has_eapol = (VC & ~VC_PMKID) != 0;
+    if (has_pmkid && (!has_eapol || L.kind == LINE_PMKID)) {
         uint32_t kb[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
@@ -362,9 +385,9 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
         sha1_outer20(op, st, out);
         found = active && out[0] == L.target[0] && out[1] == L.target[1] && out[2] == L.target[2] &&
                 out[3] == L.target[3];
-    } else {
+    } else if constexpr (has_eapol) {
         EapolKey K;
-        eapol_key(L, pool, p, K);
+        eapol_key<VC>(L, pool, p, K);
         // PHP mutates $n across keys (common.php:255-259): list k serves the k-th non-null key, the last list the rest
         const uint32_t sel = active ? (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1)) : 0xffffffffu;
         uint32_t lo = sel, hi = active ? sel : 0u;
@@ -380,7 +403,7 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
             const AttDev* al = atts + L.list_off + list * L.natt;
             for (uint32_t a = 0; a < L.natt; a++) {
                 uint32_t mic[4];
-                eapol_mic(L, pool, K, al[a], te, mic);
+                eapol_mic<VC>(L, pool, K, al[a], te, mic);
                 if (mine && !found && mic_match(L, mic)) {
                     found = true;
                     found_att = a;
@@ -388,22 +411,24 @@ __global__ __launch_bounds__(256) void k_verify(const uint32_t* __restrict__ pmk
             }
         }
     }
-    report_hits(found, lane, cand, sg.line, found_att, p, hits, hitcnt, hitcap);
+    report_hits(found, lane, cand, sg.line, found_att, pmk + poff + slot, pstride, hits, hitcnt, hitcap);
 }
 
 // Attempt-parallel verification (server checks with wide nonce windows, e.g. nc=128 -> 261 attempts,
 // common.php:250-300): one wave = one (key slot, EAPOL line) pair, lane = attempt, 64 attempts per pass in PHP
 // order.  The first pass with a match yields the earliest attempt (lowest lane), exactly the attempt PHP
 // returns.  Segment s expands to 64 waves, wave k handling slot segs[s].slot + k.
-__global__ __launch_bounds__(256) void k_verify_att(const uint32_t* __restrict__ pmk, uint32_t cap,
+template <uint32_t VC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify_att(
+                                                    const uint32_t* __restrict__ pmk, uint32_t cap,
                                                     const uint64_t* __restrict__ ids,
                                                     const SegDev* __restrict__ segs, uint32_t nsegs,
                                                     const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool,
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
-                                                    uint32_t* __restrict__ hitcnt, uint32_t hitcap, uint32_t use_aes) {
+                                                    uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
     __shared__ uint32_t te_lds[256];
-    const uint32_t* te = aes_table_lds(te_lds, use_aes);
+    const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -418,7 +443,7 @@ __global__ __launch_bounds__(256) void k_verify_att(const uint32_t* __restrict__
     for (int w = 0; w < 8; w++) p[w] = pmk[(size_t)w * cap + slot];
     const uint64_t cand = ids ? ids[slot] : (uint64_t)slot;
     EapolKey K;
-    eapol_key(L, pool, p, K);
+    eapol_key<VC>(L, pool, p, K);
     const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
     const AttDev* al = atts + L.list_off + sel * L.natt;
     for (uint32_t a0 = 0; a0 < L.natt; a0 += 64) {
@@ -426,13 +451,13 @@ __global__ __launch_bounds__(256) void k_verify_att(const uint32_t* __restrict__
         bool match = false;
         if (a < L.natt) {
             uint32_t mic[4];
-            eapol_mic(L, pool, K, al[a], te, mic);
+            eapol_mic<VC>(L, pool, K, al[a], te, mic);
             match = mic_match(L, mic);
         }
         const uint64_t m = __ballot(match);
         if (m) {
             const uint32_t first = (uint32_t)__builtin_ctzll(m);
-            report_hits(lane == first, lane, cand, sg.line, a0 + first, p, hits, hitcnt, hitcap);
+            report_hits(lane == first, lane, cand, sg.line, a0 + first, pmk + slot, cap, hits, hitcnt, hitcap);
             return;
         }
     }
@@ -488,25 +513,41 @@ hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint
     return hipGetLastError();
 }
 
+#define DWPA_VC_DISPATCH(VCV, CALL) \
+    switch (VCV) {                  \
+    case VC_PMKID: CALL(VC_PMKID); break; \
+    case VC_KV1: CALL(VC_KV1); break;     \
+    case VC_KV2: CALL(VC_KV2); break;     \
+    case VC_KV3: CALL(VC_KV3); break;     \
+    default: CALL(VC_ALL); break;         \
+    }
+
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,
                          const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt, uint32_t hitcap,
-                         bool use_aes, hipStream_t s, const uint32_t* line_list, const uint32_t* line_poff,
+                         uint32_t vc, hipStream_t s, const uint32_t* line_list, const uint32_t* line_poff,
                          uint32_t pstride) {
     if (nsegs == 0 || nlines == 0) return hipSuccess;
     if (!pstride) pstride = cap;
-    hipLaunchKernelGGL(k_verify, dim3(cdiv(nsegs, 4), segs ? 1 : nlines), dim3(256), 0, s, pmk, cap, ids, counter, segs,
-                       nsegs, line_base, line_list, line_poff, pstride, lines, pool, atts, hits, hitcnt, hitcap,
-                       use_aes ? 1u : 0u);
+    const dim3 grid(cdiv(nsegs, 4), segs ? 1 : nlines);
+#define DWPA_LAUNCH_VERIFY(V)                                                                                  \
+    hipLaunchKernelGGL(k_verify<V>, grid, dim3(256), 0, s, pmk, cap, ids, counter, segs, nsegs, line_base,      \
+                       line_list, line_poff, pstride, lines, pool, atts, hits, hitcnt, hitcap)
+    DWPA_VC_DISPATCH(vc, DWPA_LAUNCH_VERIFY)
+#undef DWPA_LAUNCH_VERIFY
     return hipGetLastError();
 }
 
 hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
                              uint32_t nsegs, const LineDev* lines, const uint32_t* pool, const AttDev* atts,
-                             HitDev* hits, uint32_t* hitcnt, uint32_t hitcap, bool use_aes, hipStream_t s) {
+                             HitDev* hits, uint32_t* hitcnt, uint32_t hitcap, uint32_t vc, hipStream_t s) {
     if (nsegs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_verify_att, dim3(cdiv((uint64_t)nsegs * 64, 4)), dim3(256), 0, s, pmk, cap, ids, segs, nsegs,
-                       lines, pool, atts, hits, hitcnt, hitcap, use_aes ? 1u : 0u);
+    const dim3 grid(cdiv((uint64_t)nsegs * 64, 4));
+#define DWPA_LAUNCH_VERIFY_ATT(V) \
+    hipLaunchKernelGGL(k_verify_att<V>, grid, dim3(256), 0, s, pmk, cap, ids, segs, nsegs, lines, pool, atts, hits, \
+                       hitcnt, hitcap)
+    DWPA_VC_DISPATCH(vc & ~VC_PMKID, DWPA_LAUNCH_VERIFY_ATT)
+#undef DWPA_LAUNCH_VERIFY_ATT
     return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t co
 // one wave per (slot, EAPOL line) pair, lanes = nonce-correction attempts (lists with >= ATT_PARALLEL_MIN attempts)
 hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
                              uint32_t nsegs, const LineDev* lines, const uint32_t* pool, const AttDev* atts,
-                             HitDev* hits, uint32_t* hitcnt, uint32_t hitcap, bool use_aes, hipStream_t s);
+                             HitDev* hits, uint32_t* hitcnt, uint32_t hitcap, uint32_t vc, hipStream_t s);
 // many ESSID groups x one batch per launch (cap % 64 == 0): gsalt[c] = {salt word offset, nsalt} of chunk group c,
 // PMK word k of (c, slot) at pmk[k * pstride + c * cap + slot]
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
@@ -43,7 +43,7 @@ hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,
                          const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt, uint32_t hitcap,
-                         bool use_aes, hipStream_t s, const uint32_t* line_list = nullptr,
+                         uint32_t vc, hipStream_t s, const uint32_t* line_list = nullptr,
                          const uint32_t* line_poff = nullptr, uint32_t pstride = 0);
 
 }  // namespace dwpa

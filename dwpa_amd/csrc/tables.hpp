@@ -46,6 +46,11 @@ struct AttDev {
     uint32_t v0, v1;      // values of stream words patch_w0 / patch_w1 for this attempt (LineDev.patch_w0 != NO_PATCH)
     uint32_t pad0, pad1;
 };
+// Verify classes: kernels are instantiated per class so that each launch carries only one MAC's code and registers.
+enum : uint32_t { VC_PMKID = 1, VC_KV1 = 2, VC_KV2 = 4, VC_KV3 = 8, VC_ALL = 15 };
+inline uint32_t verify_class(const LineDev& L) {
+    return L.kind == LINE_PMKID ? VC_PMKID : L.keyver == 1 ? VC_KV1 : L.keyver == 2 ? VC_KV2 : VC_KV3;
+}
 // attempt-parallel verification (one wave = one key x 64 attempts) pays off once a list has this many attempts
 constexpr uint32_t ATT_PARALLEL_MIN = 64;
 
