@@ -216,46 +216,53 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     RCHK(d.batch.reserve(n, n));
     st.src.assign(n, 0);
     std::vector<std::string_view> ukeys;
-    size_t tcap = 16;
-    while (tcap < 2 * (size_t)n) tcap <<= 1;
-    std::vector<uint32_t> table(tcap, UINT32_MAX);  // open addressing -> unique index
+    ukeys.reserve(n);
+    st.sref.reserve(n);
+    // one small open-addressing table per ESSID run (a run's keys stay cache-resident; a whole-batch table
+    // costs a cache miss per key)
+    std::vector<uint32_t> table;
     std::vector<uint64_t> uhash;
-    std::vector<uint32_t> urun;
-    const std::string* cur = nullptr;
-    uint32_t cur_ref = 0, run = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const Slot& sl = slots[b + i];
-        if (!sl.pbkdf2) {
-            const uint8_t* p = job_pmk[sl.job];
-            st.src[i] = GATHER_CALLER | (uint32_t)(st.cpmk.size() / 8);
-            for (int k = 0; k < 8; k++)
-                st.cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 |
-                                  (uint32_t)p[4 * k + 2] << 8 | p[4 * k + 3]);
-            continue;
+    uhash.reserve(n);
+    for (uint32_t i0 = 0; i0 < n;) {
+        const std::string* essid = slots[b + i0].essid;
+        uint32_t i1 = i0 + 1;
+        while (i1 < n && (slots[b + i1].essid == essid || *slots[b + i1].essid == *essid)) i1++;
+        size_t tcap = 16;
+        while (tcap < 2 * (size_t)(i1 - i0)) tcap <<= 1;
+        table.assign(tcap, UINT32_MAX);
+        uint32_t cur_ref = UINT32_MAX;
+        for (uint32_t i = i0; i < i1; i++) {
+            const Slot& sl = slots[b + i];
+            if (i + 16 < i1) __builtin_prefetch(slots[b + i + 16].key.data());
+            if (!sl.pbkdf2) {
+                const uint8_t* p = job_pmk[sl.job];
+                st.src[i] = GATHER_CALLER | (uint32_t)(st.cpmk.size() / 8);
+                for (int k = 0; k < 8; k++)
+                    st.cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 |
+                                      (uint32_t)p[4 * k + 2] << 8 | p[4 * k + 3]);
+                continue;
+            }
+            if (cur_ref == UINT32_MAX) {
+                std::vector<uint32_t> sb;
+                const uint32_t nb = build_salt_blocks(*essid, sb);
+                cur_ref = (uint32_t)st.spool.size();
+                st.spool.push_back(nb);
+                st.spool.insert(st.spool.end(), sb.begin(), sb.end());
+            }
+            const uint64_t h = hash_bytes(sl.key.data(), sl.key.size(), 0);
+            size_t pos = h & (tcap - 1);
+            uint32_t u;
+            while ((u = table[pos]) != UINT32_MAX && !(uhash[u] == h && ukeys[u] == sl.key)) pos = (pos + 1) & (tcap - 1);
+            if (u == UINT32_MAX) {
+                u = (uint32_t)ukeys.size();
+                table[pos] = u;
+                ukeys.push_back(sl.key);
+                uhash.push_back(h);
+                st.sref.push_back(cur_ref);
+            }
+            st.src[i] = u;
         }
-        if (!cur || (sl.essid != cur && *sl.essid != *cur)) {
-            cur = sl.essid;
-            run++;
-            std::vector<uint32_t> sb;
-            const uint32_t nb = build_salt_blocks(*cur, sb);
-            cur_ref = (uint32_t)st.spool.size();
-            st.spool.push_back(nb);
-            st.spool.insert(st.spool.end(), sb.begin(), sb.end());
-        }
-        const uint64_t h = hash_bytes(sl.key.data(), sl.key.size(), run);
-        size_t pos = h & (tcap - 1);
-        uint32_t u;
-        while ((u = table[pos]) != UINT32_MAX && !(uhash[u] == h && urun[u] == run && ukeys[u] == sl.key))
-            pos = (pos + 1) & (tcap - 1);
-        if (u == UINT32_MAX) {
-            u = (uint32_t)ukeys.size();
-            table[pos] = u;
-            ukeys.push_back(sl.key);
-            uhash.push_back(h);
-            urun.push_back(run);
-            st.sref.push_back(cur_ref);
-        }
-        st.src[i] = u;
+        i0 = i1;
     }
     const uint32_t nu = (uint32_t)ukeys.size();
     tr.mark("  dedup (ESSID, key)");
@@ -266,6 +273,7 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     st.bytes.assign(total + 8, 0);
     size_t pos = 0;
     for (uint32_t u = 0; u < nu; u++) {
+        if (u + 16 < nu) __builtin_prefetch(ukeys[u + 16].data());
         st.off[u] = pos;
         memcpy(st.bytes.data() + pos, ukeys[u].data(), ukeys[u].size());
         pos += ukeys[u].size();
@@ -405,7 +413,11 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         if (parsed[j].status) continue;
         rcs[j] = DWPA_MISS;
         if (!line_can_match(parsed[j])) continue;  // PMKID/MIC shorter than 16 bytes never verifies
+        keys[j].reserve(jobs[j].nkeys);
+        key_index[j].reserve(jobs[j].nkeys);
         for (size_t k = 0; k < jobs[j].nkeys; k++) {
+            // caller keys are scattered (one PHP string / Python bytes object each): prefetch ahead
+            if (k + 16 < jobs[j].nkeys && jobs[j].keys[k + 16].ptr) __builtin_prefetch(jobs[j].keys[k + 16].ptr);
             const dwpa_bytes& kb = jobs[j].keys[k];
             if (!kb.ptr) continue;  // is_null($key): skipped (common.php:172,240)
             std::string_view key((const char*)kb.ptr, kb.len);
