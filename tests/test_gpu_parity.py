@@ -268,3 +268,34 @@ def test_scan_run_many_essids_matches_per_group():
     for li, cand, nc, endian, pmk in results[0]:
         essid = next(e for l, _, e in plants if l == li)
         assert pmk == O.c_pbkdf2(words[cand], essid)
+
+
+def test_crack_files_hex_dictionary_and_outfile_escaping(tmp_path):
+    """A13/A15: $HEX[] dictionary words are decoded before hashing (help_crack.py:520-552, maint.php:55-60), CRLF
+    and empty lines are tolerated, and a PSK that is not printable ASCII or contains ':' is written back as
+    $HEX[..] (help_crack.py:807-815 reads the outfile as UTF-8 and splits on ':'); plain PSKs stay plain."""
+    rng = random.Random(21)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    psk_colon = b"pa:ss\xe9word!"          # ':' and a non-ASCII byte -> $HEX[] both ways
+    psk_plain = b"plain-psk-123"
+    lines = [S.pmkid_line(psk_colon, essid, ap, sta),
+             S.eapol_line(psk_plain, essid, ap, rng.randbytes(6), an, sn, 2, -2, "BE", rng=rng)]
+    hf = tmp_path / "h.hash"
+    hf.write_bytes(b"\n".join(lines) + b"\n")
+    words = [b"filler%05d" % i for i in range(3000)]
+    words[1000] = b"$HEX[" + psk_colon.hex().encode() + b"]"
+    words[2000] = psk_plain
+    d = tmp_path / "d.txt.gz"
+    with gzip.open(d, "wb") as f:
+        f.write(b"\r\n".join(words[:1500]) + b"\r\n\r\n" + b"\n".join(words[1500:]) + b"\n")
+    out = tmp_path / "o.key"
+    rc = dwpa_amd.crack_files(str(hf), [str(d)], None, 8, str(out))
+    assert rc == 0
+    recs = sorted(out.read_bytes().strip().split(b"\n"))
+    assert len(recs) == 2
+    assert sum(r.endswith(b":$HEX[" + psk_colon.hex().encode() + b"]") for r in recs) == 1
+    assert sum(r.endswith(b":" + psk_plain) for r in recs) == 1
+    # help_crack's get_key: split(":", 4) on the UTF-8 text recovers field 4 exactly
+    for r in recs:
+        arr = r.decode("utf-8").split(":", 4)
+        assert len(arr) == 5 and arr[1] == ap.hex()
