@@ -299,3 +299,63 @@ def test_crack_files_hex_dictionary_and_outfile_escaping(tmp_path):
     for r in recs:
         arr = r.decode("utf-8").split(":", 4)
         assert len(arr) == 5 and arr[1] == ap.hex()
+
+
+def _get_key(key_file):
+    """help_crack.py:804-815 (get_key): outfile records -> {MAC_AP: hex(PSK)} (k = arr[1][:12], v from arr[4])."""
+    res = {}
+    with open(key_file, encoding="utf-8", errors="ignore") as f:
+        for line in f:
+            arr = line.rstrip("\n").split(":", 4)
+            if len(arr) == 5:
+                res[arr[1][:12]] = arr[4].encode("utf-8").hex()
+    return res
+
+
+def test_help_crack_two_pass_flow(tmp_path):
+    """help_crack.py:923-933 through the ctypes drop-in: pass 1 without rules is exhausted (rc 1), pass 2 with the
+    work unit's rules ("-S -r help_crack.rules") cracks the rest (rc 0); get_key parses the outfile unchanged."""
+    from dwpa_amd.help_crack import run_cracker
+    rng = random.Random(31)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    alnum = b"abcdefghijklmnopqrstuvwxyz0123456789"  # outfile-safe PSKs: get_key returns them verbatim
+    base = [bytes(rng.choice(alnum) for _ in range(rng.randint(8, 14))) for _ in range(2000)]
+    rules = ["$1", "u", "c $2 $0 $2 $4"]
+    direct, ruled = base[42], R.apply(R.parse(rules[2]), base[1500])
+    ap2 = rng.randbytes(6)
+    lines = [S.pmkid_line(direct, essid, ap, sta),
+             S.eapol_line(ruled, essid, ap2, sta, an, sn, 2, 1, "LE", rng=rng)]
+    conf = {"hash_file": str(tmp_path / "help_crack.hash"), "key_file": str(tmp_path / "help_crack.key"),
+            "rules": "", "coptions": ""}
+    (tmp_path / "help_crack.hash").write_bytes(b"\n".join(lines) + b"\n")
+    d = tmp_path / "dict.txt.gz"
+    with gzip.open(d, "wb") as f:
+        f.write(b"\n".join(base) + b"\n")
+    assert run_cracker(conf, [str(d)]) == 1
+    assert _get_key(conf["key_file"]) == {ap.hex(): direct.hex()}
+    (tmp_path / "help_crack.rules").write_text("\n".join(rules) + "\n")
+    conf["rules"] = "-S -r " + str(tmp_path / "help_crack.rules")
+    (tmp_path / "help_crack.hash").write_bytes(lines[1] + b"\n")  # prepare_work writes the uncracked lines
+    assert run_cracker(conf, [str(d)]) == 0
+    assert _get_key(conf["key_file"]) == {ap.hex(): direct.hex(), ap2.hex(): ruled.hex()}
+    conf["hash_file"] = str(tmp_path / "missing.hash")
+    assert run_cracker(conf, [str(d)]) == -1
+
+
+def test_help_crack_expand_rules_file(tmp_path):
+    """`hashcat --stdout -r bestWPA.rule source.txt` (help_crack.py:508) via the GPU rule engine: the gz output
+    equals the rule oracle's expansion with rejected candidates skipped (parity with hashcat itself unpinned)."""
+    from dwpa_amd.help_crack import expand_rules
+    rng = random.Random(32)
+    words = [S.random_psk(rng, 1, 20) for _ in range(500)] + [b"x" * 300]
+    rules = wpa_rules()
+    src = tmp_path / "source.txt"
+    src.write_bytes(b"\n".join(words) + b"\n")
+    rf = tmp_path / "bestWPA.rule"
+    rf.write_text("\n".join(rules) + "\n")
+    out = tmp_path / "cracked.txt.gz"
+    n = expand_rules(str(rf), str(src), str(out), chunk=128)
+    exp = [c for row in R.expand(rules, words) for c in row if c is not None]
+    with gzip.open(out, "rb") as f:
+        got = f.read().split(b"\n")[:-1]
+    assert n == len(exp) and got == exp

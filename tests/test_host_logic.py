@@ -80,3 +80,14 @@ def test_rule_parser_matches_oracle_count():
     n = ctypes.c_uint32(0)
     assert lib.dwpa_rules_expand(0, text, len(text), None, 0, None, None, ctypes.byref(n)) == 0
     assert n.value == sum(1 for r in rules if R.parse(r))
+
+
+@pytest.mark.parametrize("rules,coptions,expect", [
+    ("", "", (None, 0)),
+    ("-S -r help_crack.rules", "", ("help_crack.rules", 0)),          # help_crack.py:445-447
+    ("", "-d 1,3 --force", (None, 0b101)),                             # hashcat numbers devices from 1
+    ("--rules-file=x.rule", "--backend-devices 2", ("x.rule", 0b10)),
+])
+def test_help_crack_option_parsing(rules, coptions, expect):
+    from dwpa_amd.help_crack import _parse_options
+    assert _parse_options(rules, coptions) == expect
