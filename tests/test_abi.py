@@ -66,3 +66,29 @@ def test_compute_fails_loudly_without_gpu():
         dwpa_amd.pbkdf2_pmk([b"password"], b"IEEE")
     lib = L.load()
     assert lib.dwpa_device_count() == L.DWPA_E_NODEV
+
+
+def _structs(txt):
+    """typedef struct { fields } name;  ->  {name: [normalised field declarations]}"""
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    out = {}
+    for body, name in re.findall(r"typedef\s+struct\s*\{(.*?)\}\s*(\w+)\s*;", txt, flags=re.S):
+        out[name] = [" ".join(f.split()) for f in body.split(";") if f.strip()]
+    return out
+
+
+def test_php_ffi_cdef_matches_header():
+    """php/dwpa22000.php declares the ABI again for FFI::cdef (the server binding, common.php:157-307); its structs
+    and prototypes must stay identical to include/dwpa22000.h (PHP is not installed here, so this is the check)."""
+    php = open(os.path.join(os.path.dirname(L.HEADER), "..", "php", "dwpa22000.php")).read()
+    cdef = re.search(r"<<<'CDEF'(.*?)CDEF;", php, flags=re.S).group(1)
+    hdr = open(L.HEADER).read()
+    hs, ps = _structs(hdr), _structs(cdef)
+    assert ps, "no structs in the PHP cdef"
+    for name, fields in ps.items():
+        assert hs.get(name) == fields, name
+    def norm(s):
+        s = " ".join(re.sub(r"/\*.*?\*/", "", s, flags=re.S).split())
+        return re.sub(r"\s+([,);])", r"\1", s)
+    for proto in re.findall(r"^\s*((?:int|const char \*)\s*dwpa_\w+\(.*?\);)", cdef, flags=re.M | re.S):
+        assert norm(proto) in norm(hdr), proto
