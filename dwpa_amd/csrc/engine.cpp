@@ -74,6 +74,35 @@ void DevBuf::release() {
     n = 0;
 }
 
+// Pinned host staging (hipHostMalloc): uploads from it are plain DMA, unlike pageable copies, which HIP stages
+// through its own buffers on the calling thread.  One arena per device, carved per call; the caller synchronises
+// the stream before the arena is reused.
+struct PinnedArena {
+    uint8_t* p = nullptr;
+    size_t cap = 0, used = 0;
+    int reset(size_t bytes) {
+        used = 0;
+        if (cap >= bytes) return 0;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipHostMalloc((void**)&p, bytes, hipHostMallocDefault) != hipSuccess) return DWPA_E_NOMEM;
+        cap = bytes;
+        return 0;
+    }
+    template <typename T>
+    T* take(size_t n) {
+        const size_t off = (used + 63) & ~(size_t)63;
+        used = off + n * sizeof(T);
+        return (T*)(p + off);
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = used = 0;
+    }
+};
+
 // ---------------------------------------------------------------------------------------------------------
 // global state
 // ---------------------------------------------------------------------------------------------------------
@@ -82,6 +111,7 @@ struct Device {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;   // check path: table uploads while PBKDF2 runs on `stream`
     hipEvent_t side_done = nullptr;
+    PinnedArena stage;            // check path: host staging of the derive uploads
     std::mutex mu;
     Batch batch;
     DevBuf lines, atts, pool, segs, salt, koff, kbytes, idsup;
@@ -196,11 +226,52 @@ static uint64_t hash_bytes(const char* p, size_t n, uint64_t seed) {
     return h ^ (h >> 29);
 }
 
-// Host staging of one derive step, kept alive until the stream that reads it is synchronised.
+// Host threads for the check path's host work: at least `min_per_thread` items each, at most 8 threads (the box
+// shares its cores; hardware_concurrency() reports the whole machine).
+static size_t host_threads(size_t n, size_t min_per_thread) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::max<size_t>(1, std::min<size_t>({8, hw ? hw : 1, n / std::max<size_t>(1, min_per_thread)}));
+}
+
+// fn(t) for t in [0, T) on T threads (the calling thread runs t = 0).
+template <typename F>
+static void parallel_for(size_t T, const F& fn) {
+    if (T <= 1) {
+        if (T == 1) fn(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < T; t++) th.emplace_back([&fn, t] { fn(t); });
+    fn(0);
+    for (auto& x : th) x.join();
+}
+
+// A typed view of pinned staging memory.
+template <typename T>
+struct Span {
+    T* p = nullptr;
+    size_t n = 0;
+    T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
+    T* data() const { return p; }
+    size_t size() const { return n; }
+};
+template <typename T>
+static Span<T> take(PinnedArena& a, size_t n) {
+    return Span<T>{a.take<T>(n), n};
+}
+template <typename T>
+static int upload_span(DevBuf& b, const Span<T>& v, hipStream_t s) {
+    RCHK(b.ensure(std::max<size_t>(v.n * sizeof(T), 16)));
+    if (v.n) HIPCHK(hipMemcpyAsync(b.p, v.p, v.n * sizeof(T), hipMemcpyHostToDevice, s));
+    return 0;
+}
+
+// Host staging of one derive step in the device's pinned arena; valid until the stream is synchronised.
 struct DeriveStage {
-    std::vector<uint64_t> off, ids;
-    std::vector<uint8_t> bytes;
-    std::vector<uint32_t> src, sref, spool, cpmk;
+    Span<uint64_t> off, ids;
+    Span<uint8_t> bytes;
+    Span<uint32_t> src, sref, spool, cpmk;
 };
 
 // Derive the PMKs of slots [b, e) into batch.pmk (slot order) and their key ordinals into batch.ids.  Unique
@@ -214,84 +285,134 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
     RCHK(d.batch.reserve(n, n));
-    st.src.assign(n, 0);
-    std::vector<std::string_view> ukeys;
-    ukeys.reserve(n);
-    st.sref.reserve(n);
-    // one small open-addressing table per ESSID run (a run's keys stay cache-resident; a whole-batch table
-    // costs a cache miss per key)
-    std::vector<uint32_t> table;
-    std::vector<uint64_t> uhash;
-    uhash.reserve(n);
-    for (uint32_t i0 = 0; i0 < n;) {
-        const std::string* essid = slots[b + i0].essid;
-        uint32_t i1 = i0 + 1;
-        while (i1 < n && (slots[b + i1].essid == essid || *slots[b + i1].essid == *essid)) i1++;
-        size_t tcap = 16;
-        while (tcap < 2 * (size_t)(i1 - i0)) tcap <<= 1;
-        table.assign(tcap, UINT32_MAX);
-        uint32_t cur_ref = UINT32_MAX;
-        for (uint32_t i = i0; i < i1; i++) {
-            const Slot& sl = slots[b + i];
-            if (i + 16 < i1) __builtin_prefetch(slots[b + i + 16].key.data());
-            if (!sl.pbkdf2) {
-                const uint8_t* p = job_pmk[sl.job];
-                st.src[i] = GATHER_CALLER | (uint32_t)(st.cpmk.size() / 8);
-                for (int k = 0; k < 8; k++)
-                    st.cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 |
-                                      (uint32_t)p[4 * k + 2] << 8 | p[4 * k + 3]);
-                continue;
+    // ESSID runs of this chunk (slots arrive grouped by ESSID)
+    std::vector<uint32_t> runs{0};
+    size_t keybytes = 0, saltwords = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        keybytes += slots[b + i].key.size();
+        if (i && slots[b + i].essid != slots[b + i - 1].essid && *slots[b + i].essid != *slots[b + i - 1].essid)
+            runs.push_back(i);
+    }
+    runs.push_back(n);
+    const size_t nruns = runs.size() - 1;
+    for (size_t r = 0; r < nruns; r++)  // count word + [2][nblk][16], nblk = SHA-1 blocks of ESSID || INT(i) || pad
+        saltwords += 1 + 32 * ((slots[b + runs[r]].essid->size() + 4 + 9 + 63) / 64);
+    // pinned staging, sized by upper bounds: <= n unique keys, <= keybytes key bytes, <= n caller PMKs
+    RCHK(d.stage.reset(8 * (n + 1) + keybytes + 8 + 4 * (size_t)n + 4 * saltwords + 32 * (size_t)n + 4 * (size_t)n +
+                       8 * (size_t)n + 8 * 64));
+    st.src = take<uint32_t>(d.stage, n);
+    st.ids = take<uint64_t>(d.stage, n);
+    // Runs are deduplicated independently (one small open-addressing table per run keeps it cache-resident), on
+    // up to 8 host threads that each take a contiguous block of runs; the parts are then concatenated.
+    struct Part {
+        std::vector<std::string_view> ukeys;
+        std::vector<uint32_t> sref, spool, cpmk;  // sref: offsets into this part's spool
+        size_t rb = 0, re = 0, ubase = 0, sbase = 0, cbase = 0, bbase = 0;
+    };
+    const size_t T = host_threads(n, 16384);
+    std::vector<Part> parts(std::min(T, nruns));
+    for (size_t t = 0; t < parts.size(); t++) {  // split runs so that parts hold about equal slot counts
+        parts[t].rb = t ? parts[t - 1].re : 0;
+        const uint64_t goal = (uint64_t)n * (t + 1) / parts.size();
+        size_t r = parts[t].rb;
+        while (r < nruns && (runs[r + 1] <= goal || r == parts[t].rb)) r++;
+        parts[t].re = t + 1 == parts.size() ? nruns : r;
+    }
+    parallel_for(parts.size(), [&](size_t t) {
+        Part& P = parts[t];
+        std::vector<uint32_t> table;
+        std::vector<uint64_t> uhash;
+        for (size_t r = P.rb; r < P.re; r++) {
+            const uint32_t i0 = runs[r], i1 = runs[r + 1];
+            size_t tcap = 16;
+            while (tcap < 2 * (size_t)(i1 - i0)) tcap <<= 1;
+            table.assign(tcap, UINT32_MAX);
+            const size_t u0 = P.ukeys.size();
+            uint32_t cur_ref = UINT32_MAX;
+            for (uint32_t i = i0; i < i1; i++) {
+                const Slot& sl = slots[b + i];
+                if (i + 16 < i1) __builtin_prefetch(slots[b + i + 16].key.data());
+                if (!sl.pbkdf2) {
+                    const uint8_t* p = job_pmk[sl.job];
+                    st.src[i] = GATHER_CALLER | (uint32_t)(P.cpmk.size() / 8);
+                    for (int k = 0; k < 8; k++)
+                        P.cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 |
+                                         (uint32_t)p[4 * k + 2] << 8 | p[4 * k + 3]);
+                    continue;
+                }
+                if (cur_ref == UINT32_MAX) {
+                    std::vector<uint32_t> sb;
+                    const uint32_t nb = build_salt_blocks(*sl.essid, sb);
+                    cur_ref = (uint32_t)P.spool.size();
+                    P.spool.push_back(nb);
+                    P.spool.insert(P.spool.end(), sb.begin(), sb.end());
+                }
+                const uint64_t h = hash_bytes(sl.key.data(), sl.key.size(), 0);
+                size_t pos = h & (tcap - 1);
+                uint32_t u;
+                while ((u = table[pos]) != UINT32_MAX && !(uhash[u - u0] == h && P.ukeys[u] == sl.key))
+                    pos = (pos + 1) & (tcap - 1);
+                if (u == UINT32_MAX) {
+                    u = (uint32_t)P.ukeys.size();
+                    table[pos] = u;
+                    P.ukeys.push_back(sl.key);
+                    uhash.push_back(h);
+                    P.sref.push_back(cur_ref);
+                }
+                st.src[i] = u;  // part-local; rebased below
             }
-            if (cur_ref == UINT32_MAX) {
-                std::vector<uint32_t> sb;
-                const uint32_t nb = build_salt_blocks(*essid, sb);
-                cur_ref = (uint32_t)st.spool.size();
-                st.spool.push_back(nb);
-                st.spool.insert(st.spool.end(), sb.begin(), sb.end());
-            }
-            const uint64_t h = hash_bytes(sl.key.data(), sl.key.size(), 0);
-            size_t pos = h & (tcap - 1);
-            uint32_t u;
-            while ((u = table[pos]) != UINT32_MAX && !(uhash[u] == h && ukeys[u] == sl.key)) pos = (pos + 1) & (tcap - 1);
-            if (u == UINT32_MAX) {
-                u = (uint32_t)ukeys.size();
-                table[pos] = u;
-                ukeys.push_back(sl.key);
-                uhash.push_back(h);
-                st.sref.push_back(cur_ref);
-            }
-            st.src[i] = u;
+            uhash.clear();
         }
-        i0 = i1;
+    });
+    size_t nu_total = 0, nsp = 0, ncp = 0, nbytes = 0;
+    for (Part& P : parts) {
+        P.ubase = nu_total;
+        P.sbase = nsp;
+        P.cbase = ncp;
+        P.bbase = nbytes;
+        nu_total += P.ukeys.size();
+        nsp += P.spool.size();
+        ncp += P.cpmk.size() / 8;
+        for (std::string_view k : P.ukeys) nbytes += k.size();
     }
-    const uint32_t nu = (uint32_t)ukeys.size();
+    const uint32_t nu = (uint32_t)nu_total;
+    st.sref = take<uint32_t>(d.stage, nu);
+    st.spool = take<uint32_t>(d.stage, nsp);
+    st.cpmk = take<uint32_t>(d.stage, ncp * 8);
+    st.off = take<uint64_t>(d.stage, nu + 1);
+    st.bytes = take<uint8_t>(d.stage, nbytes + 8);
+    if (d.stage.used > d.stage.cap) return DWPA_E_ARG;  // the bounds above are exact upper bounds
+    memset(st.bytes.data() + nbytes, 0, 8);
+    // rebase and concatenate; unique keys -> offsets/bytes (back to back: k_prep_dict derives len from offsets)
+    parallel_for(parts.size(), [&](size_t t) {
+        const Part& P = parts[t];
+        for (uint32_t i = runs[P.rb]; i < runs[P.re]; i++)
+            st.src[i] = (st.src[i] & GATHER_CALLER) ? st.src[i] + (uint32_t)P.cbase : st.src[i] + (uint32_t)P.ubase;
+        for (size_t u = 0; u < P.ukeys.size(); u++) st.sref[P.ubase + u] = P.sref[u] + (uint32_t)P.sbase;
+        std::copy(P.spool.begin(), P.spool.end(), st.spool.data() + P.sbase);
+        std::copy(P.cpmk.begin(), P.cpmk.end(), st.cpmk.data() + 8 * P.cbase);
+        size_t pos = P.bbase;
+        for (size_t u = 0; u < P.ukeys.size(); u++) {
+            if (u + 16 < P.ukeys.size()) __builtin_prefetch(P.ukeys[u + 16].data());
+            st.off[P.ubase + u] = pos;
+            memcpy(st.bytes.data() + pos, P.ukeys[u].data(), P.ukeys[u].size());
+            pos += P.ukeys[u].size();
+        }
+    });
+    st.off[nu] = nbytes;
     tr.mark("  dedup (ESSID, key)");
-    // unique keys -> offsets/bytes (back to back: k_prep_dict derives len = off[i+1] - off[i])
-    st.off.assign(nu + 1, 0);
-    size_t total = 0;
-    for (uint32_t u = 0; u < nu; u++) total += ukeys[u].size();
-    st.bytes.assign(total + 8, 0);
-    size_t pos = 0;
-    for (uint32_t u = 0; u < nu; u++) {
-        if (u + 16 < nu) __builtin_prefetch(ukeys[u + 16].data());
-        st.off[u] = pos;
-        memcpy(st.bytes.data() + pos, ukeys[u].data(), ukeys[u].size());
-        pos += ukeys[u].size();
-    }
-    st.off[nu] = pos;
     // ids = key ordinals (select the PHP attempt list of each key)
-    st.ids.resize(n);
     for (uint32_t i = 0; i < n; i++) st.ids[i] = slots[b + i].ordinal;
 
     RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
     if (nu) {
-        RCHK(upload(d.koff, st.off, s));
-        RCHK(upload(d.kbytes, st.bytes, s));
-        RCHK(upload(d.salt, st.spool, s));
-        RCHK(upload(d.sref, st.sref, s));
+        RCHK(upload_span(d.koff, st.off, s));
+        RCHK(upload_span(d.kbytes, st.bytes, s));
+        RCHK(upload_span(d.salt, st.spool, s));
+        RCHK(upload_span(d.sref, st.sref, s));
     }
-    RCHK(upload(d.cpmk, st.cpmk, s));
-    RCHK(upload(d.src, st.src, s));
+    RCHK(upload_span(d.cpmk, st.cpmk, s));
+    RCHK(upload_span(d.src, st.src, s));
     HIPCHK(hipMemcpyAsync(d.batch.ids.p, st.ids.data(), n * 8, hipMemcpyHostToDevice, s));
     tr.mark("  stage+upload");
     if (nu) {
@@ -400,9 +521,11 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     std::vector<uint32_t> job_line(njobs, 0);
     std::vector<const uint8_t*> job_pmk(njobs, nullptr);
     std::vector<std::vector<std::string_view>> keys(njobs);
-    std::deque<std::string> unhexed;  // decoded $HEX[] keys (stable addresses)
     std::vector<std::vector<uint32_t>> key_index(njobs);
-    for (size_t j = 0; j < njobs; j++) {
+    const size_t TP = host_threads(njobs, 64);
+    std::vector<std::deque<std::string>> unhexed(TP);  // decoded $HEX[] keys (stable addresses), per thread
+    parallel_for(TP, [&](size_t t) {
+      for (size_t j = njobs * t / TP; j < njobs * (t + 1) / TP; j++) {
         out[j].key_index = -1;
         out[j].nc = 0;
         out[j].endian = 0;
@@ -422,14 +545,15 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
             if (!kb.ptr) continue;  // is_null($key): skipped (common.php:172,240)
             std::string_view key((const char*)kb.ptr, kb.len);
             if (starts_hex(kb.ptr, kb.len)) {
-                unhexed.push_back(hc_unhex(std::string(key)));
-                key = unhexed.back();
+                unhexed[t].push_back(hc_unhex(std::string(key)));
+                key = unhexed[t].back();
             }
             keys[j].push_back(key);
             key_index[j].push_back((uint32_t)k);
         }
         job_pmk[j] = jobs[j].pmk;
-    }
+      }
+    });
     tr.mark("parse+keys");
     // slots grouped by ESSID (jobs in input order within an ESSID, keys in order within a job)
     std::unordered_map<std::string_view, uint32_t> essid_id;
@@ -877,6 +1001,7 @@ void dwpa_shutdown(void) {
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();
         d->batch.cap = d->batch.hitcap = 0;
+        d->stage.release();
         if (d->stream) (void)hipStreamDestroy(d->stream);
         if (d->side) (void)hipStreamDestroy(d->side);
         if (d->side_done) (void)hipEventDestroy(d->side_done);
