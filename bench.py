@@ -54,9 +54,10 @@ def parse():
     ap.add_argument("--dict-words", type=int, default=DICT_WORDS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5"], default="c2",
+    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files"], default="c2",
                     help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs; "
-                         "c1/c5 = the FFI check path (host buffers, PCIe-inclusive)")
+                         "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
+                         "dwpa_crack_files from a gz dictionary on disk (the help_crack client path)")
     ap.add_argument("--essids", type=int, default=1000, help="c3: number of ESSIDs (BASELINE: 1000)")
     return ap.parse_args()
 
@@ -207,6 +208,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.workload in ("c1", "c5"):
         return main_ffi(args, world, rank, local)
+    if args.workload == "c2files":
+        return main_files(args, world, rank, local)
     if world > 1:
         # control plane only (barrier, max-over-ranks time, sum of PMKs): the data path shards the keyspace and
         # never exchanges data, so there is no RCCL collective on the GPU.
@@ -391,6 +394,87 @@ def main_ffi(args, world, rank, local):
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0 and not verified:
+        sys.exit(3)
+
+
+def main_files(args, world, rank, local):
+    """C2 end to end through the client path (dwpa_crack_files, help_crack.py:765-802): the 100M-word dictionary
+    as a gzip file on local disk, streamed, inflated and $HEX[]-decoded on the host, uploaded chunk by chunk and
+    scanned against the C2 line (hashcat nonce mode, --nonce-error-corrections=8).  The planted PSK is the
+    99,999,000th word, so the run covers the dictionary up to there.  One pass = one step; N>1 runs replicas."""
+    import gzip
+    import random
+    import tempfile
+    import numpy as np
+    import torch.distributed as dist
+    import dwpa_amd
+    from dwpa_amd import synth as S
+    from dwpa_amd.shard import reduce_timing
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    n = args.dict_words
+    plant = min(PLANT_INDEX, n - 1)
+    rng = np.random.default_rng(2)
+    lens = np.clip(rng.geometric(0.3, n) + 7, 8, 63).astype(np.int64)
+    ends = np.cumsum(lens + 1)
+    text = rng.integers(0x21, 0x7F, int(ends[-1]), dtype=np.uint8)
+    text[ends - 1] = 0x0A
+    psk = text[int(ends[plant - 1]) if plant else 0:int(ends[plant]) - 1].tobytes()
+    rr = random.Random(1)
+    essid, ap, sta, an, sn = S.random_net(rr, essid_len=10)
+    line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rr)
+    tmp = tempfile.mkdtemp(prefix="dwpa_c2files_")
+    dpath, hpath, opath = (os.path.join(tmp, x) for x in ("dict.txt.gz", "h.hash", "o.key"))
+    t0 = time.perf_counter()
+    with gzip.open(dpath, "wb", compresslevel=1) as f:
+        step = 64 << 20
+        for o in range(0, len(text), step):
+            f.write(text[o:o + step].tobytes())
+    gz_s = time.perf_counter() - t0
+    gz_bytes = os.path.getsize(dpath)
+    del text
+    with open(hpath, "wb") as f:
+        f.write(line + b"\n")
+    cracked = True
+    times = []
+    for rep in range(args.warmup + args.steps):
+        if os.path.exists(opath):
+            os.remove(opath)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        rc = dwpa_amd.crack_files(hpath, [dpath], None, 8, opath, device_mask=1 << local, batch=args.batch)
+        el = time.perf_counter() - t0
+        if rep >= args.warmup:
+            times.append(el)
+        recs = open(opath, "rb").read().strip().split(b"\n") if os.path.exists(opath) else []
+        cracked &= rc == 0 and len(recs) == 1 and recs[0].endswith(b":" + psk)
+    elapsed = sum(times) / len(times)
+    words = plant + 1
+    if world > 1:
+        elapsed, total = reduce_timing(dist, elapsed, float(words))
+    else:
+        total = float(words)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "C2 via dwpa_crack_files: 100M-word gzip dictionary on local disk (streamed, "
+                                   "inflated and uploaded per chunk), one EAPOL keyver-2 line, hashcat NC mode 8",
+                       "dict_words": n, "gz_bytes": gz_bytes, "gz_write_s": round(gz_s, 2),
+                       "words_scanned_per_pass": words, "batch": args.batch,
+                       "parallelism": f"replicas x{world}"},
+            "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked)}), flush=True)
+    for x in (dpath, hpath, opath):
+        if os.path.exists(x):
+            os.remove(x)
+    os.rmdir(tmp)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0 and not cracked:
         sys.exit(3)
 
 

@@ -32,7 +32,9 @@ struct Chunk {
     size_t words() const { return off.empty() ? 0 : off.size() - 1; }
 };
 
-// Dictionary reader: plain or gzip (zlib reads both), one word per line, "\n" or "\r\n", $HEX[] decoded.
+// Dictionary reader: plain or gzip (zlib reads both), one word per line, "\n" or "\r\n", $HEX[] decoded.  Lines
+// are cut straight out of the inflate buffer with memchr and appended to the chunk (no per-line allocation): the
+// reader has to keep up with 8 GPUs at ~5 M words/s each when a work unit has one ESSID and no rules.
 class DictReader {
   public:
     explicit DictReader(const std::vector<std::string>& paths) : paths_(paths) {}
@@ -47,17 +49,41 @@ class DictReader {
                 gz_ = gzopen(paths_[idx_].c_str(), "rb");
                 if (!gz_) { err = true; return false; }
                 gzbuffer(gz_, 1 << 20);
+                pos_ = len_ = 0;
             }
-            std::string line;
-            if (!getline(line)) {
-                gzclose(gz_);
-                gz_ = nullptr;
-                idx_++;
-                continue;
+            if (pos_ >= len_) {
+                const int r = gzread(gz_, buf_, sizeof(buf_));
+                if (r < 0) { err = true; return false; }
+                if (r == 0) {  // end of this file: a last line without '\n' is still a word
+                    if (!partial_.empty()) emit(c, partial_.data(), partial_.size());
+                    partial_.clear();
+                    gzclose(gz_);
+                    gz_ = nullptr;
+                    idx_++;
+                    continue;
+                }
+                pos_ = 0;
+                len_ = (size_t)r;
             }
-            if (starts_hex((const uint8_t*)line.data(), line.size())) line = hc_unhex(line);
-            c.bytes += line;
-            c.off.push_back(c.bytes.size());
+            const char* p = buf_ + pos_;
+            const char* end = buf_ + len_;
+            while (p < end && c.words() < max_words && c.bytes.size() < max_bytes) {
+                const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+                if (!nl) {
+                    partial_.append(p, (size_t)(end - p));
+                    p = end;
+                    break;
+                }
+                if (!partial_.empty()) {
+                    partial_.append(p, (size_t)(nl - p));
+                    emit(c, partial_.data(), partial_.size());
+                    partial_.clear();
+                } else {
+                    emit(c, p, (size_t)(nl - p));
+                }
+                p = nl + 1;
+            }
+            pos_ = (size_t)(p - buf_);
         }
         return c.words() > 0;
     }
@@ -66,41 +92,18 @@ class DictReader {
     }
 
   private:
-    bool getline(std::string& out) {
-        out.clear();
-        for (;;) {
-            if (pos_ >= len_) {
-                int r = gzread(gz_, buf_, sizeof(buf_));
-                if (r <= 0) {
-                    if (out.empty() && !pending_) return false;
-                    pending_ = false;
-                    break;
-                }
-                len_ = (size_t)r;
-                pos_ = 0;
-            }
-            const char* b = buf_ + pos_;
-            const void* nl = memchr(b, '\n', len_ - pos_);
-            if (nl) {
-                size_t k = (const char*)nl - b;
-                out.append(b, k);
-                pos_ += k + 1;
-                pending_ = false;
-                break;
-            }
-            out.append(b, len_ - pos_);
-            pending_ = true;
-            pos_ = len_;
-        }
-        if (!out.empty() && out.back() == '\r') out.pop_back();
-        return true;
+    static void emit(Chunk& c, const char* p, size_t k) {
+        if (k && p[k - 1] == '\r') k--;
+        if (k > 5 && p[0] == '$' && starts_hex((const uint8_t*)p, k)) c.bytes += hc_unhex(std::string(p, k));
+        else c.bytes.append(p, k);
+        c.off.push_back(c.bytes.size());
     }
     std::vector<std::string> paths_;
     size_t idx_ = 0;
     gzFile gz_ = nullptr;
     char buf_[1 << 16];
     size_t pos_ = 0, len_ = 0;
-    bool pending_ = false;
+    std::string partial_;
 };
 
 struct CrackShared {
@@ -118,25 +121,42 @@ static std::string outfile_record(const ParsedLine& p, const std::string& psk) {
            hashcat_plain(p.essid) + ":" + hashcat_plain(psk) + "\n";
 }
 
+// Per-device state.  Shards are uploaded into one of two buffer slots on the `up` stream by the thread that read
+// the chunk, so the upload of chunk k+1 overlaps the scan of chunk k; the scan waits on `staged[slot]`.
 struct DevWork {
     int device;
     dwpa_scan* scan = nullptr;
-    DevBuf off, bytes;
-    hipStream_t stream = nullptr;
+    DevBuf off[2], bytes[2];
+    std::vector<uint64_t> hoff[2];  // host staging of the rebased offsets (alive until the upload completes)
+    hipStream_t stream = nullptr, up = nullptr;
+    hipEvent_t staged[2] = {nullptr, nullptr};
 };
 
-static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, size_t e, const RuleSet* rules,
-                      DevRules* drules) {
-    if (e <= b) return 0;
+// Upload words [b, e) of chunk c (offsets rebased to the shard) into slot `slot` of device w.
+static int stage_shard(DevWork& w, const Chunk& c, size_t b, size_t e, int slot) {
     if (hipSetDevice(w.device) != hipSuccess) return DWPA_E_HIP;
-    // upload shard (offsets rebased to the shard)
-    std::vector<uint64_t> off(e - b + 1);
+    std::vector<uint64_t>& off = w.hoff[slot];
+    off.resize(e - b + 1);
     for (size_t i = b; i <= e; i++) off[i - b] = c.off[i] - c.off[b];
     const size_t nbytes = c.off[e] - c.off[b];
-    if (w.off.ensure(off.size() * 8) || w.bytes.ensure(nbytes + 64)) return DWPA_E_NOMEM;
-    if (hipMemcpyAsync(w.off.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, w.stream) != hipSuccess ||
-        hipMemcpyAsync(w.bytes.p, c.bytes.data() + c.off[b], nbytes, hipMemcpyHostToDevice, w.stream) != hipSuccess)
+    DevBuf& ob = w.off[slot];
+    DevBuf& bb = w.bytes[slot];
+    if ((ob.n < off.size() * 8 && ob.ensure(off.size() * 8 * 3 / 2)) || (bb.n < nbytes + 64 && bb.ensure((nbytes + 64) * 3 / 2)))
+        return DWPA_E_NOMEM;
+    if (hipMemcpyAsync(ob.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, w.up) != hipSuccess ||
+        (nbytes && hipMemcpyAsync(bb.p, c.bytes.data() + c.off[b], nbytes, hipMemcpyHostToDevice, w.up) != hipSuccess) ||
+        hipEventRecord(w.staged[slot], w.up) != hipSuccess || hipStreamSynchronize(w.up) != hipSuccess)
         return DWPA_E_HIP;
+    return 0;
+}
+
+static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, size_t e, const RuleSet* rules,
+                      DevRules* drules, int slot) {
+    if (e <= b) return 0;
+    if (hipSetDevice(w.device) != hipSuccess) return DWPA_E_HIP;
+    if (hipStreamWaitEvent(w.stream, w.staged[slot], 0) != hipSuccess) return DWPA_E_HIP;
+    const DevBuf& woff = w.off[slot];
+    const DevBuf& wbytes = w.bytes[slot];
     const uint32_t cap = scan_batch_cap(w.scan);
     const size_t words = e - b;
     const uint64_t nrules = rules ? rules->size() : 1;
@@ -147,9 +167,9 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
         const uint32_t nw = (uint32_t)std::min<size_t>(words_per_batch, words - wb);
         int r;
         if (rules)
-            r = rules_load(w.scan, drules, (const uint64_t*)w.off.p, (const uint8_t*)w.bytes.p, wb, nw, w.stream);
+            r = rules_load(w.scan, drules, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, w.stream);
         else
-            r = scan_load_dict(w.scan, (const uint64_t*)w.off.p, (const uint8_t*)w.bytes.p, wb, nw, 8, 63, w.stream);
+            r = scan_load_dict(w.scan, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, 8, 63, w.stream);
         if (r < 0) return r;
         if ((r = scan_run(w.scan, w.stream)) < 0) return r;  // all ESSID groups, grouped per launch
         std::vector<HitDev> hits;
@@ -232,7 +252,11 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     for (size_t k = 0; k < devs.size() && rc >= 0; k++) {
         work[k].device = devs[k];
         (void)hipSetDevice(devs[k]);
-        if (hipStreamCreateWithFlags(&work[k].stream, hipStreamNonBlocking) != hipSuccess) rc = DWPA_E_HIP;
+        if (hipStreamCreateWithFlags(&work[k].stream, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&work[k].up, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&work[k].staged[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&work[k].staged[1], hipEventDisableTiming) != hipSuccess)
+            rc = DWPA_E_HIP;
         if (rc >= 0) rc = scan_create(devs[k], lp.data(), ll.data(), lines.size(), nec, nc_mode, batch, &work[k].scan);
         if (rc >= 0 && rp) rc = rules_upload(devs[k], rules, &drules[k]);
     }
@@ -242,39 +266,61 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     DictReader reader(dpaths);
     bool ioerr = false;
     const size_t chunk_words = (size_t)batch * devs.size() * 8;
-    // double-buffered: the next chunk is read/inflated on a host thread while the devices scan this one
+    // double-buffered: the next chunk is read/inflated on a host thread while the devices scan this one.  The
+    // first chunk is one batch per device, so the GPUs start after ~0.3 s of reading instead of a full chunk's.
+    // Chunks then double until they reach chunk_words, so each read stays shorter than the previous chunk's scan.
     Chunk cur, nxt;
-    bool have = reader.next(cur, chunk_words, (size_t)1 << 31, ioerr);
+    size_t next_words = (size_t)batch * devs.size();
+    const size_t G = work.size();
+    // contiguous, equal shards of a chunk, one per device, staged into buffer slot `slot`
+    auto stage_all = [&](const Chunk& c, int slot) {
+        int r = 0;
+        for (size_t k = 0; k < G && r >= 0; k++) r = stage_shard(work[k], c, c.words() * k / G, c.words() * (k + 1) / G, slot);
+        return r;
+    };
+    bool have = reader.next(cur, next_words, (size_t)1 << 31, ioerr);
+    int slot = 0, stage_rc = 0;
+    if (have && rc >= 0) rc = stage_all(cur, slot);
     while (rc >= 0 && have && sh.ncracked < sh.valid) {
         bool have_next = false;
-        std::thread prefetch([&] { have_next = reader.next(nxt, chunk_words, (size_t)1 << 31, ioerr); });
+        next_words = std::min(chunk_words, 2 * next_words);
+        std::thread prefetch([&] {
+            have_next = reader.next(nxt, next_words, (size_t)1 << 31, ioerr);
+            if (have_next) stage_rc = stage_all(nxt, slot ^ 1);
+        });
         {
             std::lock_guard<std::mutex> lk(sh.mu);  // retire lines cracked so far on every device
             for (size_t k = 0; k < work.size(); k++)
                 for (size_t i = 0; i < lines.size(); i++)
                     if (sh.cracked[i]) scan_mark_cracked(work[k].scan, (uint32_t)i);
         }
-        const size_t W = cur.words(), G = work.size();
+        const size_t W = cur.words();
         std::vector<std::thread> th;
         std::vector<int> rcs(G, 0);
         for (size_t k = 0; k < G; k++) {
             const size_t b = W * k / G, e = W * (k + 1) / G;
-            th.emplace_back([&, k, b, e] { rcs[k] = scan_shard(work[k], sh, cur, b, e, rp, &drules[k]); });
+            th.emplace_back([&, k, b, e] { rcs[k] = scan_shard(work[k], sh, cur, b, e, rp, &drules[k], slot); });
         }
         for (auto& t : th) t.join();
         prefetch.join();
         for (int r : rcs)
             if (r < 0) rc = r;
+        if (stage_rc < 0) rc = stage_rc;
         std::swap(cur, nxt);
+        slot ^= 1;
         have = have_next;
     }
     for (size_t k = 0; k < work.size(); k++) {
         if (work[k].scan) scan_destroy(work[k].scan);
         (void)hipSetDevice(work[k].device);
-        work[k].off.release();
-        work[k].bytes.release();
+        for (int q = 0; q < 2; q++) {
+            work[k].off[q].release();
+            work[k].bytes[q].release();
+            if (work[k].staged[q]) (void)hipEventDestroy(work[k].staged[q]);
+        }
         rules_release(&drules[k]);
         if (work[k].stream) (void)hipStreamDestroy(work[k].stream);
+        if (work[k].up) (void)hipStreamDestroy(work[k].up);
     }
     fclose(sh.out);
     if (rc < 0 || ioerr) return DWPA_RC_ERROR;
