@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -104,6 +106,70 @@ class DictReader {
     char buf_[1 << 16];
     size_t pos_ = 0, len_ = 0;
     std::string partial_;
+};
+
+// Dictionary chunks from several files at once: worker t reads files t, t+T, ... with its own DictReader and
+// queues its chunks (first chunk small, then doubling to max_words), so inflating several gz dictionaries uses
+// several host cores.  Chunks arrive in completion order; candidate order only decides which of two identical
+// PSKs is written, so the outfile is the same as hashcat's.
+class ChunkSource {
+  public:
+    ChunkSource(const std::vector<std::string>& paths, size_t first_words, size_t max_words) {
+        const size_t T = std::max<size_t>(1, std::min<size_t>(paths.size(), 4));
+        cap_ = T + 1;
+        live_ = T;
+        for (size_t t = 0; t < T; t++) {
+            std::vector<std::string> mine;
+            for (size_t i = t; i < paths.size(); i += T) mine.push_back(paths[i]);
+            workers_.emplace_back([this, mine, first_words, max_words, T] { work(mine, first_words, std::max<size_t>(first_words, max_words / T)); });
+        }
+    }
+    ~ChunkSource() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& w : workers_) w.join();
+    }
+    // Blocks until a chunk is ready; false once every file is read (or on an I/O error: err is set).
+    bool next(Chunk& c, bool& err) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty() || live_ == 0; });
+        err = err || err_;
+        if (q_.empty()) return false;
+        c = std::move(q_.front());
+        q_.pop_front();
+        cv_.notify_all();
+        return true;
+    }
+
+  private:
+    void work(const std::vector<std::string>& paths, size_t words, size_t max_words) {
+        DictReader reader(paths);
+        bool err = false;
+        for (;;) {
+            Chunk c;
+            const bool have = reader.next(c, words, (size_t)1 << 31, err);
+            words = std::min(max_words, 2 * words);
+            std::unique_lock<std::mutex> lk(mu_);
+            if (!have || err || stop_) break;
+            cv_.wait(lk, [&] { return q_.size() < cap_ || stop_; });
+            if (stop_) break;
+            q_.push_back(std::move(c));
+            cv_.notify_all();
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        err_ = err_ || err;
+        live_--;
+        cv_.notify_all();
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Chunk> q_;
+    size_t cap_ = 2, live_ = 0;
+    bool stop_ = false, err_ = false;
+    std::vector<std::thread> workers_;
 };
 
 struct CrackShared {
@@ -263,14 +329,13 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
 
     std::vector<std::string> dpaths;
     for (size_t i = 0; i < ndicts; i++) dpaths.push_back(dicts[i]);
-    DictReader reader(dpaths);
     bool ioerr = false;
     const size_t chunk_words = (size_t)batch * devs.size() * 8;
     // double-buffered: the next chunk is read/inflated on a host thread while the devices scan this one.  The
     // first chunk is one batch per device, so the GPUs start after ~0.3 s of reading instead of a full chunk's.
     // Chunks then double until they reach chunk_words, so each read stays shorter than the previous chunk's scan.
     Chunk cur, nxt;
-    size_t next_words = (size_t)batch * devs.size();
+    ChunkSource source(dpaths, (size_t)batch * devs.size(), chunk_words);
     const size_t G = work.size();
     // contiguous, equal shards of a chunk, one per device, staged into buffer slot `slot`
     auto stage_all = [&](const Chunk& c, int slot) {
@@ -278,14 +343,13 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
         for (size_t k = 0; k < G && r >= 0; k++) r = stage_shard(work[k], c, c.words() * k / G, c.words() * (k + 1) / G, slot);
         return r;
     };
-    bool have = reader.next(cur, next_words, (size_t)1 << 31, ioerr);
+    bool have = source.next(cur, ioerr);
     int slot = 0, stage_rc = 0;
     if (have && rc >= 0) rc = stage_all(cur, slot);
     while (rc >= 0 && have && sh.ncracked < sh.valid) {
         bool have_next = false;
-        next_words = std::min(chunk_words, 2 * next_words);
         std::thread prefetch([&] {
-            have_next = reader.next(nxt, next_words, (size_t)1 << 31, ioerr);
+            have_next = source.next(nxt, ioerr);
             if (have_next) stage_rc = stage_all(nxt, slot ^ 1);
         });
         {
