@@ -359,3 +359,33 @@ def test_help_crack_expand_rules_file(tmp_path):
     with gzip.open(out, "rb") as f:
         got = f.read().split(b"\n")[:-1]
     assert n == len(exp) and got == exp
+
+
+def test_crack_files_several_dictionaries(tmp_path):
+    """help_crack passes a dictionary list (help_crack.py:520-552): plain and gz files are read in parallel, a
+    last line without '\\n' is still a word, and every planted PSK is found whichever file holds it."""
+    rng = random.Random(41)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    alnum = b"abcdefghijklmnopqrstuvwxyz0123456789"
+    files, lines, psks = [], [], []
+    for f in range(3):
+        words = [bytes(rng.choice(alnum) for _ in range(rng.randint(8, 16))) for _ in range(20000 + 5000 * f)]
+        psk = words[-1] if f == 2 else words[rng.randrange(len(words))]
+        psks.append(psk)
+        a = rng.randbytes(6)
+        lines.append(S.pmkid_line(psk, essid, a, sta) if f != 1 else
+                     S.eapol_line(psk, essid, a, sta, an, sn, 2, f, "LE", rng=rng))
+        body = b"\n".join(words) + (b"" if f == 2 else b"\n")  # file 2 ends without a newline
+        path = tmp_path / (f"d{f}.txt" if f == 0 else f"d{f}.txt.gz")
+        if f == 0:
+            path.write_bytes(body)
+        else:
+            with gzip.open(path, "wb") as fh:
+                fh.write(body)
+        files.append(str(path))
+    hf = tmp_path / "h.hash"
+    hf.write_bytes(b"\n".join(lines) + b"\n")
+    out = tmp_path / "o.key"
+    assert dwpa_amd.crack_files(str(hf), files, None, 8, str(out), batch=1 << 14) == 0
+    recs = out.read_bytes().strip().split(b"\n")
+    assert sorted(r.rsplit(b":", 1)[1] for r in recs) == sorted(psks)
