@@ -206,6 +206,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("DWPA_BENCH_ONE_DEVICE") == "1":
+        local = 0  # rehearsal of the N>1 control path with every rank on one GPU (not a scaling measurement)
     if args.workload in ("c1", "c5"):
         return main_ffi(args, world, rank, local)
     if args.workload == "c2files":
