@@ -376,7 +376,6 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
         L.mic_nblk = (uint32_t)(w.size() / 16);
         pool.insert(pool.end(), w.begin(), w.end());
     } else {
-        any_aes = true;
         const size_t len = p.eapol.size();
         const size_t nb = (len + 15) / 16;
         std::string b = p.eapol;

@@ -35,7 +35,6 @@ struct TableBuilder {
     std::vector<AttDev> atts;
     std::vector<uint32_t> pool;  // pre-padded hash blocks (16 words each) and CMAC blocks (4 words each)
     std::vector<uint8_t> never;  // per line: 1 if the line can never match (target shorter than 16 bytes)
-    bool any_aes = false;
 
     // Adds a parsed (status 0) line; returns its index.
     uint32_t add_line(const ParsedLine& p, int nc, int nc_mode, int nec);
