@@ -28,9 +28,9 @@ NC = 8
 # Roofline.  Work unit: 16,388 SHA-1 compressions per PMK (north_star).  Bound: integer
 # VALU issue.  Measured on gfx950 (tools/valu_peak, profiles/r01/valu_issue_costs.json): xor/bitop3/add_u32 take
 # 2 SIMD cycles per wave64 instruction, alignbit (rotate) and add3 take 4, so the cheapest HMAC inner-loop
-# compression costs C_MIN = 1887 SIMD-cycles per wave (64 lanes).
+# compression costs C_MIN = 1878.5 SIMD-cycles per wave (64 lanes; derivation in DESIGN.md section 4).
 COMPRESSIONS_PER_PMK = 16388
-C_MIN_CYCLES = 1887
+C_MIN_CYCLES = 1878.5
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
 # HBM traffic of k_pbkdf2 per PMK, from the PMC passes of tools/profile_traffic.sh over this bench command
@@ -59,6 +59,9 @@ def parse():
                          "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
                          "dwpa_crack_files from a gz dictionary on disk (the help_crack client path)")
     ap.add_argument("--essids", type=int, default=1000, help="c3: number of ESSIDs (BASELINE: 1000)")
+    ap.add_argument("--short-words", action="store_true",
+                    help="c2files: lengths geometric(0.3)+6 so ~30 %% of the words are shorter than 8 and dropped "
+                         "by the m22000 filter (as in real wordlists); PMK/s counts only 8..63-byte words")
     return ap.parse_args()
 
 
@@ -418,7 +421,8 @@ def main_files(args, world, rank, local):
     n = args.dict_words
     plant = min(PLANT_INDEX, n - 1)
     rng = np.random.default_rng(2)
-    lens = np.clip(rng.geometric(0.3, n) + 7, 8, 63).astype(np.int64)
+    lens = np.clip(rng.geometric(0.3, n) + (6 if args.short_words else 7), 1, 63).astype(np.int64)
+    lens[plant] = max(int(lens[plant]), 8)
     ends = np.cumsum(lens + 1)
     text = rng.integers(0x21, 0x7F, int(ends[-1]), dtype=np.uint8)
     text[ends - 1] = 0x0A
@@ -453,7 +457,7 @@ def main_files(args, world, rank, local):
         recs = open(opath, "rb").read().strip().split(b"\n") if os.path.exists(opath) else []
         cracked &= rc == 0 and len(recs) == 1 and recs[0].endswith(b":" + psk)
     elapsed = sum(times) / len(times)
-    words = plant + 1
+    words = int(np.count_nonzero(lens[:plant + 1] >= 8))  # PMKs derived: words inside the 8..63 filter
     if world > 1:
         elapsed, total = reduce_timing(dist, elapsed, float(words))
     else:
@@ -464,7 +468,8 @@ def main_files(args, world, rank, local):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "C2 via dwpa_crack_files: 100M-word gzip dictionary on local disk (streamed, "
-                                   "inflated and uploaded per chunk), one EAPOL keyver-2 line, hashcat NC mode 8",
+                                   "inflated and uploaded per chunk), one EAPOL keyver-2 line, hashcat NC mode 8"
+                                   + (", ~30 % of the words shorter than 8" if args.short_words else ""),
                        "dict_words": n, "gz_bytes": gz_bytes, "gz_write_s": round(gz_s, 2),
                        "words_scanned_per_pass": words, "batch": args.batch,
                        "parallelism": f"replicas x{world}"},

@@ -227,17 +227,39 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
     const size_t words = e - b;
     const uint64_t nrules = rules ? rules->size() : 1;
     const uint64_t total = words * nrules;
-    // candidate id = word * nrules + rule; batches walk the candidate space in order
-    const uint32_t words_per_batch = rules ? std::max<uint32_t>(1, cap / (uint32_t)nrules) : cap;
-    for (size_t wb = 0; wb < words; wb += words_per_batch) {
-        const uint32_t nw = (uint32_t)std::min<size_t>(words_per_batch, words - wb);
+    // candidate id = word * nrules + rule; batches walk the candidate space in order.  Every PBKDF2 lane runs the
+    // same 4096 iterations, so a batch costs ceil(candidates / 256K) wave rounds whatever its fill: the words per
+    // batch follow the observed fraction of candidates that survive the 8..63 filter (and the rules), aiming at
+    // 99.5 % of the batch.  A load that overflows the batch (the compaction drops and counts the excess) is
+    // repeated with fewer words before anything is derived.
+    double keep = 1.0;  // surviving candidates per (word x rule)
+    for (size_t wb = 0; wb < words;) {
+        // keep == 1 (nothing filtered so far): exactly one batch of candidates, which cannot overflow
+        const double want = (keep >= 1.0 ? 1.0 : 0.995) * cap / ((double)nrules * keep);
+        const uint64_t most = 16ull * cap / nrules;  // kernel-side bound on a fill-mode load
+        const uint32_t nw = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)want, most, words - wb}));
         int r;
         if (rules)
-            r = rules_load(w.scan, drules, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, w.stream);
+            r = rules_load(w.scan, drules, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, w.stream, true);
         else
-            r = scan_load_dict(w.scan, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, 8, 63, w.stream);
+            r = scan_load_dict(w.scan, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, 8, 63, w.stream,
+                               true);
         if (r < 0) return r;
+        uint32_t raw = 0;
+        if ((r = scan_counter_raw(w.scan, w.stream, &raw)) < 0) return r;
+        const double seen = (double)raw / ((double)nw * nrules);
+        if (raw > cap) {  // overflow: nothing derived yet, retry these words in a smaller batch
+            if (nw == 1) return DWPA_E_OVERFLOW;
+            keep = std::max(seen, keep * 1.05);
+            continue;
+        }
+        if (raw > 0) keep = std::min(1.0, std::max(0.01, seen));
+        if (raw == 0) {
+            wb += nw;
+            continue;
+        }
         if ((r = scan_run(w.scan, w.stream)) < 0) return r;  // all ESSID groups, grouped per launch
+        wb += nw;
         std::vector<HitDev> hits;
         if ((r = scan_hits_raw(w.scan, hits, w.stream)) < 0) return r;
         if (hits.empty()) continue;

@@ -98,6 +98,14 @@ __device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// Ch(b, c, d) = (b & c) | (~b & d) in one full-rate op (bitop3 truth table 0xCA: src0 = 0xF0, src1 = 0xCC,
+// src2 = 0xAA).  Left to itself LLVM emits a bitop3 for (c ^ d) & b and folds the final xor into the next add as
+// v_xad_u32, one instruction fewer but a half-rate (4-cycle) op on gfx950: 2 extra SIMD-cycles per Ch round.
+__device__ __forceinline__ uint32_t ch3(uint32_t b, uint32_t c, uint32_t d) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(b), "v"(c), "v"(d));
+    return r;
+}
 // a ^ b ^ K with a wave-uniform constant K in an SGPR (VOP3 on gfx9 takes no literal operand).
 __device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
     uint32_t r;
@@ -148,7 +156,7 @@ __device__ __forceinline__ void spacer() {
 template <int T, int NOP = 0>
 __device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[16]) {
     uint32_t f;
-    if constexpr (T < 20) f = DWPA_SHA1_CH(b, c, d);
+    if constexpr (T < 20) f = ch3(b, c, d);
     else if constexpr (T < 40) f = xor3(b, c, d);
     else if constexpr (T < 60) f = maj3(b, c, d);
     else f = xor3(b, c, d);

@@ -765,13 +765,21 @@ void scan_destroy(dwpa_scan* sc) {
 }
 
 int scan_load_dict(dwpa_scan* sc, const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t count,
-                   uint32_t minlen, uint32_t maxlen, void* stream) {
-    if (!sc || count > sc->batch_cap) return DWPA_E_ARG;
+                   uint32_t minlen, uint32_t maxlen, void* stream, bool fill) {
+    if (!sc || count > (fill ? 16 * (uint64_t)sc->batch_cap : sc->batch_cap)) return DWPA_E_ARG;
     HIPCHK(hipSetDevice(sc->device));
     hipStream_t s = as_stream(stream);
     HIPCHK(hipMemsetAsync(sc->batch.counters.p, 0, 4, s));
     HIPCHK(launch_prep_dict(off, bytes, first, count, minlen, maxlen, (uint32_t*)sc->batch.mid.p,
                             (uint64_t*)sc->batch.ids.p, (uint32_t*)sc->batch.counters.p, sc->batch_cap, true, s));
+    return 0;
+}
+
+int scan_counter_raw(dwpa_scan* sc, void* stream, uint32_t* raw) {
+    HIPCHK(hipSetDevice(sc->device));
+    hipStream_t s = as_stream(stream);
+    HIPCHK(hipMemcpyAsync(raw, sc->batch.counters.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
 

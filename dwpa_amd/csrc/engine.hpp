@@ -34,8 +34,11 @@ uint32_t engine_batch();
 int scan_create(int device, const char* const* lines, const size_t* lens, size_t nlines, int nc, int nc_mode,
                 uint32_t batch, dwpa_scan** out);
 void scan_destroy(dwpa_scan* sc);
+// fill = true (crack_files): count may exceed the batch; candidates beyond it are dropped by the compaction and
+// counted, and scan_counter_raw tells the caller to retry with fewer words.
+int scan_counter_raw(dwpa_scan* sc, void* stream, uint32_t* raw);
 int scan_load_dict(dwpa_scan* sc, const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t count,
-                   uint32_t minlen, uint32_t maxlen, void* stream);
+                   uint32_t minlen, uint32_t maxlen, void* stream, bool fill = false);
 int scan_load_numeric(dwpa_scan* sc, uint64_t first, uint32_t count, uint32_t digits, void* stream);
 int scan_pbkdf2(dwpa_scan* sc, int group, void* stream);
 int scan_verify(dwpa_scan* sc, int group, void* stream);

@@ -166,8 +166,8 @@ int rules_upload(int device, const RuleSet& rs, DevRules* out) {
 }
 
 int rules_load(dwpa_scan* scan, const DevRules* r, const uint64_t* off, const uint8_t* bytes, uint64_t first,
-               uint32_t nwords, hipStream_t s) {
-    if (!scan || !r || (uint64_t)nwords * r->nrules > scan_batch_cap(scan)) return DWPA_E_ARG;
+               uint32_t nwords, hipStream_t s, bool fill) {
+    if (!scan || !r || (uint64_t)nwords * r->nrules > (fill ? 16ull : 1ull) * scan_batch_cap(scan)) return DWPA_E_ARG;
     Batch& b = scan_batch_ref(scan);
     if (hipSetDevice(r->device) != hipSuccess) return DWPA_E_HIP;
     if (hipMemsetAsync(b.counters.p, 0, 4, s) != hipSuccess) return DWPA_E_HIP;

@@ -47,7 +47,7 @@ void rules_release(DevRules* r);
 // Stage 1 for word x rule candidates: words [first, first+nwords) of an HBM dictionary, every rule; candidates
 // outside 8..63 bytes are dropped; candidate id = word * nrules + rule.
 int rules_load(dwpa_scan* scan, const DevRules* r, const uint64_t* off, const uint8_t* bytes, uint64_t first,
-               uint32_t nwords, hipStream_t s);
+               uint32_t nwords, hipStream_t s, bool fill = false);
 
 hipError_t launch_rules_expand(const uint64_t* off, const uint8_t* bytes, uint32_t nwords, const uint32_t* roffs,
                                const uint8_t* rcode, uint32_t nrules, uint8_t* out, uint32_t* out_len,
