@@ -16,6 +16,35 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t n) { return __buil
 __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// 3-input XOR in one VALU op: v_bitop3_b32 with truth table 0x96 (gfx950).  LLVM selects bitop3 for Ch/Maj but
+// splits XOR3 into two v_xor_b32, which costs ~100 extra ops per compression in the schedule and parity rounds.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// Majority in one op (bitop3 truth table 0xE8); left to itself LLVM emits v_xor + v_bfi for it.
+__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// Ch(b, c, d) = (b & c) | (~b & d) in one full-rate op (bitop3 truth table 0xCA: src0 = 0xF0, src1 = 0xCC,
+// src2 = 0xAA).  Left to itself LLVM emits a bitop3 for (c ^ d) & b and folds the final xor into the next add as
+// v_xad_u32, one instruction fewer but a half-rate (4-cycle) op on gfx950: 2 extra SIMD-cycles per Ch round.
+__device__ __forceinline__ uint32_t ch3(uint32_t b, uint32_t c, uint32_t d) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(b), "v"(c), "v"(d));
+    return r;
+}
+// a ^ b ^ K with a wave-uniform constant K in an SGPR (VOP3 on gfx9 takes no literal operand).
+__device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
+
 // ------------------------------------------------------------------------------------------------
 // SHA-1
 // ------------------------------------------------------------------------------------------------
@@ -27,6 +56,8 @@ constexpr uint32_t SHA1_K0 = 0x5a827999u, SHA1_K1 = 0x6ed9eba1u, SHA1_K2 = 0x8f1
 constexpr uint32_t SHA1_IV0 = 0x67452301u, SHA1_IV1 = 0xefcdab89u, SHA1_IV2 = 0x98badcfeu, SHA1_IV3 = 0x10325476u,
                    SHA1_IV4 = 0xc3d2e1f0u;
 
+// Generic round functions, left to the compiler: forcing the bitop3 forms here (as step84 does in the PBKDF2 loop)
+// raises the verify kernels' register pressure past 64 VGPRs for a ~0.2 % gain on C2.
 template <int T>
 __device__ __forceinline__ uint32_t sha1_f(uint32_t b, uint32_t c, uint32_t d) {
     if constexpr (T < 20) return DWPA_SHA1_CH(b, c, d);
@@ -83,34 +114,6 @@ __device__ __forceinline__ Sha1Mid sha1_mid(const uint32_t h[5]) {
     m.c0 = rotl(h[0], 5) + DWPA_SHA1_CH(h[1], h[2], h[3]) + h[4] + SHA1_K0;
     m.c1 = DWPA_SHA1_CH(h[0], m.r1, h[2]) + h[3] + SHA1_K0;
     return m;
-}
-
-// 3-input XOR in one VALU op: v_bitop3_b32 with truth table 0x96 (gfx950).  LLVM selects bitop3 for Ch/Maj but
-// splits XOR3 into two v_xor_b32, which costs ~100 extra ops per compression in the schedule and parity rounds.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// Majority in one op (bitop3 truth table 0xE8); left to itself LLVM emits v_xor + v_bfi for it.
-__device__ __forceinline__ uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// Ch(b, c, d) = (b & c) | (~b & d) in one full-rate op (bitop3 truth table 0xCA: src0 = 0xF0, src1 = 0xCC,
-// src2 = 0xAA).  Left to itself LLVM emits a bitop3 for (c ^ d) & b and folds the final xor into the next add as
-// v_xad_u32, one instruction fewer but a half-rate (4-cycle) op on gfx950: 2 extra SIMD-cycles per Ch round.
-__device__ __forceinline__ uint32_t ch3(uint32_t b, uint32_t c, uint32_t d) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(b), "v"(c), "v"(d));
-    return r;
-}
-// a ^ b ^ K with a wave-uniform constant K in an SGPR (VOP3 on gfx9 takes no literal operand).
-__device__ __forceinline__ uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
-    return r;
 }
 
 // Message words of the 84-byte HMAC inner/outer message: W0..W4 variable, W5 = 0x80000000, W6..W14 = 0, W15 = 672.
