@@ -1,8 +1,12 @@
 // pbkdf2_module.cpp -- loads the issue-pass PBKDF2 code object (embedded at build time) on each device and launches
-// it.  DWPA_PBKDF2_PLAIN=1 selects the hipcc-scheduled k_pbkdf2 instead (A/B reference; identical results).
+// it.  Launches with at most one wave per SIMD (small server checks: C1) take the hipcc-scheduled k_pbkdf2 instead:
+// the issue pass's s_nops only pay when several waves share a SIMD, and a lone wave runs its stream 1.55x slower
+// with them (profiles/r01/partial_round/).  DWPA_PBKDF2_PLAIN=1 forces the plain kernel everywhere and
+// DWPA_PBKDF2_ISSUE=1 the issue-pass kernel everywhere (A/B; identical results).
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 
@@ -15,16 +19,32 @@ extern const size_t pbkdf2_gfx950_hsaco_size;
 
 struct Fns {
     hipFunction_t one, ms, mg;  // k_pbkdf2_gfx950 (one ESSID), _ms (per-slot salt), _mg (ESSID groups x batch)
+    uint64_t level_lanes;       // lanes that give every SIMD of the device one wave: CUs x 4 SIMDs x 64
 };
 static std::mutex g_mod_mu;
 static std::map<int, Fns> g_fn;
 
+static bool env_flag(const char* name) {
+    const char* e = getenv(name);
+    return e && *e && *e != '0';
+}
 static bool use_plain() {
-    static const bool plain = [] {
-        const char* e = getenv("DWPA_PBKDF2_PLAIN");
-        return e && *e && *e != '0';
-    }();
+    static const bool plain = env_flag("DWPA_PBKDF2_PLAIN");
     return plain;
+}
+static bool force_issue() {
+    static const bool issue = env_flag("DWPA_PBKDF2_ISSUE");
+    return issue;
+}
+
+// Workgroup size of the issue-pass launches (DWPA_PBKDF2_WG = 64/128/256, default 256): partial-round experiments.
+static uint32_t wg_size() {
+    static const uint32_t wg = [] {
+        const char* e = getenv("DWPA_PBKDF2_WG");
+        const int v = e ? atoi(e) : 256;
+        return (uint32_t)((v == 64 || v == 128) ? v : 256);
+    }();
+    return wg;
 }
 
 static hipError_t tuned_functions(Fns* fn) {
@@ -42,9 +62,15 @@ static hipError_t tuned_functions(Fns* fn) {
     if ((e = hipModuleGetFunction(&fn->one, mod, "k_pbkdf2_gfx950")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->ms, mod, "k_pbkdf2_gfx950_ms")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->mg, mod, "k_pbkdf2_gfx950_mg")) != hipSuccess) return e;
+    int cus = 0;
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    fn->level_lanes = (uint64_t)(cus > 0 ? cus : 256) * 4 * 64;
     g_fn[dev] = *fn;
     return hipSuccess;
 }
+
+// At most one wave per SIMD (both output blocks counted): latency-bound, the plain schedule is faster.
+static bool lone_waves(const Fns& fn, uint64_t pmks) { return !force_issue() && 2 * pmks <= fn.level_lanes; }
 
 hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
                          const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s) {
@@ -53,9 +79,13 @@ hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint3
     Fns fn;
     hipError_t e = tuned_functions(&fn);
     if (e != hipSuccess) return e;
+    // with a device counter the host only knows the upper bound min(count, cap - base)
+    if (lone_waves(fn, std::min<uint64_t>(count, cap > base ? cap - base : 0)))
+        return launch_pbkdf2_plain(mid, cap, base, count, counter, salt, nsalt, pmk, s);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&base, (void*)&count, (void*)&counter,
                     (void*)&salt, (void*)&nsalt, (void*)&pmk};
-    return hipModuleLaunchKernel(fn.one, (count + 255) / 256, 2, 1, 256, 1, 1, 0, s, args, nullptr);
+    const uint32_t wg = wg_size();
+    return hipModuleLaunchKernel(fn.one, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args, nullptr);
 }
 
 hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
@@ -65,8 +95,10 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
     Fns fn;
     hipError_t e = tuned_functions(&fn);
     if (e != hipSuccess) return e;
+    if (lone_waves(fn, std::min(count, cap))) return launch_pbkdf2_ms_plain(mid, cap, count, pool, sref, pmk, s);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk};
-    return hipModuleLaunchKernel(fn.ms, (count + 255) / 256, 2, 1, 256, 1, 1, 0, s, args, nullptr);
+    const uint32_t wg = wg_size();
+    return hipModuleLaunchKernel(fn.ms, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args, nullptr);
 }
 
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
@@ -80,11 +112,17 @@ hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* c
     if (e != hipSuccess) return e;
     const uint64_t lanes = (uint64_t)ngroups * cap;
     if (lanes > 0xffffffffull - 255) return hipErrorInvalidValue;
+    if (lone_waves(fn, lanes)) return launch_pbkdf2_mg_plain(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride, s);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&counter, (void*)&ngroups, (void*)&salt, (void*)&gsalt,
                     (void*)&pmk, (void*)&pstride};
-    return hipModuleLaunchKernel(fn.mg, (uint32_t)((lanes + 255) / 256), 2, 1, 256, 1, 1, 0, s, args, nullptr);
+    const uint32_t wg = wg_size();
+    return hipModuleLaunchKernel(fn.mg, (uint32_t)((lanes + wg - 1) / wg), 2, 1, wg, 1, 1, 0, s, args, nullptr);
 }
 
-const char* pbkdf2_variant() { return use_plain() ? "k_pbkdf2 (hipcc schedule)" : "k_pbkdf2_gfx950 (issue pass)"; }
+const char* pbkdf2_variant() {
+    return use_plain() ? "k_pbkdf2 (hipcc schedule)"
+                       : force_issue() ? "k_pbkdf2_gfx950 (issue pass)"
+                                       : "k_pbkdf2_gfx950 (issue pass; hipcc schedule at <= 1 wave per SIMD)";
+}
 
 }  // namespace dwpa

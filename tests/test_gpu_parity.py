@@ -389,3 +389,21 @@ def test_crack_files_several_dictionaries(tmp_path):
     assert dwpa_amd.crack_files(str(hf), files, None, 8, str(out), batch=1 << 14) == 0
     recs = out.read_bytes().strip().split(b"\n")
     assert sorted(r.rsplit(b":", 1)[1] for r in recs) == sorted(psks)
+
+
+@pytest.mark.skipif(os.environ.get("DWPA_PBKDF2_ISSUE") == "1", reason="already the forced issue-pass run")
+def test_issue_pass_kernels_at_small_sizes():
+    """Launches of at most one wave per SIMD take the plain-schedule PBKDF2 kernel (pbkdf2_module.cpp), so the
+    small parity cases above run it.  Re-run the PBKDF2-bearing ones with the issue-pass kernels forced
+    (DWPA_PBKDF2_ISSUE=1), in a child process because the switch is read once per process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sel = ("pbkdf2_vectors or pbkdf2_random_lengths or challenge_kat or mixed_golden_batch or random_batch_vs_oracle"
+           " or scan_dictionary_hbm or scan_numeric_keyspace or scan_run_many_essids")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_gpu_parity.py"), "-k", sel],
+                       cwd=root, env=dict(os.environ, DWPA_PBKDF2_ISSUE="1"), capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout
