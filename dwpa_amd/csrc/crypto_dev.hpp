@@ -56,14 +56,31 @@ constexpr uint32_t SHA1_K0 = 0x5a827999u, SHA1_K1 = 0x6ed9eba1u, SHA1_K2 = 0x8f1
 constexpr uint32_t SHA1_IV0 = 0x67452301u, SHA1_IV1 = 0xefcdab89u, SHA1_IV2 = 0x98badcfeu, SHA1_IV3 = 0x10325476u,
                    SHA1_IV4 = 0xc3d2e1f0u;
 
-// Generic round functions, left to the compiler: forcing the bitop3 forms here (as step84 does in the PBKDF2 loop)
-// raises the verify kernels' register pressure past 64 VGPRs for a ~0.2 % gain on C2.
+// Generic round functions and schedule (verify kernels).  DWPA_SHA1_GENERIC_BITOP selects how many of them are
+// forced into one v_bitop3_b32: 0 none (LLVM splits XOR3 into two v_xor and emits Ch/Maj as bitop3 + v_xad),
+// 1 the schedule's XOR3, 2 also the parity rounds, 3 also Ch and Maj.  3 keeps every verify class inside its VGPR
+// budget and took k_verify<kv2> from 13.2 to 11.2 ms per C2 step, k_verify_att<kv2> from 3.66 to 3.11 ms per C5
+// call (profiles/r01/generic_sha1_ab.json).
+#ifndef DWPA_SHA1_GENERIC_BITOP
+#define DWPA_SHA1_GENERIC_BITOP 3
+#endif
 template <int T>
 __device__ __forceinline__ uint32_t sha1_f(uint32_t b, uint32_t c, uint32_t d) {
-    if constexpr (T < 20) return DWPA_SHA1_CH(b, c, d);
-    else if constexpr (T < 40) return DWPA_SHA1_PAR(b, c, d);
-    else if constexpr (T < 60) return DWPA_SHA1_MAJ(b, c, d);
-    else return DWPA_SHA1_PAR(b, c, d);
+    if constexpr (T < 20) {
+        if constexpr (DWPA_SHA1_GENERIC_BITOP >= 3) return ch3(b, c, d);
+        else return DWPA_SHA1_CH(b, c, d);
+    } else if constexpr (T < 40 || T >= 60) {
+        if constexpr (DWPA_SHA1_GENERIC_BITOP >= 2) return xor3(b, c, d);
+        else return DWPA_SHA1_PAR(b, c, d);
+    } else {
+        if constexpr (DWPA_SHA1_GENERIC_BITOP >= 3) return maj3(b, c, d);
+        else return DWPA_SHA1_MAJ(b, c, d);
+    }
+}
+// W[t] of the generic schedule: xor of four words (one bitop3 + one xor when DWPA_SHA1_GENERIC_BITOP >= 1)
+__device__ __forceinline__ uint32_t sha1_w4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    if constexpr (DWPA_SHA1_GENERIC_BITOP >= 1) return xor3(a, b, c) ^ d;
+    else return a ^ b ^ c ^ d;
 }
 template <int T>
 __device__ __forceinline__ constexpr uint32_t sha1_k() {
@@ -81,7 +98,7 @@ __device__ __forceinline__ void sha1_compress(uint32_t st[5], const uint32_t m[1
         uint32_t wt;                                                                                        \
         if constexpr ((T) < 16) wt = w[(T)];                                                                \
         else {                                                                                              \
-            wt = rotl(w[((T) - 3) & 15] ^ w[((T) - 8) & 15] ^ w[((T) - 14) & 15] ^ w[(T) & 15], 1);          \
+            wt = rotl(sha1_w4(w[((T) - 3) & 15], w[((T) - 8) & 15], w[((T) - 14) & 15], w[(T) & 15]), 1);   \
             w[(T) & 15] = wt;                                                                               \
         }                                                                                                   \
         uint32_t t = rotl(a, 5) + sha1_f<(T)>(b, c, d) + e + sha1_k<(T)>() + wt;                            \

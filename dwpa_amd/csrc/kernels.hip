@@ -177,6 +177,30 @@ __device__ __forceinline__ void att_block(const uint32_t* __restrict__ w, uint32
     }
 }
 
+// The attempt's PRF blocks after the shared prefix, fed to `compress`.  Patched lines take the stream from the line
+// (LineDev.att_off/att_nblk, wave-uniform): in k_verify_att the lanes hold different attempts, and the per-attempt
+// copy of the same offset would turn every message word into a per-lane vector load.  Explicit per-attempt
+// streams (short ANONCE) are per lane.
+template <typename F>
+__device__ __forceinline__ void prf_blocks(const LineDev& L, const uint32_t* __restrict__ pool, const AttDev& at,
+                                           F&& compress) {
+    uint32_t m[16];
+    if (L.patch_w0 != NO_PATCH) {
+        const uint32_t* aw = pool + L.att_off;
+        for (uint32_t b = 0; b < L.att_nblk; b++) {
+            att_block(aw, b, L.patch_w0, L.patch_w1, at.v0, at.v1, m);
+            compress(m);
+        }
+    } else {
+        const uint32_t* aw = pool + at.blk_off;
+        for (uint32_t b = 0; b < at.nblk; b++) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) m[j] = aw[b * 16 + j];
+            compress(m);
+        }
+    }
+}
+
 // Everything of an EAPOL check that depends on the PMK but not on the nonce-correction attempt.
 struct EapolKey {
     uint32_t op1[5], pre1[5];  // keyver 1/2: HMAC-SHA1(PMK) opad midstate, inner state after the shared PRF prefix
@@ -213,16 +237,11 @@ template <uint32_t VC>
 __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __restrict__ pool, const EapolKey& K,
                                           const AttDev& at, const uint32_t* te, uint32_t mic[4]) {
     constexpr bool has1 = (VC & VC_KV1) != 0, has2 = (VC & VC_KV2) != 0, has3 = (VC & VC_KV3) != 0;
-    const uint32_t* aw = pool + at.blk_off;
     if ((has1 || has2) && (!has3 || L.keyver != 3)) {
         uint32_t st[5], ptk[5];
 #pragma unroll
         for (int k = 0; k < 5; k++) st[k] = K.pre1[k];
-        for (uint32_t b = 0; b < at.nblk; b++) {
-            uint32_t m[16];
-            att_block(aw, b, L.patch_w0, L.patch_w1, at.v0, at.v1, m);
-            sha1_compress(st, m);
-        }
+        prf_blocks(L, pool, at, [&](const uint32_t m[16]) { sha1_compress(st, m); });
         sha1_outer20(K.op1, st, ptk);  // PTK[0..19]; KCK = PTK[0..15]
         if (has2 && (!has1 || L.keyver == 2)) {
             // HMAC-SHA1(KCK, EAPOL): the opad midstate is computed after the inner hash so that the two key-pad
@@ -254,11 +273,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         uint32_t st[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) st[k] = K.pre2[k];
-        for (uint32_t b = 0; b < at.nblk; b++) {
-            uint32_t m[16];
-            att_block(aw, b, L.patch_w0, L.patch_w1, at.v0, at.v1, m);
-            sha256_compress(st, m);
-        }
+        prf_blocks(L, pool, at, [&](const uint32_t m[16]) { sha256_compress(st, m); });
         uint32_t m[16] = {st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7],
                           0x80000000u, 0, 0, 0, 0, 0, 0, 768u};
         uint32_t ptk[8];

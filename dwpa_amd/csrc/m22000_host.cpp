@@ -340,6 +340,8 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
         pool.insert(pool.end(), w.begin() + 16 * prefix, w.end());
         L.patch_w0 = W0 - 16 * prefix;
         L.patch_w1 = W1 - 16 * prefix;
+        L.att_off = blk_off;
+        L.att_nblk = (uint32_t)(w.size() / 16 - prefix);
         L.list_off = (uint32_t)atts.size();
         L.nlists = 1;
         for (size_t a = 0; a < order.size(); a++) {

@@ -33,7 +33,8 @@ struct LineDev {
     // substr_replace grows $n).
     uint32_t patch_w0;
     uint32_t patch_w1;
-    uint32_t pad0, pad1;
+    uint32_t att_off;     // patched lines: the shared stream (word offset, blocks) every AttDev.blk_off/nblk repeats,
+    uint32_t att_nblk;    // read from the line so that the attempt-parallel kernel keeps it wave-uniform
 };
 static_assert(sizeof(LineDev) % 16 == 0, "LineDev must stay 16-byte aligned");
 constexpr uint32_t NO_PATCH = 0xffffffffu;
