@@ -111,10 +111,12 @@ struct Device {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;   // check path: table uploads while PBKDF2 runs on `stream`
     hipEvent_t side_done = nullptr;
+    hipStream_t tail = nullptr;   // check path: the PBKDF2 remainder (< one wave per SIMD) + its verify
+    hipEvent_t head_done = nullptr, tail_done = nullptr;
     PinnedArena stage;            // check path: host staging of the derive uploads
     std::mutex mu;
     Batch batch;
-    DevBuf lines, atts, pool, segs, salt, koff, kbytes, idsup;
+    DevBuf lines, atts, pool, segs, segs_tail, salt, koff, kbytes, idsup;
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
 };
 
@@ -165,6 +167,9 @@ static int device_stream(Device& d) {
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&d.side_done, hipEventDisableTiming));
+        HIPCHK(hipStreamCreateWithFlags(&d.tail, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&d.head_done, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.tail_done, hipEventDisableTiming));
     }
     return 0;
 }
@@ -272,7 +277,28 @@ struct DeriveStage {
     Span<uint64_t> off, ids;
     Span<uint8_t> bytes;
     Span<uint32_t> src, sref, spool, cpmk;
+    uint32_t split = 0;  // slots [0, split) read d.stream's PMKs; [split, n) d.tail's (== n: no tail)
 };
+
+// DWPA_CHECK_SPLIT=0 keeps every derive in one PBKDF2 launch (A/B of the head/tail split below).
+static bool check_split_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("DWPA_CHECK_SPLIT");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
+// Head/tail split of one derive.  PBKDF2 is issue-bound, so a launch takes as long as its fullest SIMD: nu unique
+// PMKs at k.f waves per SIMD cost k + 1 whole wave times (~7 ms each at C5 size), the last one with 1 - f of the
+// chip idle.  The head (k whole waves per SIMD) runs alone; the tail (< one wave per SIMD, the latency-bound plain
+// kernel) starts when the head ends and overlaps the head's verify on d.tail.  Below 4 waves per SIMD the lone
+// tail's ~8 ms chain costs more than the wave time it saves, so small derives stay in one launch.
+static uint32_t head_pmks(uint32_t nu) {
+    const uint32_t unit = pbkdf2_wave_unit();
+    if (!check_split_enabled() || !unit || nu < 4 * unit) return nu;
+    return nu / unit * unit;
+}
 
 // Derive the PMKs of slots [b, e) into batch.pmk (slot order) and their key ordinals into batch.ids.  Unique
 // (ESSID, key) pairs are derived once, all ESSIDs in one PBKDF2 launch (server batches fan one key out to every
@@ -405,6 +431,16 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     for (uint32_t i = 0; i < n; i++) st.ids[i] = slots[b + i].ordinal;
 
     RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
+    // head = unique PMKs [0, nh); unique ids are numbered in first-occurrence slot order, so slots [0, split) only
+    // read head PMKs (or caller PMKs) and the slots after it wait for the tail
+    const uint32_t nh = head_pmks(nu);
+    st.split = n;
+    if (nh < nu)
+        for (uint32_t i = 0; i < n; i++)
+            if (!(st.src[i] & GATHER_CALLER) && st.src[i] >= nh) {
+                st.split = i;
+                break;
+            }
     if (nu) {
         RCHK(upload_span(d.koff, st.off, s));
         RCHK(upload_span(d.kbytes, st.bytes, s));
@@ -414,28 +450,49 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     RCHK(upload_span(d.cpmk, st.cpmk, s));
     RCHK(upload_span(d.src, st.src, s));
     HIPCHK(hipMemcpyAsync(d.batch.ids.p, st.ids.data(), n * 8, hipMemcpyHostToDevice, s));
+    // hit counter reset ahead of every kernel of this derive (the tail's verify may run before the head's)
+    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
     tr.mark("  stage+upload");
+    const uint32_t cap = d.batch.cap;
+    const uint32_t* mid = (const uint32_t*)d.batch.mid.p;
+    const uint32_t* sref = (const uint32_t*)d.sref.p;
+    uint32_t* upmk = (uint32_t*)d.upmk.p;
     if (nu) {
         HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, nu, 0, 0xffffffffu,
-                                (uint32_t*)d.batch.mid.p, nullptr, nullptr, d.batch.cap, false, s));
-        HIPCHK(launch_pbkdf2_ms((const uint32_t*)d.batch.mid.p, d.batch.cap, nu, (const uint32_t*)d.salt.p,
-                                (const uint32_t*)d.sref.p, (uint32_t*)d.upmk.p, s));
+                                (uint32_t*)d.batch.mid.p, nullptr, nullptr, cap, false, s));
+        HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
     }
-    HIPCHK(launch_gather_pmk((const uint32_t*)d.upmk.p, d.batch.cap, (const uint32_t*)d.cpmk.p,
-                             (const uint32_t*)d.src.p, n, (uint32_t*)d.batch.pmk.p, d.batch.cap, s));
+    // SoA rows keep their stride (cap), so a sub-range is the same launch on offset base pointers
+    const uint32_t sp = st.split;
+    if (sp)
+        HIPCHK(launch_gather_pmk(upmk, cap, (const uint32_t*)d.cpmk.p, (const uint32_t*)d.src.p, sp,
+                                 (uint32_t*)d.batch.pmk.p, cap, s));
+    if (sp < n) {
+        HIPCHK(hipEventRecord(d.head_done, s));
+        HIPCHK(hipStreamWaitEvent(d.tail, d.head_done, 0));
+        HIPCHK(launch_pbkdf2_ms(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh, d.tail));
+        HIPCHK(launch_gather_pmk(upmk, cap, (const uint32_t*)d.cpmk.p, (const uint32_t*)d.src.p + sp, n - sp,
+                                 (uint32_t*)d.batch.pmk.p + sp, cap, d.tail));
+    }
     return 0;
 }
 
-// Verify the derived slots [b, e) against their jobs' lines and append the hits.  The line tables go up on the
-// side stream (while PBKDF2 may still run) and d.stream waits for them.  EAPOL lines with wide nonce windows use
-// the attempt-parallel kernel (a wave per key, lanes = attempts), the rest the key-parallel one; segments are
-// runs of <= 64 consecutive slots of one job.
-static int verify_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
+// d.stream waits for everything queued on d.tail so far.
+static int join_tail(Device& d) {
+    HIPCHK(hipEventRecord(d.tail_done, d.tail));
+    HIPCHK(hipStreamWaitEvent(d.stream, d.tail_done, 0));
+    return 0;
+}
+
+// Queue the verification of derived slots [b, e) (batch rows from b - base) against their jobs' lines on stream
+// s.  The line tables go up on the side stream (while PBKDF2 may still run) and s waits for them.  EAPOL lines with
+// wide nonce windows use the attempt-parallel kernel (a wave per key, lanes = attempts), the rest the key-parallel
+// one; segments are runs of <= 64 consecutive slots of one job.  Hits are appended on the device (collect_hits).
+static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, size_t b, size_t e,
                         const std::vector<uint32_t>& job_line, const TableBuilder& tb, bool upload_tables,
-                        std::vector<HitDev>& hits_out) {
-    PhaseTrace tr;
-    hipStream_t s = d.stream;
-    const uint32_t n = (uint32_t)(e - b);
+                        hipStream_t s, DevBuf& segbuf) {
+    const uint32_t n = (uint32_t)(e - b), row0 = (uint32_t)(b - base);
+    if (!n && !upload_tables) return 0;
     // bucket = mode * 4 + class index; mode 1 = attempt-parallel (EAPOL lines with >= ATT_PARALLEL_MIN attempts)
     std::vector<SegDev> bucket[8];
     for (uint32_t i = 0; i < n;) {
@@ -445,7 +502,8 @@ static int verify_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
         const uint32_t li = job_line[job];
         const LineDev& L = tb.lines[li];
         const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
-        if (!tb.never[li]) bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, i, j - i, 0});
+        if (!tb.never[li])
+            bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, row0 + i, j - i, 0});
         i = j;
     }
     std::vector<SegDev> segs;
@@ -460,14 +518,13 @@ static int verify_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
         RCHK(upload(d.atts, tb.atts, d.side));
         RCHK(upload(d.pool, tb.pool, d.side));
     }
-    RCHK(upload(d.segs, segs, d.side));
+    RCHK(upload(segbuf, segs, d.side));
     HIPCHK(hipEventRecord(d.side_done, d.side));
     HIPCHK(hipStreamWaitEvent(s, d.side_done, 0));
-    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
     uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
     for (int k = 0; k < 8; k++) {
         const uint32_t nb = (uint32_t)(bstart[k + 1] - bstart[k]), vc = 1u << (k & 3);
-        const SegDev* sg = (const SegDev*)d.segs.p + bstart[k];
+        const SegDev* sg = (const SegDev*)segbuf.p + bstart[k];
         if (!nb) continue;
         if (k < 4)
             HIPCHK(launch_verify((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, nullptr,
@@ -479,7 +536,15 @@ static int verify_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
                                      (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc,
                                      s));
     }
-    tr.mark("  verify queued");
+    return 0;
+}
+
+// Wait for the derive + verify kernels of one chunk (both streams) and append their hits.
+static int collect_hits(Device& d, std::vector<HitDev>& hits_out) {
+    PhaseTrace tr;
+    hipStream_t s = d.stream;
+    RCHK(join_tail(d));
+    uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
     uint32_t nh = 0;
     HIPCHK(hipMemcpyAsync(&nh, hitcnt, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -588,7 +653,10 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
                 for (uint32_t j : js) job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
             tr.mark("tables (overlapped)");
         }
-        RCHK(verify_slots(d, slots, b, e, job_line, tb, b == 0, hits));
+        RCHK(queue_verify(d, slots, b, b, b + st.split, job_line, tb, b == 0, d.stream, d.segs));
+        RCHK(queue_verify(d, slots, b, b + st.split, e, job_line, tb, false, d.tail, d.segs_tail));
+        tr.mark("  verify queued");
+        RCHK(collect_hits(d, hits));
     }
     tr.mark("device");
 
@@ -647,6 +715,7 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
         const size_t e = std::min(nkeys, b + chunk);
         DeriveStage st;
         RCHK(derive_slots(d, slots, b, e, jp, st));
+        RCHK(join_tail(d));
         std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
         HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, d.stream));
         HIPCHK(hipStreamSynchronize(d.stream));
@@ -1004,7 +1073,7 @@ void dwpa_shutdown(void) {
         std::lock_guard<std::mutex> dl(d->mu);
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
-        for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->salt, &d->koff, &d->kbytes, &d->idsup,
+        for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->salt, &d->koff, &d->kbytes, &d->idsup,
                           &d->upmk, &d->sref, &d->src, &d->cpmk,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();
@@ -1013,8 +1082,11 @@ void dwpa_shutdown(void) {
         if (d->stream) (void)hipStreamDestroy(d->stream);
         if (d->side) (void)hipStreamDestroy(d->side);
         if (d->side_done) (void)hipEventDestroy(d->side_done);
-        d->stream = d->side = nullptr;
-        d->side_done = nullptr;
+        if (d->tail) (void)hipStreamDestroy(d->tail);
+        if (d->head_done) (void)hipEventDestroy(d->head_done);
+        if (d->tail_done) (void)hipEventDestroy(d->tail_done);
+        d->stream = d->side = d->tail = nullptr;
+        d->side_done = d->head_done = d->tail_done = nullptr;
     }
     g_dev.clear();
     g_init = false;

@@ -19,6 +19,8 @@ hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base,
                                const uint32_t* counter, const uint32_t* salt, uint32_t nsalt, uint32_t* pmk,
                                hipStream_t s);
 const char* pbkdf2_variant();
+// PMKs that give every SIMD of the current device one PBKDF2 wave (two output-block lanes per PMK); 0 on error
+uint32_t pbkdf2_wave_unit();
 // many ESSIDs per launch: slot s uses the salt entry pool + sref[s] = {nsalt, [2][nsalt][16] words}
 hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                             const uint32_t* sref, uint32_t* pmk, hipStream_t s);

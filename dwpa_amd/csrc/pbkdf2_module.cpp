@@ -119,6 +119,12 @@ hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* c
     return hipModuleLaunchKernel(fn.mg, (uint32_t)((lanes + wg - 1) / wg), 2, 1, wg, 1, 1, 0, s, args, nullptr);
 }
 
+uint32_t pbkdf2_wave_unit() {
+    Fns fn;
+    if (tuned_functions(&fn) != hipSuccess) return 0;
+    return (uint32_t)(fn.level_lanes / 2);
+}
+
 const char* pbkdf2_variant() {
     return use_plain() ? "k_pbkdf2 (hipcc schedule)"
                        : force_issue() ? "k_pbkdf2_gfx950 (issue pass)"

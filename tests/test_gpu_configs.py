@@ -70,6 +70,39 @@ def test_c5_mixed_batch_full_size():
     assert not bad, [(i, jobs[i][0][:40], got[i]) for i in bad[:3]]
 
 
+def test_batch_head_tail_split():
+    """A derive of >= 4 waves per SIMD of unique (ESSID, key) pairs is split: the head (whole waves per SIMD) and
+    the tail (the remainder, on the second stream, overlapping the head's verify).  Hits are planted in head slots,
+    in tail slots that derive a tail PMK, and in tail slots that re-use a head PMK (same ESSID, later job), and
+    re-derived by the oracle from the winning key alone; the random keys around them never match."""
+    import random
+    rng = random.Random(91)
+    n_per = 36000  # 4 ESSIDs x 36,000 unique keys = 144,000 > 4 x 32,768 (MI355X: 256 CUs x 4 SIMDs x 64 / 2)
+    nets = [S.random_net(rng, essid_len=9 + e) for e in range(4)]
+    keyset = [[b"k%d-%06d-" % (e, i) + S.fast_psk(rng, 8, 20) for i in range(n_per)] for e in range(4)]
+    jobs, want = [], []
+    for e, (essid, ap, sta, an, sn) in enumerate(nets):
+        keys = list(keyset[e])
+        hit = [100, 20000, 1000, 30000][e]  # ESSID 3: the key sits past the head boundary (tail PMK)
+        line = (S.pmkid_line(keys[hit], essid, ap, sta) if e % 2 else
+                S.eapol_line(keys[hit], essid, ap, sta, an, sn, 2, -2 if e else 5, "LE", rng=rng))
+        jobs.append((line, keys, False, 8))
+        want.append(hit)
+    essid, ap, sta, an, sn = nets[3]
+    late = keyset[3]
+    # later jobs of ESSID 3 (all their slots are tail slots): a key derived by the head, one derived by the tail
+    for src in (5, 35000):
+        keys = [b"miss-%05d-" % i + S.fast_psk(rng, 8, 12) for i in range(300)]
+        keys[150] = late[src]
+        jobs.append((S.eapol_line(late[src], essid, ap, sta, an, sn, 2, 3, "BE", rng=rng), keys, False, 8))
+        want.append(150)
+    got = dwpa_amd.check_batch(jobs)
+    for job, g, w in zip(jobs, got, want):
+        line, keys, _, nc = job
+        assert g and g[0] == keys[w], (line[:30], g)
+        assert O.c_check_key_m22000(line, [keys[w]], False, nc) == g
+
+
 def test_batch_fanout_dedup_and_mixed_salt_lengths():
     """put_work shape (common.php:879-902): one submitted key checked against every net of an ESSID, plus PMK
     re-use jobs (:919) -- the engine derives each (ESSID, key) once.  ESSIDs of 1..60 bytes put 1- and 2-block
