@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--dict-words", type=int, default=DICT_WORDS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="batches in flight (c2/c3/c4), each on its own scan working set and HIP stream.  Measured "
+                         "A/B (profiles/r01/pipeline/): 2 gains 0.2 %% -- the next batch's PBKDF2 waves hold the "
+                         "SIMDs, so the verify runs starved beside it -- and blurs the per-kernel events; default 1")
     ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files"], default="c2",
                     help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs; "
                          "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
@@ -96,17 +100,17 @@ def build_c2(args, local, S, Scan, Dictionary):
     w.dict = Dictionary(w.off, w.data, device=local)
     w.B = (args.batch + 63) & ~63
     w.nbatches = (n + w.B - 1) // w.B
-    w.scan = Scan([w.line], device=local, nc=NC, nc_mode=0, batch=w.B)
+    w.scans = [Scan([w.line], device=local, nc=NC, nc_mode=0, batch=w.B) for _ in range(args.pipeline)]
     w.groups = 1
     w.name = "C2"
     w.description = ("C2: one ESSID, one EAPOL keyver-2 line (mp 0x80, planted NC +3 LE), 100M-word synthetic "
                      "dictionary resident in HBM, PHP nonce window nc=8 (21 attempts)")
     w.extra = {"dict_words": n}
 
-    def load(i, hs):
+    def load(i, hs, sc):
         first = (i % w.nbatches) * w.B
         cnt = min(w.B, n - first)
-        w.scan.load_dict(w.dict.off.ptr, w.dict.data.ptr, first, cnt, 8, 63, hs)
+        sc.load_dict(w.dict.off.ptr, w.dict.data.ptr, first, cnt, 8, 63, hs)
         return cnt
 
     def check(hits):
@@ -127,16 +131,16 @@ def build_c4(args, local, S, Scan, Dictionary):
     w.line = S.pmkid_line(b"%08d" % w.plant, w.essid, ap, sta)
     w.B = (args.batch + 63) & ~63
     w.nbatches = (n + w.B - 1) // w.B
-    w.scan = Scan([w.line], device=local, nc=NC, nc_mode=0, batch=w.B)
+    w.scans = [Scan([w.line], device=local, nc=NC, nc_mode=0, batch=w.B) for _ in range(args.pipeline)]
     w.groups = 1
     w.name = "C4"
     w.description = "C4: 8-digit numeric keyspace (10^8) generated on the GPU, one ESSID, PMKID line"
     w.extra = {"keyspace": n}
 
-    def load(i, hs):
+    def load(i, hs, sc):
         first = (i % w.nbatches) * w.B
         cnt = min(w.B, n - first)
-        w.scan.load_numeric(first, cnt, 8, hs)
+        sc.load_numeric(first, cnt, 8, hs)
         return cnt
 
     def check(hits):
@@ -178,21 +182,21 @@ def build_c3(args, local, S, Scan, Dictionary):
     # multi-group PBKDF2 launches (dwpa_scan_run).  Rule filtering makes the per-step count data-dependent, so the
     # last wave round of each launch is partial; 4x the C2 step keeps that tail near 2 %.
     w.B = max(len(rules) + 63, 4 * args.batch // max(1, args.essids)) // 64 * 64
-    w.scan = Scan(lines, device=local, nc=NC, nc_mode=0, batch=w.B)
-    w.nrules = w.scan.set_rules("\n".join(rules))
+    w.scans = [Scan(lines, device=local, nc=NC, nc_mode=0, batch=w.B) for _ in range(args.pipeline)]
+    w.nrules = [sc.set_rules("\n".join(rules)) for sc in w.scans][0]
     w.words_per_step = max(1, w.B // w.nrules)
     w.nbatches = (len(base) + w.words_per_step - 1) // w.words_per_step
-    w.groups = w.scan.groups
+    w.groups = w.scans[0].groups
     w.name = "C3"
     w.description = (f"C3: 10k-word dictionary x {w.nrules} WPA rules amplified on the GPU (8..63 filter), "
                      f"{w.groups} ESSIDs x 1-4 lines, one PMK per ESSID x candidate")
     w.extra = {"essids": w.groups, "lines": len(lines), "rules": w.nrules}
 
-    def load(i, hs):
+    def load(i, hs, sc):
         first = (i % w.nbatches) * w.words_per_step
         nw = min(w.words_per_step, len(base) - first)
-        w.scan.load_rules(w.dict.off.ptr, w.dict.data.ptr, first, nw, hs)
-        return w.scan.loaded(hs) * w.groups
+        sc.load_rules(w.dict.off.ptr, w.dict.data.ptr, first, nw, hs)
+        return sc.loaded(hs) * w.groups
 
     def check(hits):
         return all(any(h["line"] == li and h["pmk"] == S.pmk(psk, essid) for h in hits)
@@ -227,12 +231,19 @@ def main():
 
     build = {"c2": build_c2, "c3": build_c3, "c4": build_c4}[args.workload]
     w = build(args, local, S, dwpa_amd.Scan, Dictionary)
-    stream = Stream(local)
-    hs = stream.handle
-    sc = w.scan
+    # pipeline slot k: its own scan working set (batch buffers, hit buffer) and stream; batch s goes to slot
+    # s % P, so batch s+1's PBKDF2 is queued while batch s's verify still runs
+    P = len(w.scans)
+    streams = [Stream(local) for _ in range(P)]
 
-    def step(i, ev=None):
-        cnt = w.load(i, hs)
+    def sync_all():
+        for st in streams:
+            st.synchronize()
+
+    def step(i, k, ev=None):
+        sc, stream = w.scans[k], streams[k]
+        hs = stream.handle
+        cnt = w.load(i, hs, sc)
         if w.groups > 1:
             # all ESSID groups per launch; the events bracket PBKDF2 + verify (conservative for the roofline)
             if ev is not None:
@@ -241,31 +252,31 @@ def main():
             if ev is not None:
                 ev[1].record(stream)
             return cnt
-        for g in range(w.groups):
-            if ev is not None and g == 0:
-                ev[0].record(stream)
-            sc.pbkdf2(g, hs)
-            if ev is not None and g == 0:
-                ev[1].record(stream)
-            sc.verify(g, hs)
+        if ev is not None:
+            ev[0].record(stream)
+        sc.pbkdf2(0, hs)
+        if ev is not None:
+            ev[1].record(stream)
+        sc.verify(0, hs)
         return cnt
 
-    for b in batch_ids(rank, world, 0, args.warmup, w.nbatches):
-        step(b)
-    stream.synchronize()
-    sc.hits(hs)  # drop warmup hits
+    for s, b in enumerate(batch_ids(rank, world, 0, args.warmup, w.nbatches)):
+        step(b, s % P)
+    sync_all()
+    for k in range(P):
+        w.scans[k].hits(streams[k].handle)  # drop warmup hits
 
     kev = [(Event(local), Event(local)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
-    stream.synchronize()
+    sync_all()
     t0 = time.perf_counter()
     done = 0
     counts = []
     for s, b in enumerate(batch_ids(rank, world, args.warmup, args.steps, w.nbatches)):
-        counts.append(step(b, kev[s]))
+        counts.append(step(b, s % P, kev[s]))
         done += counts[-1]
-    stream.synchronize()
+    sync_all()
     elapsed_local = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
@@ -279,8 +290,10 @@ def main():
         total = float(done)
 
     # correctness: the batch holding the planted PSK(s) must report them (untimed)
-    step(w.plant_batch)
-    verified = bool(w.check(sc.hits(hs)))
+    for k in range(P):
+        w.scans[k].hits(streams[k].handle)
+    step(w.plant_batch, 0)
+    verified = bool(w.check(w.scans[0].hits(streams[0].handle)))
 
     per_launch = list(counts) if w.groups > 1 else [c / w.groups for c in counts]
     pmk_per_launch = sum(per_launch) / len(per_launch)
@@ -330,9 +343,11 @@ def main():
             "pbkdf2_kernel": "k_pbkdf2 (hipcc schedule)" if os.environ.get("DWPA_PBKDF2_PLAIN", "0") not in ("", "0")
                              else "k_pbkdf2_gfx950 (gfx950 VALU issue pass)",
             "rank0_local_s": round(elapsed_local, 4),
+            "pipeline": P,
         }
         print(json.dumps(result), flush=True)
-    sc.close()
+    for sc in w.scans:
+        sc.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
