@@ -106,6 +106,15 @@ struct PinnedArena {
 // ---------------------------------------------------------------------------------------------------------
 // global state
 // ---------------------------------------------------------------------------------------------------------
+// One candidate key of one job in the check path (explicit keys -> slots).
+struct Slot {
+    std::string_view key;     // bytes hashed (after hc_unhex): the caller's buffer or a decoded copy
+    uint32_t job;
+    uint32_t ordinal;         // index among the job's non-null keys
+    const std::string* essid;
+    bool pbkdf2;              // false: PMK supplied by the caller
+};
+
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
@@ -118,6 +127,7 @@ struct Device {
     Batch batch;
     DevBuf lines, atts, pool, segs, segs_tail, salt, koff, kbytes, idsup;
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
+    std::vector<Slot> slots;       // check path: the call's slots (capacity kept between calls)
 };
 
 static std::mutex g_mu;
@@ -208,13 +218,6 @@ static void pmk_bytes(const uint32_t w[8], uint8_t out[32]) {
 // ---------------------------------------------------------------------------------------------------------
 // explicit keys -> slots (server-side check path and dwpa_pbkdf2_pmk)
 // ---------------------------------------------------------------------------------------------------------
-struct Slot {
-    std::string_view key;     // bytes hashed (after hc_unhex): the caller's buffer or a decoded copy
-    uint32_t job;
-    uint32_t ordinal;         // index among the job's non-null keys
-    const std::string* essid;
-    bool pbkdf2;              // false: PMK supplied by the caller
-};
 
 // 64-bit hash of a byte string (8-byte multiply-xor rounds) for the (ESSID run, key) dedup table.
 static uint64_t hash_bytes(const char* p, size_t n, uint64_t seed) {
@@ -321,6 +324,7 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     }
     runs.push_back(n);
     const size_t nruns = runs.size() - 1;
+    tr.mark("  runs");
     for (size_t r = 0; r < nruns; r++)  // count word + [2][nblk][16], nblk = SHA-1 blocks of ESSID || INT(i) || pad
         saltwords += 1 + 32 * ((slots[b + runs[r]].essid->size() + 4 + 9 + 63) / 64);
     // pinned staging, sized by upper bounds: <= n unique keys, <= keybytes key bytes, <= n caller PMKs
@@ -390,6 +394,7 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
             uhash.clear();
         }
     });
+    tr.mark("  dedup tables");
     size_t nu_total = 0, nsp = 0, ncp = 0, nbytes = 0;
     for (Part& P : parts) {
         P.ubase = nu_total;
@@ -426,7 +431,7 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
         }
     });
     st.off[nu] = nbytes;
-    tr.mark("  dedup (ESSID, key)");
+    tr.mark("  concat");
     // ids = key ordinals (select the PHP attempt list of each key)
     for (uint32_t i = 0; i < n; i++) st.ids[i] = slots[b + i].ordinal;
 
@@ -632,20 +637,36 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         nslots += keys[j].size();
     }
     if (!nslots) return 0;
-    std::vector<Slot> slots;
-    slots.reserve(nslots);
-    for (const auto& js : by_essid)
-        for (uint32_t j : js)
-            for (uint32_t o = 0; o < keys[j].size(); o++)
-                slots.push_back({keys[j][o], j, o, &parsed[j].essid, !(o == 0 && job_pmk[j])});
+    tr.mark("essid groups");
+    // slot order: ESSID groups in first-seen order, jobs in input order, keys in order; filled per group range on
+    // up to 8 host threads (contiguous group ranges of about equal slot counts)
+    // the device's slot buffer keeps its pages between calls (a fresh 8 MB vector per C5 call page-faults)
+    std::vector<Slot>& slots = d.slots;
+    slots.resize(nslots);
+    std::vector<size_t> gbase(by_essid.size() + 1, 0);
+    for (size_t g = 0; g < by_essid.size(); g++) {
+        gbase[g + 1] = gbase[g];
+        for (uint32_t j : by_essid[g]) gbase[g + 1] += keys[j].size();
+    }
+    const size_t TS = std::min(host_threads(nslots, 16384), by_essid.size());
+    parallel_for(TS, [&](size_t t) {
+        const size_t g0 = std::lower_bound(gbase.begin(), gbase.end() - 1, nslots * t / TS) - gbase.begin();
+        const size_t g1 = std::lower_bound(gbase.begin(), gbase.end() - 1, nslots * (t + 1) / TS) - gbase.begin();
+        for (size_t g = g0; g < (t + 1 == TS ? by_essid.size() : g1); g++) {
+            size_t i = gbase[g];
+            for (uint32_t j : by_essid[g])
+                for (uint32_t o = 0; o < keys[j].size(); o++)
+                    slots[i++] = {keys[j][o], j, o, &parsed[j].essid, !(o == 0 && job_pmk[j])};
+        }
+    });
     tr.mark("slots");
 
     // The first chunk's PBKDF2 is queued before the line tables exist: the host builds them while the GPU derives.
     TableBuilder tb;
     std::vector<HitDev> hits;
     const size_t chunk = default_batch();
-    for (size_t b = 0; b < slots.size(); b += chunk) {
-        const size_t e = std::min(slots.size(), b + chunk);
+    for (size_t b = 0; b < nslots; b += chunk) {
+        const size_t e = std::min(nslots, b + chunk);
         DeriveStage st;
         RCHK(derive_slots(d, slots, b, e, job_pmk, st));
         if (b == 0) {
