@@ -126,6 +126,7 @@ struct Device {
     std::mutex mu;
     Batch batch;
     DevBuf lines, atts, pool, segs, segs_tail, salt, koff, kbytes, idsup;
+    DevBuf keys, keys_tail;        // check path: per-key EapolKey scratch of the attempt-parallel verify
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
     std::vector<Slot> slots;       // check path: the call's slots (capacity kept between calls)
 };
@@ -313,7 +314,7 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     PhaseTrace tr;
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
-    RCHK(d.batch.reserve(n, n));
+    RCHK(d.batch.reserve(n, 2 * n + 64));  // attempt-parallel verify: <= 2 matching attempts per (key, line)
     // ESSID runs of this chunk (slots arrive grouped by ESSID)
     std::vector<uint32_t> runs{0};
     size_t keybytes = 0, saltwords = 0;
@@ -495,7 +496,7 @@ static int join_tail(Device& d) {
 // one; segments are runs of <= 64 consecutive slots of one job.  Hits are appended on the device (collect_hits).
 static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, size_t b, size_t e,
                         const std::vector<uint32_t>& job_line, const TableBuilder& tb, bool upload_tables,
-                        hipStream_t s, DevBuf& segbuf) {
+                        hipStream_t s, DevBuf& segbuf, DevBuf& keybuf) {
     const uint32_t n = (uint32_t)(e - b), row0 = (uint32_t)(b - base);
     if (!n && !upload_tables) return 0;
     // bucket = mode * 4 + class index; mode 1 = attempt-parallel (EAPOL lines with >= ATT_PARALLEL_MIN attempts)
@@ -511,6 +512,20 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
             bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, row0 + i, j - i, 0});
         i = j;
     }
+    // attempt-parallel buckets: pad = the segment's first wave in its launch (ceil(count * natt / 64) waves each)
+    uint32_t nwaves[8] = {0}, kwords = 0, kstride = 0;
+    for (int k = 4; k < 8; k++) {
+        for (SegDev& sg : bucket[k]) {
+            sg.pad = nwaves[k];
+            nwaves[k] += (uint32_t)(((uint64_t)sg.count * tb.lines[sg.line].natt + 63) / 64);
+        }
+        if (!bucket[k].empty()) {
+            kwords = std::max(kwords, eapol_key_words(1u << (k & 3)));
+            kstride = std::max(kstride, (uint32_t)bucket[k].size() * 64);
+        }
+    }
+    // one scratch of per-key EapolKey states for the stream's attempt-parallel launches (they run in order)
+    if (kwords) RCHK(keybuf.ensure((size_t)kwords * kstride * 4));
     std::vector<SegDev> segs;
     size_t bstart[9];
     for (int k = 0; k < 8; k++) {
@@ -537,9 +552,9 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
                                  (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc, s));
         else
             HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, sg,
-                                     nb, (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p,
-                                     (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc,
-                                     s));
+                                     nb, nwaves[k], (uint32_t*)keybuf.p, kstride, (const LineDev*)d.lines.p,
+                                     (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p,
+                                     hitcnt, d.batch.hitcap, vc, s));
     }
     return 0;
 }
@@ -674,8 +689,8 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
                 for (uint32_t j : js) job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
             tr.mark("tables (overlapped)");
         }
-        RCHK(queue_verify(d, slots, b, b, b + st.split, job_line, tb, b == 0, d.stream, d.segs));
-        RCHK(queue_verify(d, slots, b, b + st.split, e, job_line, tb, false, d.tail, d.segs_tail));
+        RCHK(queue_verify(d, slots, b, b, b + st.split, job_line, tb, b == 0, d.stream, d.segs, d.keys));
+        RCHK(queue_verify(d, slots, b, b + st.split, e, job_line, tb, false, d.tail, d.segs_tail, d.keys_tail));
         tr.mark("  verify queued");
         RCHK(collect_hits(d, hits));
     }
@@ -1094,7 +1109,7 @@ void dwpa_shutdown(void) {
         std::lock_guard<std::mutex> dl(d->mu);
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
-        for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->salt, &d->koff, &d->kbytes, &d->idsup,
+        for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->keys, &d->keys_tail, &d->salt, &d->koff, &d->kbytes, &d->idsup,
                           &d->upmk, &d->sref, &d->src, &d->cpmk,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();

@@ -430,52 +430,106 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
 }
 
 // Attempt-parallel verification (server checks with wide nonce windows, e.g. nc=128 -> 261 attempts,
-// common.php:250-300): one wave = one (key slot, EAPOL line) pair, lane = attempt, 64 attempts per pass in PHP
-// order.  The first pass with a match yields the earliest attempt (lowest lane), exactly the attempt PHP
-// returns.  Segment s expands to 64 waves, wave k handling slot segs[s].slot + k.
+// common.php:250-300) in two launches.
+//
+// k_eapol_keys: lane = (segment, key) pair, computes everything of the check that depends on the PMK but not on
+// the attempt (HMAC key midstates, PRF prefix: EapolKey) once per pair into a SoA scratch array, word w of pair
+// (segment i, key k) at keys[w * kstride + 64 i + k].
+//
+// k_verify_att: the (key, attempt) items of a segment are laid out key-major and cut into waves of 64 lanes, so
+// every lane runs one attempt and a wave ends only where the segment does (segs[i].pad = the segment's first wave
+// within the launch).  A wave spans at most two keys (natt >= ATT_PARALLEL_MIN = 64); each lane loads its key's
+// EapolKey.  One wave per key with 64 attempts per pass left 59 of 64 lanes idle in the fifth pass of a 261-attempt
+// list and recomputed the key state in every wave; here no lane idles before the segment's last wave.  Every
+// matching attempt is reported (at most two per key: one BE, one LE value can equal the true nonce); the host
+// keeps the first key in input order, then the first attempt in PHP order.
+template <uint32_t VC>
+constexpr uint32_t eapol_key_words() { return (VC & VC_KV3) ? 16u : 10u; }
+
+template <uint32_t VC>
+__global__ __launch_bounds__(256) void k_eapol_keys(const uint32_t* __restrict__ pmk, uint32_t cap,
+                                                    const SegDev* __restrict__ segs, uint32_t nsegs,
+                                                    const LineDev* __restrict__ lines,
+                                                    const uint32_t* __restrict__ pool, uint32_t* __restrict__ keys,
+                                                    uint32_t kstride) {
+    const uint32_t segi = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const uint32_t k = threadIdx.x & 63;
+    if (segi >= nsegs) return;
+    const SegDev sg = segs[segi];
+    if (k >= sg.count) return;
+    const LineDev L = lines[sg.line];
+    uint32_t p[8];
+#pragma unroll
+    for (int w = 0; w < 8; w++) p[w] = pmk[(size_t)w * cap + sg.slot + k];
+    EapolKey K;
+    eapol_key<VC>(L, pool, p, K);
+    uint32_t* o = keys + (size_t)segi * 64 + k;
+    if ((VC & VC_KV3) && L.keyver == 3) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            o[(size_t)w * kstride] = K.op2[w];
+            o[(size_t)(8 + w) * kstride] = K.pre2[w];
+        }
+    } else {
+#pragma unroll
+        for (int w = 0; w < 5; w++) {
+            o[(size_t)w * kstride] = K.op1[w];
+            o[(size_t)(5 + w) * kstride] = K.pre1[w];
+        }
+    }
+}
+
 template <uint32_t VC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify_att(
                                                     const uint32_t* __restrict__ pmk, uint32_t cap,
                                                     const uint64_t* __restrict__ ids,
-                                                    const SegDev* __restrict__ segs, uint32_t nsegs,
+                                                    const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t nwaves,
+                                                    const uint32_t* __restrict__ keys, uint32_t kstride,
                                                     const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool,
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                     uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
     __shared__ uint32_t te_lds[256];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
-    const uint32_t segi = gw >> 6, k = gw & 63;
-    if (segi >= nsegs) return;
+    const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    if (gw >= nwaves) return;
+    // the segment holding wave gw: last i with segs[i].pad <= gw (wave-uniform binary search, scalar loads)
+    uint32_t lo = 0, hi = nsegs;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (segs[mid].pad <= gw) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t segi = lo;
     const SegDev sg = segs[segi];
-    if (k >= sg.count) return;
-    const uint32_t slot = sg.slot + k;
     const LineDev L = lines[sg.line];
-    uint32_t p[8];
-#pragma unroll
-    for (int w = 0; w < 8; w++) p[w] = pmk[(size_t)w * cap + slot];
+    const uint32_t item = (gw - sg.pad) * 64 + lane;
+    const uint32_t k = item / L.natt, a = item - k * L.natt;
+    const bool active = k < sg.count;
+    const uint32_t kk = active ? k : sg.count - 1;  // idle lanes of the segment's last wave repeat a real key
+    const uint32_t slot = sg.slot + kk;
     const uint64_t cand = ids ? ids[slot] : (uint64_t)slot;
     EapolKey K;
-    eapol_key<VC>(L, pool, p, K);
-    const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
-    const AttDev* al = atts + L.list_off + sel * L.natt;
-    for (uint32_t a0 = 0; a0 < L.natt; a0 += 64) {
-        const uint32_t a = a0 + lane;
-        bool match = false;
-        if (a < L.natt) {
-            uint32_t mic[4];
-            eapol_mic<VC>(L, pool, K, al[a], te, mic);
-            match = mic_match(L, mic);
+    const uint32_t* kp = keys + (size_t)segi * 64 + kk;
+    if ((VC & VC_KV3) && L.keyver == 3) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) {
+            K.op2[w] = kp[(size_t)w * kstride];
+            K.pre2[w] = kp[(size_t)(8 + w) * kstride];
         }
-        const uint64_t m = __ballot(match);
-        if (m) {
-            const uint32_t first = (uint32_t)__builtin_ctzll(m);
-            report_hits(lane == first, lane, cand, sg.line, a0 + first, pmk + slot, cap, hits, hitcnt, hitcap);
-            return;
+    } else {
+#pragma unroll
+        for (int w = 0; w < 5; w++) {
+            K.op1[w] = kp[(size_t)w * kstride];
+            K.pre1[w] = kp[(size_t)(5 + w) * kstride];
         }
     }
+    const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
+    uint32_t mic[4];
+    eapol_mic<VC>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic);
+    const bool found = active && mic_match(L, mic);
+    report_hits(found, lane, cand, sg.line, a, pmk + slot, cap, hits, hitcnt, hitcap);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -553,14 +607,19 @@ hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids,
     return hipGetLastError();
 }
 
+uint32_t eapol_key_words(uint32_t vc) { return (vc & VC_KV3) ? 16u : 10u; }
+
 hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
-                             uint32_t nsegs, const LineDev* lines, const uint32_t* pool, const AttDev* atts,
-                             HitDev* hits, uint32_t* hitcnt, uint32_t hitcap, uint32_t vc, hipStream_t s) {
-    if (nsegs == 0) return hipSuccess;
-    const dim3 grid(cdiv((uint64_t)nsegs * 64, 4));
-#define DWPA_LAUNCH_VERIFY_ATT(V) \
-    hipLaunchKernelGGL(k_verify_att<V>, grid, dim3(256), 0, s, pmk, cap, ids, segs, nsegs, lines, pool, atts, hits, \
-                       hitcnt, hitcap)
+                             uint32_t nsegs, uint32_t nwaves, uint32_t* keys, uint32_t kstride, const LineDev* lines,
+                             const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt,
+                             uint32_t hitcap, uint32_t vc, hipStream_t s) {
+    if (nsegs == 0 || nwaves == 0) return hipSuccess;
+    if (kstride < nsegs * 64) return hipErrorInvalidValue;
+#define DWPA_LAUNCH_VERIFY_ATT(V)                                                                                 \
+    hipLaunchKernelGGL(k_eapol_keys<V>, dim3(cdiv((uint64_t)nsegs * 64, 256)), dim3(256), 0, s, pmk, cap, segs,   \
+                       nsegs, lines, pool, keys, kstride);                                                         \
+    hipLaunchKernelGGL(k_verify_att<V>, dim3(cdiv(nwaves, 4)), dim3(256), 0, s, pmk, cap, ids, segs, nsegs, nwaves, \
+                       keys, kstride, lines, pool, atts, hits, hitcnt, hitcap)
     DWPA_VC_DISPATCH(vc & ~VC_PMKID, DWPA_LAUNCH_VERIFY_ATT)
 #undef DWPA_LAUNCH_VERIFY_ATT
     return hipGetLastError();
