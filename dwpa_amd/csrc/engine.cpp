@@ -19,6 +19,8 @@
 #include <string_view>
 #include <unordered_map>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -242,17 +244,76 @@ static size_t host_threads(size_t n, size_t min_per_thread) {
     return std::max<size_t>(1, std::min<size_t>({8, hw ? hw : 1, n / std::max<size_t>(1, min_per_thread)}));
 }
 
-// fn(t) for t in [0, T) on T threads (the calling thread runs t = 0).
+// Host worker pool of the check path: a C5 call runs four parallel phases, and spawning 7 threads per phase cost
+// more than the smaller phases themselves.  Workers live for the process; concurrent calls (one per device) share
+// them, and a caller waiting for its tasks runs queued tasks itself, so waiting never blocks progress.
+class HostPool {
+  public:
+    static HostPool& get() {
+        static HostPool* pool = new HostPool();  // never destroyed: workers may outlive static destructors
+        return *pool;
+    }
+    template <typename F>
+    void run(size_t T, const F& fn) {
+        std::atomic<size_t> left{T - 1};
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            grow_locked(T - 1);
+            for (size_t t = 1; t < T; t++)
+                q_.push_back([&fn, &left, t] {
+                    fn(t);
+                    left.fetch_sub(1, std::memory_order_acq_rel);
+                });
+        }
+        cv_.notify_all();
+        fn(0);
+        while (left.load(std::memory_order_acquire)) {
+            std::function<void()> task;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!q_.empty()) {
+                    task = std::move(q_.front());
+                    q_.pop_front();
+                }
+            }
+            if (task) task();
+            else std::this_thread::yield();
+        }
+    }
+
+  private:
+    void grow_locked(size_t want) {
+        while (workers_ < want) {
+            std::thread([this] { loop(); }).detach();
+            workers_++;
+        }
+    }
+    void loop() {
+        for (;;) {
+            std::function<void()> task;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return !q_.empty(); });
+                task = std::move(q_.front());
+                q_.pop_front();
+            }
+            task();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    size_t workers_ = 0;
+};
+
+// fn(t) for t in [0, T) on up to T threads (the calling thread runs t = 0, pool workers the rest).
 template <typename F>
 static void parallel_for(size_t T, const F& fn) {
     if (T <= 1) {
         if (T == 1) fn(0);
         return;
     }
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < T; t++) th.emplace_back([&fn, t] { fn(t); });
-    fn(0);
-    for (auto& x : th) x.join();
+    HostPool::get().run(T, fn);
 }
 
 // A typed view of pinned staging memory.
