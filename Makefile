@@ -57,7 +57,7 @@ clean:
 
 .PHONY: all oracle clean asm
 
-tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat
+tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -72,3 +72,7 @@ tools/bin/valu_peak: tools/valu_peak.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
 .PHONY: tools
+
+tools/bin/valu_peak64: tools/valu_peak64.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
