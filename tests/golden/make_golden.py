@@ -241,6 +241,17 @@ def mixed():
     add(line, [psk, psk], nc=8, tag="dup-keys")
     add(line, [], nc=8, tag="no-keys")
     add(line, [None, None], nc=8, tag="null-keys")
+    # short ANONCE with wide windows (>= 64 attempts per list): the attempt-parallel verify with explicit per-key
+    # lists, the winning attempt past the first 64 lanes and the key past the first list
+    for (anlen, keys_before, att, nc, kv) in [(20, 2, 40, 32, 2), (29, 1, 100, 128, 2), (20, 3, 200, 128, 2),
+                                              (20, 1, 70, 128, 1)]:
+        essid, ap, sta, an, sn = S.random_net(rng)
+        sn = bytes([0]) + sn[1:]
+        an = bytes([255]) + an[1:anlen]
+        psk = S.random_psk(rng)
+        line = short_anonce_line(psk, essid, ap, sta, sn, an, kv, keys_before, att, nc)
+        keys = [S.random_psk(rng) for _ in range(keys_before)] + [psk, S.random_psk(rng)]
+        add(line, keys, nc=nc, tag=f"short-anonce-wide-{anlen}-{keys_before}-{att}-{nc}-kv{kv}")
     return {"jobs": jobs}
 
 
