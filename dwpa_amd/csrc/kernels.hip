@@ -344,8 +344,9 @@ __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
 
 // Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
 // wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
-// Occupancy target per class (VGPR budget without scratch spills): PMKID and keyver 1 fit 64 VGPRs (8 waves/SIMD),
-// keyver 2 80 (6 waves), keyver 3 keeps 44 AES round-key registers (2 waves).
+// Occupancy target per class: PMKID and keyver 1 fit 64 VGPRs (8 waves/SIMD); keyver 2 is held at 64 too and spills
+// 9 VGPRs, which measured level with a 6-wave, spill-free build (profiles/r01/verify_waves_ab); keyver 3 keeps 44 AES
+// round-key registers (2 waves).
 constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? 2 : 8; }
 
 template <uint32_t VC>
