@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <memory>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -24,161 +26,20 @@
 #include "dwpa22000.h"
 #include "engine.hpp"
 #include "m22000_host.hpp"
+#include "dict_reader.hpp"
 #include "rules.hpp"
 
 namespace dwpa {
 
-struct Chunk {
-    std::vector<uint64_t> off;  // words+1 offsets
-    std::string bytes;          // concatenated words (decoded)
-    size_t words() const { return off.empty() ? 0 : off.size() - 1; }
-};
-
-// Dictionary reader: plain or gzip (zlib reads both), one word per line, "\n" or "\r\n", $HEX[] decoded.  Lines
-// are cut straight out of the inflate buffer with memchr and appended to the chunk (no per-line allocation): the
-// reader has to keep up with 8 GPUs at ~5 M words/s each when a work unit has one ESSID and no rules.
-class DictReader {
-  public:
-    explicit DictReader(const std::vector<std::string>& paths) : paths_(paths) {}
-    // Returns false at the end of all files; sets err on I/O failure.
-    bool next(Chunk& c, size_t max_words, size_t max_bytes, bool& err) {
-        c.off.clear();
-        c.bytes.clear();
-        c.off.push_back(0);
-        while (c.words() < max_words && c.bytes.size() < max_bytes) {
-            if (!gz_) {
-                if (idx_ >= paths_.size()) break;
-                gz_ = gzopen(paths_[idx_].c_str(), "rb");
-                if (!gz_) { err = true; return false; }
-                gzbuffer(gz_, 1 << 20);
-                pos_ = len_ = 0;
-            }
-            if (pos_ >= len_) {
-                const int r = gzread(gz_, buf_, sizeof(buf_));
-                if (r < 0) { err = true; return false; }
-                if (r == 0) {  // end of this file: a last line without '\n' is still a word
-                    if (!partial_.empty()) emit(c, partial_.data(), partial_.size());
-                    partial_.clear();
-                    gzclose(gz_);
-                    gz_ = nullptr;
-                    idx_++;
-                    continue;
-                }
-                pos_ = 0;
-                len_ = (size_t)r;
-            }
-            const char* p = buf_ + pos_;
-            const char* end = buf_ + len_;
-            while (p < end && c.words() < max_words && c.bytes.size() < max_bytes) {
-                const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
-                if (!nl) {
-                    partial_.append(p, (size_t)(end - p));
-                    p = end;
-                    break;
-                }
-                if (!partial_.empty()) {
-                    partial_.append(p, (size_t)(nl - p));
-                    emit(c, partial_.data(), partial_.size());
-                    partial_.clear();
-                } else {
-                    emit(c, p, (size_t)(nl - p));
-                }
-                p = nl + 1;
-            }
-            pos_ = (size_t)(p - buf_);
-        }
-        return c.words() > 0;
-    }
-    ~DictReader() {
-        if (gz_) gzclose(gz_);
-    }
-
-  private:
-    static void emit(Chunk& c, const char* p, size_t k) {
-        if (k && p[k - 1] == '\r') k--;
-        if (k > 5 && p[0] == '$' && starts_hex((const uint8_t*)p, k)) c.bytes += hc_unhex(std::string(p, k));
-        else c.bytes.append(p, k);
-        c.off.push_back(c.bytes.size());
-    }
-    std::vector<std::string> paths_;
-    size_t idx_ = 0;
-    gzFile gz_ = nullptr;
-    char buf_[1 << 16];
-    size_t pos_ = 0, len_ = 0;
-    std::string partial_;
-};
-
-// Dictionary chunks from several files at once: worker t reads files t, t+T, ... with its own DictReader and
-// queues its chunks (first chunk small, then doubling to max_words), so inflating several gz dictionaries uses
-// several host cores.  Chunks arrive in completion order; candidate order only decides which of two identical
-// PSKs is written, so the outfile is the same as hashcat's.
-class ChunkSource {
-  public:
-    ChunkSource(const std::vector<std::string>& paths, size_t first_words, size_t max_words) {
-        const size_t T = std::max<size_t>(1, std::min<size_t>(paths.size(), 4));
-        cap_ = T + 1;
-        live_ = T;
-        for (size_t t = 0; t < T; t++) {
-            std::vector<std::string> mine;
-            for (size_t i = t; i < paths.size(); i += T) mine.push_back(paths[i]);
-            workers_.emplace_back([this, mine, first_words, max_words, T] { work(mine, first_words, std::max<size_t>(first_words, max_words / T)); });
-        }
-    }
-    ~ChunkSource() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& w : workers_) w.join();
-    }
-    // Blocks until a chunk is ready; false once every file is read (or on an I/O error: err is set).
-    bool next(Chunk& c, bool& err) {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return !q_.empty() || live_ == 0; });
-        err = err || err_;
-        if (q_.empty()) return false;
-        c = std::move(q_.front());
-        q_.pop_front();
-        cv_.notify_all();
-        return true;
-    }
-
-  private:
-    void work(const std::vector<std::string>& paths, size_t words, size_t max_words) {
-        DictReader reader(paths);
-        bool err = false;
-        for (;;) {
-            Chunk c;
-            const bool have = reader.next(c, words, (size_t)1 << 31, err);
-            words = std::min(max_words, 2 * words);
-            std::unique_lock<std::mutex> lk(mu_);
-            if (!have || err || stop_) break;
-            cv_.wait(lk, [&] { return q_.size() < cap_ || stop_; });
-            if (stop_) break;
-            q_.push_back(std::move(c));
-            cv_.notify_all();
-        }
-        std::lock_guard<std::mutex> lk(mu_);
-        err_ = err_ || err;
-        live_--;
-        cv_.notify_all();
-    }
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<Chunk> q_;
-    size_t cap_ = 2, live_ = 0;
-    bool stop_ = false, err_ = false;
-    std::vector<std::thread> workers_;
-};
-
 struct CrackShared {
     std::mutex mu;
-    std::vector<uint8_t> cracked;         // per input line
+    std::vector<uint8_t> cracked;         // per input line (1: cracked, or never usable)
     std::vector<ParsedLine> parsed;
     FILE* out = nullptr;
     size_t valid = 0, ncracked = 0;
-    int error = 0;
+    std::atomic<uint32_t> version{0};     // bumped for every newly cracked line: workers re-sync their scans
+    std::atomic<bool> stop{false};        // every usable line cracked, or an error
+    std::atomic<int> error{0};
 };
 
 static std::string outfile_record(const ParsedLine& p, const std::string& psk) {
@@ -187,18 +48,77 @@ static std::string outfile_record(const ParsedLine& p, const std::string& psk) {
            hashcat_plain(p.essid) + ":" + hashcat_plain(psk) + "\n";
 }
 
-// Per-device state.  Shards are uploaded into one of two buffer slots on the `up` stream by the thread that read
-// the chunk, so the upload of chunk k+1 overlaps the scan of chunk k; the scan waits on `staged[slot]`.
+// One contiguous word range of a dictionary chunk.  The chunk stays alive until its last range is scanned.
+struct WorkItem {
+    std::shared_ptr<const Chunk> chunk;
+    size_t b = 0, e = 0;
+};
+
+// Cuts the reader's chunks into work items that every shard worker pulls for itself: a device that finishes its
+// item early takes the next one, so no device waits for the slowest at a chunk boundary.  Items start at `first`
+// words (one batch of candidates, so every device starts after one batch's read) and double up to `most`.
+class ItemQueue {
+  public:
+    ItemQueue(ChunkSource& src, size_t first, size_t most) : src_(src), size_(std::max<size_t>(1, first)),
+                                                             most_(std::max<size_t>(1, most)) {}
+    bool next(WorkItem& it) {
+        std::lock_guard<std::mutex> lk(mu_);
+        while (!cur_ || pos_ >= cur_->words()) {
+            if (done_) return false;
+            Chunk c;
+            if (!src_.next(c, err_)) {
+                done_ = true;
+                cur_.reset();
+                return false;
+            }
+            cur_ = std::make_shared<const Chunk>(std::move(c));
+            pos_ = 0;
+        }
+        const size_t n = std::min(size_, cur_->words() - pos_);
+        it.chunk = cur_;
+        it.b = pos_;
+        it.e = pos_ + n;
+        pos_ += n;
+        size_ = std::min(most_, 2 * size_);
+        return true;
+    }
+    bool io_error() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return err_;
+    }
+
+  private:
+    ChunkSource& src_;
+    std::mutex mu_;
+    std::shared_ptr<const Chunk> cur_;
+    size_t pos_ = 0, size_, most_;
+    bool done_ = false, err_ = false;
+};
+
+// One shard worker (one per device, or DWPA_CRACK_SHARDS_PER_DEVICE per device).  Its stager thread uploads the
+// next item into the free one of two buffer slots on the `up` stream while its scanner thread scans the other.
 struct DevWork {
-    int device;
+    int device = 0;
     dwpa_scan* scan = nullptr;
+    DevRules rules;
     DevBuf off[2], bytes[2];
     std::vector<uint64_t> hoff[2];  // host staging of the rebased offsets (alive until the upload completes)
     hipStream_t stream = nullptr, up = nullptr;
     hipEvent_t staged[2] = {nullptr, nullptr};
+    double keep = 1.0;              // surviving candidates per (word x rule), carried from item to item
+    uint32_t seen_version = 0;      // sh.version this scan's retired lines reflect
+    size_t items = 0, words = 0;    // statistics (DWPA_TRACE)
+    double wait_s = 0;              // scanner time spent waiting for a staged item
+    // stager -> scanner hand-over
+    std::mutex mu;
+    std::condition_variable cv;
+    WorkItem slot_item[2];
+    bool slot_full[2] = {false, false};
+    std::deque<int> ready;
+    bool staging_done = false;
 };
 
-// Upload words [b, e) of chunk c (offsets rebased to the shard) into slot `slot` of device w.
+// Upload words [b, e) of chunk c (offsets rebased to the item) into slot `slot` of worker w.
 static int stage_shard(DevWork& w, const Chunk& c, size_t b, size_t e, int slot) {
     if (hipSetDevice(w.device) != hipSuccess) return DWPA_E_HIP;
     std::vector<uint64_t>& off = w.hoff[slot];
@@ -216,8 +136,18 @@ static int stage_shard(DevWork& w, const Chunk& c, size_t b, size_t e, int slot)
     return 0;
 }
 
+// Retire on w's scan every line cracked anywhere so far (hashcat reports each hash once).
+static void sync_retired(DevWork& w, CrackShared& sh) {
+    const uint32_t v = sh.version.load(std::memory_order_acquire);
+    if (v == w.seen_version) return;
+    std::lock_guard<std::mutex> lk(sh.mu);
+    for (size_t i = 0; i < sh.cracked.size(); i++)
+        if (sh.cracked[i]) scan_mark_cracked(w.scan, (uint32_t)i);
+    w.seen_version = v;
+}
+
 static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, size_t e, const RuleSet* rules,
-                      DevRules* drules, int slot) {
+                      int slot) {
     if (e <= b) return 0;
     if (hipSetDevice(w.device) != hipSuccess) return DWPA_E_HIP;
     if (hipStreamWaitEvent(w.stream, w.staged[slot], 0) != hipSuccess) return DWPA_E_HIP;
@@ -226,21 +156,20 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
     const uint32_t cap = scan_batch_cap(w.scan);
     const size_t words = e - b;
     const uint64_t nrules = rules ? rules->size() : 1;
-    const uint64_t total = words * nrules;
     // candidate id = word * nrules + rule; batches walk the candidate space in order.  Every PBKDF2 lane runs the
     // same 4096 iterations, so a batch costs ceil(candidates / 256K) wave rounds whatever its fill: the words per
     // batch follow the observed fraction of candidates that survive the 8..63 filter (and the rules), aiming at
     // 99.5 % of the batch.  A load that overflows the batch (the compaction drops and counts the excess) is
     // repeated with fewer words before anything is derived.
-    double keep = 1.0;  // surviving candidates per (word x rule)
-    for (size_t wb = 0; wb < words;) {
+    double& keep = w.keep;
+    for (size_t wb = 0; wb < words && !sh.stop.load(std::memory_order_relaxed);) {
         // keep == 1 (nothing filtered so far): exactly one batch of candidates, which cannot overflow
         const double want = (keep >= 1.0 ? 1.0 : 0.995) * cap / ((double)nrules * keep);
         const uint64_t most = 16ull * cap / nrules;  // kernel-side bound on a fill-mode load
         const uint32_t nw = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)want, most, words - wb}));
         int r;
         if (rules)
-            r = rules_load(w.scan, drules, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, w.stream, true);
+            r = rules_load(w.scan, &w.rules, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, w.stream, true);
         else
             r = scan_load_dict(w.scan, (const uint64_t*)woff.p, (const uint8_t*)wbytes.p, wb, nw, 8, 63, w.stream,
                                true);
@@ -258,6 +187,7 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
             wb += nw;
             continue;
         }
+        sync_retired(w, sh);
         if ((r = scan_run(w.scan, w.stream)) < 0) return r;  // all ESSID groups, grouped per launch
         wb += nw;
         std::vector<HitDev> hits;
@@ -274,21 +204,37 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
             if (rules) plain = rules->apply_host((size_t)rule, plain);
             sh.cracked[ph.line] = 1;
             sh.ncracked++;
+            sh.version.fetch_add(1, std::memory_order_acq_rel);
             const std::string rec = outfile_record(sh.parsed[ph.line], plain);
             fwrite(rec.data(), 1, rec.size(), sh.out);
             fflush(sh.out);
         }
-        (void)total;
+        if (sh.ncracked == sh.valid) sh.stop = true;
     }
     return 0;
+}
+
+// DWPA_CRACK_SHARDS_PER_DEVICE=k runs k shard workers per selected device (default 1).  On a one-GPU box k = 2
+// rehearses the multi-device path -- per-worker queues, shard scans and cross-worker line retirement -- that a
+// volunteer's 8-GPU node runs (hashcat uses every device, help_crack.py:773).
+static size_t shards_per_device() {
+    const char* e = getenv("DWPA_CRACK_SHARDS_PER_DEVICE");
+    const long k = e ? strtol(e, nullptr, 10) : 1;
+    return (size_t)std::min<long>(8, std::max<long>(1, k));
+}
+
+static bool trace_on() {
+    const char* e = getenv("DWPA_TRACE");
+    return e && *e == '1';
 }
 
 static int crack_impl(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file, int nec,
                       const char* out_file, const dwpa_config* cfg) {
     if (!hash_file || !out_file || (!dicts && ndicts)) return DWPA_RC_ERROR;
-    if (cfg && dwpa_init(cfg) < 0) return DWPA_RC_ERROR;
+    if (cfg && cfg->struct_size && cfg->struct_size < sizeof(uint32_t) * 3) return DWPA_RC_ERROR;
+    // the config applies to this call only (dwpa_init's process-wide selection stays as it is)
     if (engine_init() < 0) return DWPA_RC_ERROR;
-    std::vector<int> devs = engine_devices();
+    std::vector<int> devs = engine_devices(cfg ? cfg->device_mask : 0);
     if (devs.empty()) return DWPA_RC_ERROR;
     const int nc_mode = cfg ? cfg->nc_mode : DWPA_NC_HASHCAT;
 
@@ -315,7 +261,9 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     sh.cracked.assign(lines.size(), 0);
     for (size_t i = 0; i < lines.size(); i++) {
         sh.parsed[i] = parse_m22000(lines[i].data(), lines[i].size());
-        if (sh.parsed[i].status) sh.cracked[i] = 1;  // rejected by the parser (hashcat: token exception)
+        // rejected by the parser (hashcat: token exception), or a PMKID/MIC shorter than 16 bytes that can never
+        // verify (hashcat refuses such a hash at load time): neither is counted, so rc 0 stays reachable
+        if (sh.parsed[i].status || !line_can_match(sh.parsed[i])) sh.cracked[i] = 1;
         else sh.valid++;
     }
     if (sh.valid == 0) return DWPA_RC_ERROR;  // hashcat: "No hashes loaded"
@@ -334,82 +282,137 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     std::vector<size_t> ll(lines.size());
     for (size_t i = 0; i < lines.size(); i++) { lp[i] = lines[i].data(); ll[i] = lines[i].size(); }
     const uint32_t batch = cfg && cfg->batch ? cfg->batch : engine_batch();
-    std::vector<DevWork> work(devs.size());
-    std::vector<DevRules> drules(devs.size());
+    const size_t spd = shards_per_device();
+    std::vector<std::unique_ptr<DevWork>> work;
     int rc = 0;
-    for (size_t k = 0; k < devs.size() && rc >= 0; k++) {
-        work[k].device = devs[k];
-        (void)hipSetDevice(devs[k]);
-        if (hipStreamCreateWithFlags(&work[k].stream, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&work[k].up, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&work[k].staged[0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&work[k].staged[1], hipEventDisableTiming) != hipSuccess)
-            rc = DWPA_E_HIP;
-        if (rc >= 0) rc = scan_create(devs[k], lp.data(), ll.data(), lines.size(), nec, nc_mode, batch, &work[k].scan);
-        if (rc >= 0 && rp) rc = rules_upload(devs[k], rules, &drules[k]);
-    }
+    for (int dev : devs)
+        for (size_t k = 0; k < spd && rc >= 0; k++) {
+            work.push_back(std::make_unique<DevWork>());
+            DevWork& w = *work.back();
+            w.device = dev;
+            (void)hipSetDevice(dev);
+            if (hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&w.up, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&w.staged[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&w.staged[1], hipEventDisableTiming) != hipSuccess)
+                rc = DWPA_E_HIP;
+            if (rc >= 0) rc = scan_create(dev, lp.data(), ll.data(), lines.size(), nec, nc_mode, batch, &w.scan);
+            if (rc >= 0 && rp) rc = rules_upload(dev, rules, &w.rules);
+        }
+    const size_t G = work.size();
 
     std::vector<std::string> dpaths;
     for (size_t i = 0; i < ndicts; i++) dpaths.push_back(dicts[i]);
-    bool ioerr = false;
-    const size_t chunk_words = (size_t)batch * devs.size() * 8;
-    // double-buffered: the next chunk is read/inflated on a host thread while the devices scan this one.  The
-    // first chunk is one batch per device, so the GPUs start after ~0.3 s of reading instead of a full chunk's.
-    // Chunks then double until they reach chunk_words, so each read stays shorter than the previous chunk's scan.
-    Chunk cur, nxt;
-    ChunkSource source(dpaths, (size_t)batch * devs.size(), chunk_words);
-    const size_t G = work.size();
-    // contiguous, equal shards of a chunk, one per device, staged into buffer slot `slot`
-    auto stage_all = [&](const Chunk& c, int slot) {
-        int r = 0;
-        for (size_t k = 0; k < G && r >= 0; k++) r = stage_shard(work[k], c, c.words() * k / G, c.words() * (k + 1) / G, slot);
-        return r;
+    // Items: the first is one batch of candidates, later ones up to 16 batches (a partial last batch per item
+    // then costs ~1 % of its wave rounds).  The reader's chunks start at one item per worker and grow to two
+    // full items per worker, so reading stays ahead of the scans without holding much more than that in memory.
+    const size_t nr = rp ? rp->size() : 1;
+    const size_t first_item = std::max<size_t>(1, batch / nr), most_item = std::max<size_t>(1, 16 * (size_t)batch / nr);
+    ChunkSource source(dpaths, first_item * G, 2 * most_item * G);
+    ItemQueue items(source, first_item, most_item);
+    const auto t0 = std::chrono::steady_clock::now();
+
+    auto stop_all = [&]() {
+        sh.stop = true;
+        source.cancel();  // a stager blocked on the reader returns at once
+        for (auto& wp : work) {
+            std::lock_guard<std::mutex> lk(wp->mu);
+            wp->cv.notify_all();
+        }
     };
-    bool have = source.next(cur, ioerr);
-    int slot = 0, stage_rc = 0;
-    if (have && rc >= 0) rc = stage_all(cur, slot);
-    while (rc >= 0 && have && sh.ncracked < sh.valid) {
-        bool have_next = false;
-        std::thread prefetch([&] {
-            have_next = source.next(nxt, ioerr);
-            if (have_next) stage_rc = stage_all(nxt, slot ^ 1);
-        });
-        {
-            std::lock_guard<std::mutex> lk(sh.mu);  // retire lines cracked so far on every device
-            for (size_t k = 0; k < work.size(); k++)
-                for (size_t i = 0; i < lines.size(); i++)
-                    if (sh.cracked[i]) scan_mark_cracked(work[k].scan, (uint32_t)i);
-        }
-        const size_t W = cur.words();
-        std::vector<std::thread> th;
-        std::vector<int> rcs(G, 0);
+    auto fail = [&](int r) {
+        int z = 0;
+        sh.error.compare_exchange_strong(z, r);
+        stop_all();
+    };
+    std::vector<std::thread> th;
+    if (rc >= 0)
         for (size_t k = 0; k < G; k++) {
-            const size_t b = W * k / G, e = W * (k + 1) / G;
-            th.emplace_back([&, k, b, e] { rcs[k] = scan_shard(work[k], sh, cur, b, e, rp, &drules[k], slot); });
+            DevWork& w = *work[k];
+            th.emplace_back([&, k] {  // stager
+                DevWork& w = *work[k];
+                for (int slot = 0;; slot ^= 1) {
+                    {
+                        std::unique_lock<std::mutex> lk(w.mu);
+                        w.cv.wait(lk, [&] { return !w.slot_full[slot] || sh.stop; });
+                    }
+                    WorkItem it;
+                    if (sh.stop || !items.next(it)) break;
+                    const int r = stage_shard(w, *it.chunk, it.b, it.e, slot);
+                    if (r < 0) {
+                        fail(r);
+                        break;
+                    }
+                    std::lock_guard<std::mutex> lk(w.mu);
+                    w.slot_item[slot] = std::move(it);
+                    w.slot_full[slot] = true;
+                    w.ready.push_back(slot);
+                    w.cv.notify_all();
+                }
+                std::lock_guard<std::mutex> lk(w.mu);
+                w.staging_done = true;
+                w.cv.notify_all();
+            });
+            th.emplace_back([&, k] {  // scanner
+                DevWork& w = *work[k];
+                for (;;) {
+                    int slot;
+                    WorkItem it;
+                    {
+                        const auto tw = std::chrono::steady_clock::now();
+                        std::unique_lock<std::mutex> lk(w.mu);
+                        w.cv.wait(lk, [&] { return !w.ready.empty() || w.staging_done || sh.stop; });
+                        w.wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
+                        if (w.ready.empty() || sh.stop) break;
+                        slot = w.ready.front();
+                        w.ready.pop_front();
+                        it = w.slot_item[slot];
+                    }
+                    const int r = scan_shard(w, sh, *it.chunk, it.b, it.e, rp, slot);
+                    w.items++;
+                    w.words += it.e - it.b;
+                    {
+                        std::lock_guard<std::mutex> lk(w.mu);
+                        w.slot_item[slot] = WorkItem();
+                        w.slot_full[slot] = false;
+                        w.cv.notify_all();
+                    }
+                    if (r < 0) {
+                        fail(r);
+                        break;
+                    }
+                    if (sh.stop) {
+                        stop_all();
+                        break;
+                    }
+                }
+            });
+            (void)w;
         }
-        for (auto& t : th) t.join();
-        prefetch.join();
-        for (int r : rcs)
-            if (r < 0) rc = r;
-        if (stage_rc < 0) rc = stage_rc;
-        std::swap(cur, nxt);
-        slot ^= 1;
-        have = have_next;
+    for (auto& t : th) t.join();
+    source.cancel();
+    const bool ioerr = items.io_error();
+    if (trace_on()) {
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (size_t k = 0; k < G; k++)
+            fprintf(stderr, "[dwpa] crack worker %zu (device %d): %zu items, %zu words, %.3f s waiting for input of %.3f s\n",
+                    k, work[k]->device, work[k]->items, work[k]->words, work[k]->wait_s, el);
     }
-    for (size_t k = 0; k < work.size(); k++) {
-        if (work[k].scan) scan_destroy(work[k].scan);
-        (void)hipSetDevice(work[k].device);
+    for (auto& wp : work) {
+        DevWork& w = *wp;
+        if (w.scan) scan_destroy(w.scan);
+        (void)hipSetDevice(w.device);
         for (int q = 0; q < 2; q++) {
-            work[k].off[q].release();
-            work[k].bytes[q].release();
-            if (work[k].staged[q]) (void)hipEventDestroy(work[k].staged[q]);
+            w.off[q].release();
+            w.bytes[q].release();
+            if (w.staged[q]) (void)hipEventDestroy(w.staged[q]);
         }
-        rules_release(&drules[k]);
-        if (work[k].stream) (void)hipStreamDestroy(work[k].stream);
-        if (work[k].up) (void)hipStreamDestroy(work[k].up);
+        rules_release(&w.rules);
+        if (w.stream) (void)hipStreamDestroy(w.stream);
+        if (w.up) (void)hipStreamDestroy(w.up);
     }
     fclose(sh.out);
-    if (rc < 0 || ioerr) return DWPA_RC_ERROR;
+    if (rc < 0 || sh.error.load() < 0 || ioerr) return DWPA_RC_ERROR;
     return sh.ncracked == sh.valid ? DWPA_RC_CRACKED : DWPA_RC_EXHAUSTED;
 }
 

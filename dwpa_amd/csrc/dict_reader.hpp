@@ -1,0 +1,172 @@
+// dict_reader.hpp -- dictionary streaming for dwpa_crack_files (help_crack.py:520-552 hands hashcat plain or gzip
+// wordlists, one candidate per line, $HEX[...] for non-printable words, maint.php:55-60).  Header-only so that
+// tools/inflate_bench.cpp measures exactly the reader the library runs.
+#pragma once
+#include <string.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "m22000_host.hpp"
+
+namespace dwpa {
+
+struct Chunk {
+    std::vector<uint64_t> off;  // words+1 offsets
+    std::string bytes;          // concatenated words (decoded)
+    size_t words() const { return off.empty() ? 0 : off.size() - 1; }
+};
+
+// Dictionary reader: plain or gzip (zlib reads both), one word per line, "\n" or "\r\n", $HEX[] decoded.  Lines
+// are cut straight out of the inflate buffer with memchr and appended to the chunk (no per-line allocation): the
+// reader has to keep up with 8 GPUs at ~5 M words/s each when a work unit has one ESSID and no rules.
+class DictReader {
+  public:
+    explicit DictReader(const std::vector<std::string>& paths) : paths_(paths) {}
+    // Returns false at the end of all files; sets err on I/O failure.  `cancel` (optional) ends the chunk early.
+    bool next(Chunk& c, size_t max_words, size_t max_bytes, bool& err, const std::atomic<bool>* cancel = nullptr) {
+        c.off.clear();
+        c.bytes.clear();
+        c.off.push_back(0);
+        while (c.words() < max_words && c.bytes.size() < max_bytes) {
+            if (cancel && cancel->load(std::memory_order_relaxed)) break;
+            if (!gz_) {
+                if (idx_ >= paths_.size()) break;
+                gz_ = gzopen(paths_[idx_].c_str(), "rb");
+                if (!gz_) { err = true; return false; }
+                gzbuffer(gz_, 1 << 20);
+                pos_ = len_ = 0;
+            }
+            if (pos_ >= len_) {
+                const int r = gzread(gz_, buf_, sizeof(buf_));
+                if (r < 0) { err = true; return false; }
+                if (r == 0) {  // end of this file: a last line without '\n' is still a word
+                    if (!partial_.empty()) emit(c, partial_.data(), partial_.size());
+                    partial_.clear();
+                    gzclose(gz_);
+                    gz_ = nullptr;
+                    idx_++;
+                    continue;
+                }
+                pos_ = 0;
+                len_ = (size_t)r;
+            }
+            const char* p = buf_ + pos_;
+            const char* end = buf_ + len_;
+            while (p < end && c.words() < max_words && c.bytes.size() < max_bytes) {
+                const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+                if (!nl) {
+                    partial_.append(p, (size_t)(end - p));
+                    p = end;
+                    break;
+                }
+                if (!partial_.empty()) {
+                    partial_.append(p, (size_t)(nl - p));
+                    emit(c, partial_.data(), partial_.size());
+                    partial_.clear();
+                } else {
+                    emit(c, p, (size_t)(nl - p));
+                }
+                p = nl + 1;
+            }
+            pos_ = (size_t)(p - buf_);
+        }
+        return c.words() > 0;
+    }
+    ~DictReader() {
+        if (gz_) gzclose(gz_);
+    }
+
+  private:
+    static void emit(Chunk& c, const char* p, size_t k) {
+        if (k && p[k - 1] == '\r') k--;
+        if (k > 5 && p[0] == '$' && starts_hex((const uint8_t*)p, k)) c.bytes += hc_unhex(std::string(p, k));
+        else c.bytes.append(p, k);
+        c.off.push_back(c.bytes.size());
+    }
+    std::vector<std::string> paths_;
+    size_t idx_ = 0;
+    gzFile gz_ = nullptr;
+    char buf_[1 << 16];
+    size_t pos_ = 0, len_ = 0;
+    std::string partial_;
+};
+
+// Dictionary chunks from several files at once: worker t reads files t, t+T, ... with its own DictReader and
+// queues its chunks (first chunk small, then doubling to max_words), so inflating several gz dictionaries uses
+// several host cores.  Chunks arrive in completion order; candidate order only decides which of two identical
+// PSKs is written, so the outfile is the same as hashcat's.
+class ChunkSource {
+  public:
+    ChunkSource(const std::vector<std::string>& paths, size_t first_words, size_t max_words) {
+        const size_t T = std::max<size_t>(1, std::min<size_t>(paths.size(), 4));
+        cap_ = T + 1;
+        live_ = T;
+        for (size_t t = 0; t < T; t++) {
+            std::vector<std::string> mine;
+            for (size_t i = t; i < paths.size(); i += T) mine.push_back(paths[i]);
+            workers_.emplace_back([this, mine, first_words, max_words, T] { work(mine, first_words, std::max<size_t>(first_words, max_words / T)); });
+        }
+    }
+    ~ChunkSource() {
+        cancel();
+        for (auto& w : workers_) w.join();
+    }
+    // Stops the readers (within one 64 KiB read) and makes next() return false.
+    void cancel() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cancel_ = true;
+        cv_.notify_all();
+    }
+    // Blocks until a chunk is ready; false once every file is read (or on an I/O error: err is set).
+    bool next(Chunk& c, bool& err) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty() || live_ == 0 || stop_; });
+        err = err || err_;
+        if (q_.empty() || stop_) return false;
+        c = std::move(q_.front());
+        q_.pop_front();
+        cv_.notify_all();
+        return true;
+    }
+
+  private:
+    void work(const std::vector<std::string>& paths, size_t words, size_t max_words) {
+        DictReader reader(paths);
+        bool err = false;
+        for (;;) {
+            Chunk c;
+            const bool have = reader.next(c, words, (size_t)1 << 31, err, &cancel_);
+            words = std::min(max_words, 2 * words);
+            std::unique_lock<std::mutex> lk(mu_);
+            if (!have || err || stop_) break;
+            cv_.wait(lk, [&] { return q_.size() < cap_ || stop_; });
+            if (stop_) break;
+            q_.push_back(std::move(c));
+            cv_.notify_all();
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        err_ = err_ || err;
+        live_--;
+        cv_.notify_all();
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Chunk> q_;
+    size_t cap_ = 2, live_ = 0;
+    bool stop_ = false, err_ = false;
+    std::atomic<bool> cancel_{false};
+    std::vector<std::thread> workers_;
+};
+
+}  // namespace dwpa

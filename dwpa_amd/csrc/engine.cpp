@@ -167,10 +167,12 @@ static int ensure_init() {
     return init_locked(nullptr);
 }
 
-static std::vector<int> active_devices() {
+// Devices selected by `mask` (0 = the dwpa_init() mask; that one 0 = every visible device).
+static std::vector<int> active_devices(uint32_t mask = 0) {
+    if (!mask) mask = g_mask;
     std::vector<int> v;
     for (int d = 0; d < g_ndev; d++)
-        if (!g_mask || (g_mask >> d & 1u)) v.push_back(d);
+        if (!mask || (mask >> d & 1u)) v.push_back(d);
     return v;
 }
 
@@ -1120,7 +1122,7 @@ int scan_device(const dwpa_scan* sc) { return sc->device; }
 // helpers for crack.cpp
 // ---------------------------------------------------------------------------------------------------------
 int engine_init() { return ensure_init(); }
-std::vector<int> engine_devices() { return active_devices(); }
+std::vector<int> engine_devices(uint32_t mask) { return active_devices(mask); }
 uint32_t engine_batch() { return default_batch(); }
 
 }  // namespace dwpa

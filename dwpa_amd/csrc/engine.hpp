@@ -28,7 +28,7 @@ struct Batch {
 };
 
 int engine_init();
-std::vector<int> engine_devices();
+std::vector<int> engine_devices(uint32_t mask);  // mask 0 = the dwpa_init() selection
 uint32_t engine_batch();
 
 int scan_create(int device, const char* const* lines, const size_t* lens, size_t nlines, int nc, int nc_mode,

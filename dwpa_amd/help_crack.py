@@ -7,18 +7,22 @@ expansions (:508, :575) with the same inputs, outputs and return codes:
               ``conf["rules"]`` ("" or "-S -r <file>", :445-447 / :931-933), ``conf["key_file"]``, the dictionary
               list (plain or .gz), ``conf["coptions"]`` (``-d 1,2`` selects devices like hashcat's ``-d``);
 * output   -- the ``-o`` key file in hashcat's m22000 outfile format, parsed unchanged by ``get_key`` (:804-879);
-* rc       -- hashcat semantics: 0 all cracked, 1 exhausted (drives the second pass at :930), -1 error.
+* rc       -- hashcat semantics: 0 all cracked, 1 exhausted (drives the second pass at :930); errors are
+              retried after ``sleepy()`` as the reference's loop does (:776-786), never returned.
 
 Usage from help_crack.py (the one-line change INTEGRATION.md shows)::
 
     from dwpa_amd.help_crack import run_cracker as _gpu_run_cracker
-    HelpCrack.run_cracker = lambda self, dictlist, disablestdout=False: _gpu_run_cracker(self.conf, dictlist)
+    HelpCrack.run_cracker = lambda self, dictlist, disablestdout=False: _gpu_run_cracker(
+        self.conf, dictlist, sleepy=self.sleepy, pprint=self.pprint)
 """
 from __future__ import annotations
 
 import gzip
 import os
 import shlex
+import sys
+import time
 
 from . import m22000 as M
 from . import _lib as L
@@ -48,13 +52,37 @@ def _parse_options(rules: str, coptions: str):
     return rules_file, devices
 
 
-def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR_CORRECTIONS) -> int:
-    """In-process equivalent of the hashcat command line at help_crack.py:773; returns its exit code."""
+def _sleepy(sec: int = 123) -> None:
+    """HelpCrack.sleepy (help_crack.py:80-87): wait for things to calm down before the next attempt."""
+    time.sleep(sec)
+
+
+def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR_CORRECTIONS, sleepy=None,
+                pprint=None, max_tries: int | None = None) -> int:
+    """In-process equivalent of the hashcat command line at help_crack.py:773 with the reference's retry loop
+    (:776-786): a failed attempt (library, GPU or I/O error -- hashcat's -1 / >= 2) is logged, followed by
+    ``sleepy()`` and retried, so only 0 (all cracked) or 1 (exhausted) ever reaches run(): returning -1 there
+    would skip the rules pass (:930) and let put_work report an unsearched work unit as searched.
+
+    ``sleepy``/``pprint`` are the HelpCrack methods when bound from help_crack.py.  ``max_tries`` (None = retry
+    forever, as the reference does) ends the loop with a DwpaError instead of a return value.  A missing hash
+    file raises FileNotFoundError (the reference would fail on an unbound ``rc``)."""
     if not os.path.exists(conf["hash_file"]):
-        return L.DWPA_RC_ERROR
+        raise FileNotFoundError(conf["hash_file"])
+    sleepy = sleepy or _sleepy
+    pprint = pprint or (lambda mess, code="HEADER": print(mess, file=sys.stderr))
     rules_file, mask = _parse_options(conf.get("rules", ""), conf.get("coptions", ""))
-    return M.crack_files(conf["hash_file"], list(dictlist), rules_file, nonce_error_corrections, conf["key_file"],
-                         device_mask=mask)
+    tries = 0
+    while True:
+        rc = M.crack_files(conf["hash_file"], list(dictlist), rules_file, nonce_error_corrections,
+                           conf["key_file"], device_mask=mask)
+        if rc in (L.DWPA_RC_CRACKED, L.DWPA_RC_EXHAUSTED):
+            return rc
+        tries += 1
+        pprint(f"libdwpa22000 crack_files failed with code {rc}", "FAIL")
+        if max_tries is not None and tries >= max_tries:
+            raise L.DwpaError(rc, f"crack_files failed {tries} times")
+        sleepy()
 
 
 def expand_rules(rules_file: str, source: str, out_gz: str, chunk: int = 1 << 16) -> int:

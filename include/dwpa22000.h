@@ -40,7 +40,9 @@ extern "C" {
 #define DWPA_E_IO (-14)        /* file could not be read or written                                            */
 #define DWPA_E_OVERFLOW (-15)  /* hit buffer overflow                                                          */
 #define DWPA_E_RULE (-16)      /* unsupported or malformed rule                                                */
-/* Every negative code maps to PHP False in the wrappers (check_key_m22000 returns False on all of them). */
+/* -1..-4 are check_key_m22000's own False returns (malformed line).  Codes <= -10 are device/runtime failures:
+ * the result is unknown, so wrappers must not turn them into False (put_work, common.php:902,919, would read
+ * "wrong PSK"); php/dwpa22000.php hands such jobs to the original PHP check or throws. */
 
 /* hashcat exit codes returned by dwpa_crack_files (help_crack.py:776-786,930 interpret them) */
 #define DWPA_RC_CRACKED 0      /* every hashline cracked                                                       */

@@ -5,15 +5,34 @@
  * check_key_m22000_gpu() is a drop-in for check_key_m22000() (web/common.php:157-307): same arguments, same
  * return value (False or [PSK, NC, 'BE'|'LE'|Null, PMK]).  check_keys_m22000_gpu_batch() takes many
  * [hashline, keys, pmk, nc] jobs at once (put_work's loop, common.php:900-925; rkg.php:126,147) so every
- * (ESSID, key) PMK is derived once on the GPU.  Every negative library code maps to False, as the PHP
- * function's own early returns do.  Needs hc_unhex() from common.php for the returned PSK.
+ * (ESSID, key) PMK is derived once on the GPU.  Needs hc_unhex() from common.php for the returned PSK.
  *
- * Not exercised in this repository's CI: the build image has no PHP interpreter (SURVEY.md §8c); the same
- * C entry points are exercised through ctypes by tests/test_gpu_parity.py.
+ * Library return code -> behaviour (pinned by tests/test_php_wrapper.py, which parses this file):
+ *   DWPA_HIT (1)                                      -> [PSK, NC, endian, PMK]
+ *   DWPA_MISS (0), parse codes -1..-4                 -> False, exactly as check_key_m22000's own early returns
+ *                                                        (common.php:160-164,276,306)
+ *   device / runtime codes <= -10 (NODEV, HIP, ARG,   -> never False: put_work (common.php:902,919) reads False
+ *   NOMEM, IO, OVERFLOW, RULE)                           as "this PSK is wrong" and would discard a genuine crack.
+ *                                                        The job goes to the original PHP check, kept under the
+ *                                                        name check_key_m22000_php (INTEGRATION.md section 2), or,
+ *                                                        if that is not defined, a Dwpa22000Error is thrown.
+ *   a caller $pmk that is not 32 bytes                 -> the original PHP check as well: PHP HMACs with the PMK's
+ *                                                        actual length (common.php:178-188), the ABI takes 32 bytes.
+ *
+ * Not exercised by a PHP interpreter here: the build image has none (SURVEY.md section 8c); the same C entry
+ * points are exercised through ctypes by tests/test_gpu_parity.py.
  */
+
+final class Dwpa22000Error extends RuntimeException
+{
+}
 
 final class Dwpa22000
 {
+    const HIT = 1;
+    const MISS = 0;
+    const FIRST_DEVICE_ERROR = -10;  /* DWPA_E_NODEV; every code <= this is a device/runtime failure */
+
     private static $ffi = null;
 
     public static function ffi()
@@ -31,6 +50,28 @@ CDEF;
             self::$ffi = FFI::cdef($cdef, $lib);
         }
         return self::$ffi;
+    }
+
+    /* rc <= -10: the library could not decide (no device, runtime error, ...) -- the answer is not "wrong key" */
+    public static function is_device_error($rc)
+    {
+        return $rc <= self::FIRST_DEVICE_ERROR;
+    }
+
+    /* the original PHP check_key_m22000 (renamed check_key_m22000_php), or an exception -- never False */
+    public static function fallback($rc, $hashline, $keys, $pmk, $nc)
+    {
+        if (function_exists('check_key_m22000_php')) {
+            return check_key_m22000_php($hashline, $keys, $pmk, $nc);
+        }
+        $msg = $rc === null ? 'caller PMK is not 32 bytes' : FFI::string(self::ffi()->dwpa_strerror($rc));
+        throw new Dwpa22000Error("libdwpa22000: $msg (rc $rc)");
+    }
+
+    /* a caller PMK the ABI can take: `if (!$pmk)` (common.php:178) means derive; otherwise exactly 32 bytes */
+    public static function pmk_ok($pmk)
+    {
+        return !$pmk || strlen((string) $pmk) == 32;
     }
 
     /* PHP array of keys -> [dwpa_bytes[], keep-alive buffers, values] */
@@ -60,13 +101,14 @@ CDEF;
         return [$arr, $keep, $vals];
     }
 
+    /* 32-byte caller PMK -> uint8_t[32], or null (derive); callers check pmk_ok() first */
     public static function pmk($pmk)
     {
         if (!$pmk) {                                 // common.php:178 -- `if (!$pmk)`
             return null;
         }
         $b = self::ffi()->new('uint8_t[32]');
-        FFI::memcpy($b, substr(str_pad((string) $pmk, 32, "\0"), 0, 32), 32);
+        FFI::memcpy($b, (string) $pmk, 32);
         return $b;
     }
 
@@ -87,52 +129,81 @@ CDEF;
 
 function check_key_m22000_gpu($hashline, $keys, $pmk = False, $nc = 128)
 {
+    if (!Dwpa22000::pmk_ok($pmk)) {
+        return Dwpa22000::fallback(null, $hashline, $keys, $pmk, $nc);
+    }
     $ffi = Dwpa22000::ffi();
     [$arr, $keep, $vals] = Dwpa22000::keys($keys);
     $pm = Dwpa22000::pmk($pmk);
     $res = $ffi->new('dwpa_result');
     $rc = $ffi->dwpa_check_m22000($hashline, strlen($hashline), $arr, count($vals),
                                   $pm === null ? null : FFI::addr($pm[0]), (int) $nc, FFI::addr($res));
-    if ($rc != 1) {
-        return False;
+    if ($rc == Dwpa22000::HIT) {
+        return Dwpa22000::result($vals, $res);
     }
-    return Dwpa22000::result($vals, $res);
+    if (Dwpa22000::is_device_error($rc)) {
+        return Dwpa22000::fallback($rc, $hashline, $keys, $pmk, $nc);
+    }
+    return False;                                    // DWPA_MISS or a parse code (-1..-4)
 }
 
 /* $jobs: list of [hashline, keys, pmk (False for none), nc]; returns a list of check_key_m22000 results */
 function check_keys_m22000_gpu_batch($jobs)
 {
-    $ffi = Dwpa22000::ffi();
+    $jobs = array_values($jobs);
     $n = count($jobs);
     if ($n == 0) {
         return [];
     }
-    $cj = $ffi->new("dwpa_job[$n]");
-    $keep = [];
-    $vals = [];
-    foreach (array_values($jobs) as $i => $job) {
-        [$line, $keys, $pmk, $nc] = $job + [null, [], False, 128];
-        [$arr, $k, $v] = Dwpa22000::keys($keys);
-        $pm = Dwpa22000::pmk($pmk);
-        $lb = $ffi->new('char[' . max(1, strlen($line)) . ']');
-        FFI::memcpy($lb, $line, strlen($line));
-        $keep[] = [$arr, $k, $pm, $lb];
-        $vals[] = $v;
-        $cj[$i]->line = FFI::addr($lb[0]);
-        $cj[$i]->line_len = strlen($line);
-        $cj[$i]->keys = FFI::addr($arr[0]);
-        $cj[$i]->nkeys = count($v);
-        $cj[$i]->pmk = $pm === null ? null : FFI::addr($pm[0]);
-        $cj[$i]->nc = (int) $nc;
+    $ffi = Dwpa22000::ffi();
+    $args = [];
+    $gpu = [];                                       // indices of the jobs the library checks
+    foreach ($jobs as $i => $job) {
+        $args[$i] = $job + [null, [], False, 128];
+        if (Dwpa22000::pmk_ok($args[$i][2])) {
+            $gpu[] = $i;
+        }
     }
-    $out = $ffi->new("dwpa_result[$n]");
-    $rcs = $ffi->new("int[$n]");
-    if ($ffi->dwpa_check_batch($cj, $n, $out, $rcs) < 0) {
-        return array_fill(0, $n, False);
+    $res = array_fill(0, $n, False);
+    $m = count($gpu);
+    $rc = 0;
+    if ($m) {
+        $cj = $ffi->new("dwpa_job[$m]");
+        $keep = [];
+        $vals = [];
+        foreach ($gpu as $s => $i) {
+            [$line, $keys, $pmk, $nc] = $args[$i];
+            [$arr, $k, $v] = Dwpa22000::keys($keys);
+            $pm = Dwpa22000::pmk($pmk);
+            $lb = $ffi->new('char[' . max(1, strlen($line)) . ']');
+            FFI::memcpy($lb, $line, strlen($line));
+            $keep[] = [$arr, $k, $pm, $lb];
+            $vals[$s] = $v;
+            $cj[$s]->line = FFI::addr($lb[0]);
+            $cj[$s]->line_len = strlen($line);
+            $cj[$s]->keys = FFI::addr($arr[0]);
+            $cj[$s]->nkeys = count($v);
+            $cj[$s]->pmk = $pm === null ? null : FFI::addr($pm[0]);
+            $cj[$s]->nc = (int) $nc;
+        }
+        $out = $ffi->new("dwpa_result[$m]");
+        $rcs = $ffi->new("int[$m]");
+        $rc = $ffi->dwpa_check_batch($cj, $m, $out, $rcs);
+        foreach ($gpu as $s => $i) {
+            // the whole batch failed (rc < 0), or this job did: the PHP check decides, never a silent False
+            $jrc = $rc < 0 ? $rc : $rcs[$s];
+            if ($jrc == Dwpa22000::HIT) {
+                $res[$i] = Dwpa22000::result($vals[$s], $out[$s]);
+            } elseif ($rc < 0 || Dwpa22000::is_device_error($jrc)) {
+                [$line, $keys, $pmk, $nc] = $args[$i];
+                $res[$i] = Dwpa22000::fallback($jrc, $line, $keys, $pmk, $nc);
+            }                                        // else DWPA_MISS / parse code: False
+        }
     }
-    $res = [];
-    for ($i = 0; $i < $n; $i++) {
-        $res[] = $rcs[$i] == 1 ? Dwpa22000::result($vals[$i], $out[$i]) : False;
+    foreach ($args as $i => $a) {
+        if (!Dwpa22000::pmk_ok($a[2])) {
+            $res[$i] = Dwpa22000::fallback(null, $a[0], $a[1], $a[2], $a[3]);
+        }
     }
     return $res;
 }

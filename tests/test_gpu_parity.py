@@ -339,7 +339,8 @@ def test_help_crack_two_pass_flow(tmp_path):
     assert run_cracker(conf, [str(d)]) == 0
     assert _get_key(conf["key_file"]) == {ap.hex(): direct.hex(), ap2.hex(): ruled.hex()}
     conf["hash_file"] = str(tmp_path / "missing.hash")
-    assert run_cracker(conf, [str(d)]) == -1
+    with pytest.raises(FileNotFoundError):
+        run_cracker(conf, [str(d)])
 
 
 def test_help_crack_expand_rules_file(tmp_path):
@@ -389,6 +390,47 @@ def test_crack_files_several_dictionaries(tmp_path):
     assert dwpa_amd.crack_files(str(hf), files, None, 8, str(out), batch=1 << 14) == 0
     recs = out.read_bytes().strip().split(b"\n")
     assert sorted(r.rsplit(b":", 1)[1] for r in recs) == sorted(psks)
+
+
+def test_crack_files_several_shard_workers(tmp_path, capfd, monkeypatch):
+    """The multi-device client path (hashcat uses every GPU, help_crack.py:773) rehearsed on one GPU: two shard
+    workers on device 0 (DWPA_CRACK_SHARDS_PER_DEVICE=2) pull dictionary items from one queue, each with its own
+    scan, stager and streams.  Hits are planted in several items (so both workers find some), one PSK appears in
+    two items (its line must be written exactly once, then retired everywhere), and a line whose PMKID is shorter
+    than 16 bytes (never matches; hashcat would not load it) must not keep rc at 1."""
+    monkeypatch.setenv("DWPA_CRACK_SHARDS_PER_DEVICE", "2")
+    monkeypatch.setenv("DWPA_TRACE", "1")
+    rng = random.Random(51)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    alnum = b"abcdefghijklmnopqrstuvwxyz0123456789"
+    n = 600_000
+    words = [b"w%07d" % i + bytes(rng.choice(alnum) for _ in range(3)) for i in range(n)]
+    where = [100, 20_000, 60_000, 200_000, 500_000, n - 1]
+    lines, psks = [], []
+    for k, i in enumerate(where):
+        psks.append(words[i])
+        a = rng.randbytes(6)
+        lines.append(S.pmkid_line(words[i], essid, a, sta) if k % 2 else
+                     S.eapol_line(words[i], essid, a, sta, an, sn, 2, k - 3, "LE", rng=rng))
+    words[30_000] = words[100]  # the first line's PSK again, in a later item
+    short = S.pmkid_line(b"never", essid, ap, sta).split(b"*")
+    short[2] = short[2][:16]    # 8-byte PMKID: strncmp over 16 bytes never matches (common.php:186)
+    lines.append(b"*".join(short))
+    hf = tmp_path / "h.hash"
+    hf.write_bytes(b"\n".join(lines) + b"\n")
+    d = tmp_path / "d.txt.gz"
+    with gzip.open(d, "wb", compresslevel=1) as f:
+        f.write(b"\n".join(words) + b"\n")
+    out = tmp_path / "o.key"
+    assert dwpa_amd.crack_files(str(hf), [str(d)], None, 8, str(out), batch=1 << 14) == 0
+    recs = out.read_bytes().strip().split(b"\n")
+    assert len(recs) == len(where)
+    assert sorted(r.rsplit(b":", 1)[1] for r in recs) == sorted(psks)
+    assert len({r.split(b":")[1] for r in recs}) == len(where)  # one record per line (MAC_AP differs per line)
+    err = capfd.readouterr().err
+    workers = [l for l in err.splitlines() if "crack worker" in l]
+    assert len(workers) == 2, err[-2000:]
+    assert all(int(l.split(": ")[1].split(" items")[0]) > 0 for l in workers), workers
 
 
 @pytest.mark.skipif(os.environ.get("DWPA_PBKDF2_ISSUE") == "1", reason="already the forced issue-pass run")

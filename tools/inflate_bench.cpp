@@ -1,0 +1,67 @@
+// inflate_bench -- how fast the dwpa_crack_files dictionary reader (dwpa_amd/csrc/dict_reader.hpp, the exact
+// code the library runs) turns gzip wordlists into candidate chunks on this host, i.e. how many GPUs one gz
+// stream can feed in the rules-less first pass (help_crack.py:929; a GPU scans ~4.9 M words/s at C2).
+//
+//   inflate_bench FILE.gz [FILE2.gz ...]
+//
+// Prints one JSON line: raw gzread throughput of the first file (inflate only), DictReader words/s on the first
+// file (inflate + line cutting + $HEX[] decoding: one stream, one core), and ChunkSource words/s over all files
+// (up to 4 reader threads, as crack_files runs them).
+#include <stdio.h>
+#include <zlib.h>
+
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "dict_reader.hpp"
+
+using clk = std::chrono::steady_clock;
+
+static double since(clk::time_point t) { return std::chrono::duration<double>(clk::now() - t).count(); }
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s FILE.gz [FILE2.gz ...]\n", argv[0]);
+        return 2;
+    }
+    std::vector<std::string> paths(argv + 1, argv + argc);
+    // 1. inflate only
+    gzFile gz = gzopen(paths[0].c_str(), "rb");
+    if (!gz) return 1;
+    gzbuffer(gz, 1 << 20);
+    std::vector<char> buf(1 << 20);
+    size_t raw = 0;
+    auto t = clk::now();
+    for (int r; (r = gzread(gz, buf.data(), (unsigned)buf.size())) > 0;) raw += (size_t)r;
+    const double t_inflate = since(t);
+    gzclose(gz);
+    // 2. one DictReader stream (what one dictionary costs one reader thread)
+    size_t words1 = 0;
+    {
+        dwpa::DictReader rd({paths[0]});
+        dwpa::Chunk c;
+        bool err = false;
+        t = clk::now();
+        while (rd.next(c, 1 << 22, (size_t)1 << 31, err)) words1 += c.words();
+        if (err) return 1;
+    }
+    const double t_reader = since(t);
+    // 3. ChunkSource over every file (crack_files' reader threads)
+    size_t words_all = 0;
+    t = clk::now();
+    {
+        dwpa::ChunkSource src(paths, 1 << 20, 1 << 24);
+        dwpa::Chunk c;
+        bool err = false;
+        while (src.next(c, err)) words_all += c.words();
+        if (err) return 1;
+    }
+    const double t_all = since(t);
+    printf("{\"files\": %zu, \"raw_bytes\": %zu, \"inflate_MBps\": %.1f, \"words\": %zu, "
+           "\"reader_words_per_s\": %.0f, \"reader_MBps\": %.1f, \"chunk_source_threads\": %zu, "
+           "\"chunk_source_words_per_s\": %.0f}\n",
+           paths.size(), raw, raw / t_inflate / 1e6, words1, words1 / t_reader, raw / t_reader / 1e6,
+           std::min<size_t>(paths.size(), 4), words_all / t_all);
+    return 0;
+}
