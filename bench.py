@@ -1,14 +1,16 @@
 """bench.py -- PMK/s (PBKDF2-HMAC-SHA1 x4096) of the m22000 engine on MI355X, BASELINE.json configs[1] (C2).
 
 Workload (per GPU): one ESSID, one EAPOL keyver-2 hashline (message_pair 0x80, planted nonce correction +3 LE,
-PHP nonce window nc=8 -> 21 attempts), a 100M-word synthetic dictionary resident in HBM (uint64 offsets +
-bytes, lengths geometric around 10 clipped to [8, 63]; the true PSK is word 99,999,000).  A step = one batch
+hashcat nonce mode --nonce-error-corrections=8 -> 33 attempts, as help_crack.py:773 runs it), a 100M-word
+synthetic dictionary resident in HBM (uint64 offsets + bytes, lengths geometric around 10 clipped to [8, 63];
+the true PSK is word 99,999,000).  A step = one batch
 of the dictionary through the hot path: candidates -> HMAC midstates -> PBKDF2 -> verify.  Rank r of N scans
 batches r, r+N, ... (static keyspace shards, no collective on the data path): weak scaling.
 
 The JSON line carries the PBKDF2 kernel's roofline (integer VALU bound) from HIP events recorded around each
 launch on the stream it runs on, and the CPU baseline (the OpenSSL restatement of check_key_m22000 from
-oracle/, timed on this host's cores on a bounded sample of the same workload).
+oracle/, timed on this host's cores on a bounded sample of the same workload: 1 thread = one PHP request, and
+the box's CPU share).
 """
 from __future__ import annotations
 
@@ -24,24 +26,34 @@ sys.path.insert(0, ROOT)
 METRIC = "PMK/s (PBKDF2-HMAC-SHA1 x4096) per GPU and per 8×MI355X node, m22000"
 DICT_WORDS = 100_000_000
 PLANT_INDEX = 99_999_000
-NC = 8
+NC = 8          # nonce-error-corrections of the client (help_crack.py:773); the CPU baseline's PHP window
+NC_MODE = 1     # DWPA_NC_HASHCAT: N+0 then +-1..+-8 in both endians = 33 attempts per candidate
 # Roofline.  Work unit: 16,388 SHA-1 compressions per PMK (north_star).  Bound: integer
 # VALU issue.  Measured on gfx950 (tools/valu_peak, profiles/r01/valu_issue_costs.json): xor/bitop3/add_u32 take
 # 2 SIMD cycles per wave64 instruction, alignbit (rotate) and add3 take 4, so the cheapest HMAC inner-loop
 # compression costs C_MIN = 1878.5 SIMD-cycles per wave (64 lanes; derivation in DESIGN.md section 4).
 COMPRESSIONS_PER_PMK = 16388
-C_MIN_CYCLES = 1878.5
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
+from tools.cmin import c_min  # noqa: E402  (the C_min model; tools/regen_peak.sh re-measures its inputs)
+C_MIN_CYCLES = c_min()  # 1878.5 at full rate 2 / half rate 4 SIMD-cycles per wave instruction
 PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
-# HBM traffic of k_pbkdf2 per PMK, from the PMC passes of tools/profile_traffic.sh over this bench command
-# (profiles/r01/traffic/traffic.json, per 4,194,304-PMK launch): FETCH_SIZE 167,954,944 B, doubled as
-# MI355X_MICROARCH.md "HBM [CDNA4]" prescribes = 80 B/PMK (each of the two output-block lanes reads the 40-byte key
-# midstate once), plus WRITE_SIZE 134,217,728 B = 32 B/PMK.  Algorithmic bytes are the same 80 + 32 = 112 B/PMK.
-# PMC counters cannot be read inside a timed run, so the bench scales the measured per-PMK figure to its launches.
-TRAFFIC_BYTES_PER_PMK = (2 * 167954944 + 134217728) / 4194304
+# HBM traffic per PMK of the kernel each workload's roofline names, from the PMC passes of tools/profile_traffic.sh
+# over that workload's bench command (FETCH_SIZE doubled as MI355X_MICROARCH.md "HBM [CDNA4]" prescribes, plus
+# WRITE_SIZE; per-launch medians divided by the PMKs of the launch).  PMC counters cannot be read inside a timed
+# run, so the bench scales the measured per-PMK figure to its launches.
+#   c2/c4: k_pbkdf2_gfx950, profiles/r01/traffic (4,194,304-PMK launch): FETCH 167,954,944 B x 2 = 80 B/PMK (each of
+#          the two output-block lanes reads the 40-byte key midstate once) + WRITE 134,217,728 B = 32 B/PMK
+#   c3:    k_pbkdf2_gfx950_mg + k_verify per dwpa_scan_run, profiles/r02/traffic_c3 (TRAFFIC_C3 below)
+TRAFFIC_BYTES_PER_PMK = {"c2": (2 * 167954944 + 134217728) / 4194304, "c4": (2 * 167954944 + 134217728) / 4194304}
+TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950, profiles/r01/traffic",
+                  "c4": "k_pbkdf2_gfx950 per PMK as measured on c2, profiles/r01/traffic"}
 ALGO_BYTES_PER_PMK = 80 + 32
-# Nominal all-ops-full-rate view (128 int32 lane-ops/clk/CU, 576.5 ops/compression): reported, not attainable.
-OPS_PER_COMPRESSION = 576.5
+# Guide view (MI355X_MICROARCH.md: 4 SIMD-32 per CU, one VALU per 2 cycles = 128 int32 lane-ops/clk/CU at 2.4 GHz,
+# every op full rate).  Reported beside the issue-cost roofline, with SURVEY.md 8(d)'s ideal 617 ops per compression
+# and with the 575.5 VALU the kernel issues per compression (4,714,742 per wave / 8,192 compressions, PMC).  Not
+# attainable on gfx950, where v_alignbit/v_add3/v_bfi issue at half rate (profiles/r01/valu_issue_costs.json).
+SURVEY_OPS_PER_COMPRESSION = 617
+ISSUED_OPS_PER_COMPRESSION = 575.5
 PEAK_LANE_OPS = 256 * 128 * CLOCK_HZ
 
 
@@ -54,6 +66,8 @@ def parse():
     ap.add_argument("--dict-words", type=int, default=DICT_WORDS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--peak-costs", default=None,
+                    help="price the roofline from a fresh tools/bin/valu_peak measurement (tools/regen_peak.sh output)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="batches in flight (c2/c3/c4), each on its own scan working set and HIP stream.  Measured "
                          "A/B (profiles/r01/pipeline/): 2 gains 0.2 %% -- the next batch's PBKDF2 waves hold the "
@@ -100,11 +114,11 @@ def build_c2(args, local, S, Scan, Dictionary):
     w.dict = Dictionary(w.off, w.data, device=local)
     w.B = (args.batch + 63) & ~63
     w.nbatches = (n + w.B - 1) // w.B
-    w.scans = [Scan([w.line], device=local, nc=NC, nc_mode=0, batch=w.B) for _ in range(args.pipeline)]
+    w.scans = [Scan([w.line], device=local, nc=NC, nc_mode=NC_MODE, batch=w.B) for _ in range(args.pipeline)]
     w.groups = 1
     w.name = "C2"
     w.description = ("C2: one ESSID, one EAPOL keyver-2 line (mp 0x80, planted NC +3 LE), 100M-word synthetic "
-                     "dictionary resident in HBM, PHP nonce window nc=8 (21 attempts)")
+                     "dictionary resident in HBM, hashcat nonce mode --nonce-error-corrections=8 (33 attempts)")
     w.extra = {"dict_words": n}
 
     def load(i, hs, sc):
@@ -116,7 +130,14 @@ def build_c2(args, local, S, Scan, Dictionary):
     def check(hits):
         return any(h["cand"] == w.plant and h["nc"] == 3 and h["endian"] == "LE" and h["pmk"] == S.pmk(w.psk, w.essid)
                    for h in hits)
+
+    def cpu_keys(m):  # the m dictionary words ending at the planted PSK
+        lo = w.plant - m + 1
+        o = w.off[lo:w.plant + 2].astype("int64")
+        raw = w.data[o[0]:o[-1]].tobytes()
+        return [raw[o[i] - o[0]:o[i + 1] - o[0]] for i in range(m)]
     w.load, w.check, w.plant_batch = load, check, w.plant // w.B
+    w.cpu_line, w.cpu_keys, w.cpu_what = w.line, cpu_keys, "dictionary words"
     return w
 
 
@@ -146,6 +167,8 @@ def build_c4(args, local, S, Scan, Dictionary):
     def check(hits):
         return any(h["cand"] == w.plant and h["pmk"] == S.pmk(b"%08d" % w.plant, w.essid) for h in hits)
     w.load, w.check, w.plant_batch = load, check, w.plant // w.B
+    w.cpu_line, w.cpu_keys = w.line, lambda m: [b"%08d" % v for v in range(w.plant - m + 1, w.plant + 1)]
+    w.cpu_what = "8-digit candidates"
     return w
 
 
@@ -182,7 +205,7 @@ def build_c3(args, local, S, Scan, Dictionary):
     # multi-group PBKDF2 launches (dwpa_scan_run).  Rule filtering makes the per-step count data-dependent, so the
     # last wave round of each launch is partial; 4x the C2 step keeps that tail near 2 %.
     w.B = max(len(rules) + 63, 4 * args.batch // max(1, args.essids)) // 64 * 64
-    w.scans = [Scan(lines, device=local, nc=NC, nc_mode=0, batch=w.B) for _ in range(args.pipeline)]
+    w.scans = [Scan(lines, device=local, nc=NC, nc_mode=NC_MODE, batch=w.B) for _ in range(args.pipeline)]
     w.nrules = [sc.set_rules("\n".join(rules)) for sc in w.scans][0]
     w.words_per_step = max(1, w.B // w.nrules)
     w.nbatches = (len(base) + w.words_per_step - 1) // w.words_per_step
@@ -201,13 +224,33 @@ def build_c3(args, local, S, Scan, Dictionary):
     def check(hits):
         return all(any(h["line"] == li and h["pmk"] == S.pmk(psk, essid) for h in hits)
                    for li, cand, essid, psk in w.plants)
+
+    def cpu_keys(m):  # the m rule candidates (word-major, 8..63 only) ending at the first planted one
+        from oracle import rules as R
+        _, cand, _, psk = w.plants[0]
+        wi, ri = divmod(cand, w.nrules)
+        parsed = [R.parse(r) for r in rules]
+        out = [c for c in (R.apply(parsed[r], base[wi]) for r in range(ri + 1)) if c and 8 <= len(c) <= 63]
+        j = wi - 1
+        while len(out) < m and j >= 0:
+            row = [c for c in (R.apply(pr, base[j]) for pr in parsed) if c and 8 <= len(c) <= 63]
+            out = row + out
+            j -= 1
+        return out[-m:]
     w.load, w.check = load, check
+    w.cpu_line, w.cpu_keys = (lines[w.plants[0][0]], cpu_keys) if w.plants else (None, None)
+    w.cpu_what = "rule candidates (word-major, 8..63) of one ESSID's line"
     w.plant_batch = (w.plants[0][1] // w.nrules) // w.words_per_step if w.plants else 0
     return w
 
 
 def main():
     args = parse()
+    if args.peak_costs:
+        global C_MIN_CYCLES, PEAK_COMPRESSIONS
+        from tools.cmin import from_costs
+        C_MIN_CYCLES = from_costs(args.peak_costs)["c_min_model"]
+        PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -299,11 +342,12 @@ def main():
     pmk_per_launch = sum(per_launch) / len(per_launch)
     kernel_pmk_s = sum(per_launch) / (sum(kms) * 1e-3)
     achieved = kernel_pmk_s * COMPRESSIONS_PER_PMK
+    traffic_pmk = TRAFFIC_BYTES_PER_PMK.get(args.workload)
     if rank == 0:
         value = total / elapsed
         cpu = None
-        if not args.no_cpu_baseline and args.workload == "c2" and world == 1:
-            cpu = cpu_baseline(w.line, w.data, w.off, w.plant, args.cpu_seconds)
+        if not args.no_cpu_baseline and world == 1 and w.cpu_keys:
+            cpu = cpu_baseline(w.cpu_line, w.cpu_keys, args.cpu_seconds, w.cpu_what)
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -326,17 +370,27 @@ def main():
                 "peak": round(PEAK_COMPRESSIONS / 1e9, 3),
                 "unit": "G SHA-1 compressions/s",
                 "frac": round(achieved / PEAK_COMPRESSIONS, 4),
-                "traffic": round(TRAFFIC_BYTES_PER_PMK * pmk_per_launch),
-                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/r01/traffic)",
+                "traffic": round(traffic_pmk * pmk_per_launch) if traffic_pmk else None,
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE of this workload, "
+                                + TRAFFIC_SOURCE.get(args.workload, "not measured") + ")",
                 "algorithmic_bytes": ALGO_BYTES_PER_PMK * pmk_per_launch,
-                "hbm_gbs": round(TRAFFIC_BYTES_PER_PMK * pmk_per_launch / (kernel_ms * 1e-3) / 1e9, 3),
+                "hbm_gbs": round(traffic_pmk * pmk_per_launch / (kernel_ms * 1e-3) / 1e9, 3) if traffic_pmk else None,
                 "kernel_ms": round(kernel_ms, 3),
                 "pmk_per_launch": pmk_per_launch,
                 "kernel_pmk_per_s": round(kernel_pmk_s, 1),
                 "roofline_pmk_per_s": round(PEAK_COMPRESSIONS / COMPRESSIONS_PER_PMK, 1),
                 "peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x 64 lanes / {C_MIN_CYCLES} SIMD-cycles per "
-                              "compression (measured gfx950 issue costs)",
-                "frac_nominal_ops": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * OPS_PER_COMPRESSION / PEAK_LANE_OPS, 4),
+                              "compression (measured gfx950 issue costs, tools/cmin.py; "
+                              + (args.peak_costs or "profiles/r01/valu_issue_costs.json") + ")",
+                # the same kernel against the guide's all-full-rate VALU peak (256 CU x 128 lane-ops/clk x 2.4 GHz)
+                "frac_guide_valu_peak": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * SURVEY_OPS_PER_COMPRESSION
+                                              / PEAK_LANE_OPS, 4),
+                "frac_guide_valu_peak_basis": f"{SURVEY_OPS_PER_COMPRESSION} ops per compression (SURVEY.md 8(d) "
+                                              "ideal count) / 78.64 T int32 lane-ops/s",
+                "frac_nominal_ops": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * ISSUED_OPS_PER_COMPRESSION
+                                          / PEAK_LANE_OPS, 4),
+                "frac_nominal_ops_basis": f"{ISSUED_OPS_PER_COMPRESSION} VALU issued per compression (PMC) / "
+                                          "78.64 T int32 lane-ops/s",
             },
             "cpu_baseline": cpu,
             "hits_verified": verified,
@@ -397,7 +451,19 @@ def main_ffi(args, world, rank, local):
     if args.workload == "c1":
         verified = bool(got[0]) and got[0][0] == psk and got[0][3] == S.pmk(psk, bytes.fromhex(line.split(b"*")[5].decode()))
     else:
-        verified = sum(1 for g in got if g) >= 0.85 * len(jobs)
+        # every hit's exact [PSK, NC, endian, PMK] tuple, re-derived by the oracle from the winning key alone
+        # (the first-key-in-order rule and the misses are checked by tests/test_gpu_configs.py)
+        from concurrent.futures import ThreadPoolExecutor
+        from oracle import oracle as O
+
+        def hit_alone(i):
+            line, keys, pmk, nc = jobs[i]
+            k = next(x for x in keys if x is not None and O.hc_unhex(x) == got[i][0])
+            return O.c_check_key_m22000(line, [k], pmk if keys[0] == k else False, nc) == got[i]
+        hit_jobs = [i for i, g in enumerate(got) if g]
+        with ThreadPoolExecutor(host_cpu()["threads_all"]) as ex:
+            exact = sum(ex.map(hit_alone, hit_jobs))
+        verified = exact == len(hit_jobs) and len(hit_jobs) >= 0.85 * len(jobs)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -409,7 +475,9 @@ def main_ffi(args, world, rank, local):
             "config": {"workload": desc, "jobs": len(jobs), "keys_per_step": batch.nkeys,
                        "parallelism": f"replicas x{world}"},
             "roofline": None, "cpu_baseline": cpu, "hits_verified": verified,
-            "hits": sum(1 for g in got if g)}), flush=True)
+            "hits": sum(1 for g in got if g),
+            "hits_checked": "every hit's [PSK, NC, endian, PMK] re-derived by the CPU oracle" if args.workload == "c5"
+                            else "the planted PSK and its PMK"}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -454,6 +522,14 @@ def main_files(args, world, rank, local):
             f.write(text[o:o + step].tobytes())
     gz_s = time.perf_counter() - t0
     gz_bytes = os.path.getsize(dpath)
+    reader = None
+    tool = os.path.join(ROOT, "tools", "bin", "inflate_bench")
+    if rank == 0 and os.path.exists(tool):
+        # crack_files' own dictionary reader on this host (dict_reader.hpp): how many GPUs one gz stream feeds
+        import subprocess
+        r = subprocess.run([tool, dpath], capture_output=True, text=True, timeout=300)
+        if r.returncode == 0:
+            reader = json.loads(r.stdout)
     del text
     with open(hpath, "wb") as f:
         f.write(line + b"\n")
@@ -488,7 +564,7 @@ def main_files(args, world, rank, local):
                        "dict_words": n, "gz_bytes": gz_bytes, "gz_write_s": round(gz_s, 2),
                        "words_scanned_per_pass": words, "batch": args.batch,
                        "parallelism": f"replicas x{world}"},
-            "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked)}), flush=True)
+            "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked), "reader": reader}), flush=True)
     for x in (dpath, hpath, opath):
         if os.path.exists(x):
             os.remove(x)
@@ -505,7 +581,8 @@ def cpu_baseline_jobs(jobs, seconds):
     parallel on up to 16 host threads, over a bounded prefix of the job list."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    hc = host_cpu()
+    threads = hc["threads_all"]
     if len(jobs) == 1:
         line, keys, pmk, nc = jobs[0]
         probe = keys[-threads * 32:]
@@ -520,11 +597,12 @@ def cpu_baseline_jobs(jobs, seconds):
         t1 = time.perf_counter()
         O.c_check_many(line, one, nc, 1)
         dt1 = time.perf_counter() - t1
-        return {"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
-                "sample": f"last {len(sample)} keys (ending at the true PSK), one check per key, {dt:.1f} s",
-                "found_planted": idx == len(sample) - 1,
-                "one_php_request": {"value": round(len(one) / dt1, 1), "cores": 1,
-                                    "sample": f"last {len(one)} keys on one thread, {dt1:.1f} s"}}
+        return dict({"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+                     "sample": f"last {len(sample)} keys (ending at the true PSK), one check per key, {dt:.1f} s",
+                     "found_planted": idx == len(sample) - 1,
+                     "one_thread": {"value": round(len(one) / dt1, 1), "unit": "PMK/s", "cores": 1,
+                                    "sample": f"last {len(one)} keys on one thread (one PHP request), {dt1:.1f} s"}},
+                    **hc)
     done, nkeys = 0, 0
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
@@ -534,35 +612,65 @@ def cpu_baseline_jobs(jobs, seconds):
             done += len(chunk)
             nkeys += sum(len(j[1]) for j in chunk)
     dt = time.perf_counter() - t0
-    return {"value": round(nkeys / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
-            "sample": f"first {done} jobs ({nkeys} keys), check_key_m22000 per job, {dt:.1f} s"}
+    # one PHP request: the jobs one after another on one thread
+    done1, nkeys1 = 0, 0
+    t1 = time.perf_counter()
+    while done1 < len(jobs) and time.perf_counter() - t1 < seconds / 3:
+        O.c_check_key_m22000(*jobs[done1])
+        nkeys1 += len(jobs[done1][1])
+        done1 += 1
+    dt1 = time.perf_counter() - t1
+    return dict({"value": round(nkeys / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+                 "sample": f"first {done} jobs ({nkeys} keys), check_key_m22000 per job on {threads} threads, {dt:.1f} s",
+                 "one_thread": {"value": round(nkeys1 / dt1, 1), "unit": "PMK/s", "cores": 1,
+                                "sample": f"first {done1} jobs ({nkeys1} keys) on 1 thread (one PHP request), "
+                                          f"{dt1:.1f} s"}},
+                **hc)
 
 
-def cpu_baseline(line, data, off, plant, seconds):
-    """The PHP CPU path: check_key_m22000(line, [word]) per word (one PHP request per key, as put_work does,
-    common.php:902), restated in C on OpenSSL (oracle/), on this host's cores; bounded sample ending at the
-    planted PSK so the sample must also find it."""
+def host_cpu():
+    """CPU model and counts of the host the baseline runs on.  threads_all = min(16, affinity): a GPU box gives one
+    GPU a 16-core share, and its nproc reports the whole machine."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), model)
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "threads_all": max(1, min(16, aff))}
+
+
+def cpu_baseline(line, keys_fn, seconds, what):
+    """The PHP CPU path: check_key_m22000(line, [key]) once per key (one PHP request per key, as put_work does,
+    common.php:902), restated in C on OpenSSL (oracle/; PKCS5_PBKDF2_HMAC is the call openssl_pbkdf2 makes,
+    common.php:178-180,246-248).  Timed on the box's CPU share (threads_all) and on 1 thread (one PHP request),
+    over bounded samples of the workload's own candidates that end at the planted PSK, which both runs must find.
+    PHP nonce window nc=8 (21 attempts per EAPOL key)."""
     from oracle import oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-
-    def words(lo, hi):
-        o = off[lo:hi + 1].astype("int64")
-        raw = data[o[0]:o[-1]].tobytes()
-        return [raw[o[i] - o[0]:o[i + 1] - o[0]] for i in range(hi - lo)]
-
-    probe = words(plant - 64 * threads + 1, plant + 1)
+    hc = host_cpu()
+    threads = hc["threads_all"]
+    probe = keys_fn(96 * threads)
+    O.c_check_many(line, probe[:threads], NC, threads)  # loads the oracle library and starts its threads
     t0 = time.perf_counter()
     O.c_check_many(line, probe, NC, threads)
     rate = len(probe) / (time.perf_counter() - t0)
     m = int(max(len(probe), min(400_000, rate * seconds)))
-    sample = words(plant - m + 1, plant + 1)
+    sample = keys_fn(m)
     t0 = time.perf_counter()
-    idx, res = O.c_check_many(line, sample, NC, threads)
+    idx, _ = O.c_check_many(line, sample, NC, threads)
     dt = time.perf_counter() - t0
-    return {"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
-            "sample": f"{len(sample)} dictionary words ending at the planted PSK, check_key_m22000 per word "
-                      f"(OpenSSL PKCS5_PBKDF2_HMAC + 21 NC attempts), {dt:.1f} s",
-            "found_planted": idx == len(sample) - 1}
+    one = keys_fn(int(max(16, min(m, rate / threads * seconds / 3))))
+    t1 = time.perf_counter()
+    idx1, _ = O.c_check_many(line, one, NC, 1)
+    dt1 = time.perf_counter() - t1
+    return dict({"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+                 "sample": f"{len(sample)} {what} ending at the planted PSK, check_key_m22000(line, [key], False, "
+                           f"{NC}) per key on {threads} threads, {dt:.1f} s",
+                 "found_planted": idx == len(sample) - 1 and idx1 == len(one) - 1,
+                 "one_thread": {"value": round(len(one) / dt1, 1), "unit": "PMK/s", "cores": 1,
+                                "sample": f"the last {len(one)} of them on 1 thread (one PHP request), {dt1:.1f} s"}},
+                **hc)
 
 
 if __name__ == "__main__":
