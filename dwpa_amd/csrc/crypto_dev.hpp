@@ -226,6 +226,28 @@ __device__ __forceinline__ void sha1_84(const Sha1Mid& M, const uint32_t in[5], 
     out[0] = M.h0 + a; out[1] = M.h1 + b; out[2] = M.h2 + c; out[3] = M.h3 + d; out[4] = M.h4 + e;
 }
 
+// Compression of a wave-uniform message block whose schedule the host has expanded: kw[t] = K_t + W_t for t < 80
+// (tables.hpp "KW blocks").  kw is read with scalar loads, so a round costs rotl5 + f + 3 adds + rotl30 and the
+// 64-word schedule (64 rotl1 + 128 xor per compression) is gone -- about a third of the generic compression.
+__device__ __forceinline__ void sha1_compress_kw(uint32_t st[5], const uint32_t* __restrict__ kw) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
+#define DWPA_SHA1_KW(T)                                                                                     \
+    {                                                                                                       \
+        const uint32_t t = rotl(a, 5) + sha1_f<(T)>(b, c, d) + e + kw[(T)];                                 \
+        e = d; d = c; c = rotl(b, 30); b = a; a = t;                                                        \
+    }
+#define DWPA_SHA1_KW4(T) DWPA_SHA1_KW(T) DWPA_SHA1_KW(T + 1) DWPA_SHA1_KW(T + 2) DWPA_SHA1_KW(T + 3)
+#define DWPA_SHA1_KW20(T) DWPA_SHA1_KW4(T) DWPA_SHA1_KW4(T + 4) DWPA_SHA1_KW4(T + 8) DWPA_SHA1_KW4(T + 12) DWPA_SHA1_KW4(T + 16)
+    DWPA_SHA1_KW20(0)
+    DWPA_SHA1_KW20(20)
+    DWPA_SHA1_KW20(40)
+    DWPA_SHA1_KW20(60)
+#undef DWPA_SHA1_KW20
+#undef DWPA_SHA1_KW4
+#undef DWPA_SHA1_KW
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
+}
+
 __device__ __forceinline__ void sha1_iv(uint32_t st[5]) {
     st[0] = SHA1_IV0; st[1] = SHA1_IV1; st[2] = SHA1_IV2; st[3] = SHA1_IV3; st[4] = SHA1_IV4;
 }
@@ -288,6 +310,22 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], const uint32_t m
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+// SHA-256 compression of a wave-uniform block with host-expanded kw[t] = K_t + W_t (t < 64, scalar loads).
+__device__ __forceinline__ void sha256_compress_kw(uint32_t st[8], const uint32_t* __restrict__ kw) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int t = 0; t < 64; t++) {
+        uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        uint32_t ch = ((f ^ g) & e) ^ g;
+        uint32_t t1 = h + S1 + ch + kw[t];
+        uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        uint32_t mj = (a & b) | ((a | b) & c);
+        uint32_t t2 = S0 + mj;
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
 __device__ __forceinline__ void sha256_hmac_mid(const uint32_t kb[16], uint32_t ipad[8], uint32_t opad[8]) {
     uint32_t blk[16];
 #pragma unroll
@@ -332,6 +370,26 @@ __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16
         d = c;
         c = b;
         b = b + rotl(a + f + MD5_K[i] + m[g], S[i >> 4][i & 3]);
+        a = t;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+}
+
+// MD5 compression of a wave-uniform block with host-folded km[i] = K_i + M[g(i)] (scalar loads).
+__device__ __forceinline__ void md5_compress_km(uint32_t st[4], const uint32_t* __restrict__ km) {
+    constexpr int S[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        uint32_t f;
+        if (i < 16) f = ((c ^ d) & b) ^ d;
+        else if (i < 32) f = ((b ^ c) & d) ^ c;
+        else if (i < 48) f = b ^ c ^ d;
+        else f = c ^ (b | ~d);
+        uint32_t t = d;
+        d = c;
+        c = b;
+        b = b + rotl(a + f + km[i], S[i >> 4][i & 3]);
         a = t;
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;

@@ -571,6 +571,8 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
         const uint32_t li = job_line[job];
         const LineDev& L = tb.lines[li];
         const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
+        // the key-parallel kernel reads every attempt's KW blocks (built for lines under ATT_PARALLEL_MIN)
+        if (L.kind == LINE_EAPOL && !att && tb.atts[L.list_off].kw_off == NO_KW) return DWPA_E_ARG;
         if (!tb.never[li])
             bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, row0 + i, j - i, 0});
         i = j;
@@ -878,6 +880,7 @@ int scan_create(int device, const char* const* lines, const size_t* lens, size_t
     sc->line_of.assign(nlines, 0);
     std::vector<ParsedLine> parsed(nlines);
     std::map<std::string, std::vector<size_t>> by_essid;
+    sc->tb.att_kw_all = true;  // scans verify key-parallel only: every attempt needs its KW blocks
     for (size_t i = 0; i < nlines; i++) {
         parsed[i] = parse_m22000(lines[i], lens[i]);
         sc->status[i] = parsed[i].status;

@@ -130,29 +130,15 @@ __global__ void k_set_pmk(uint32_t* __restrict__ pmk, uint32_t cap, uint32_t slo
 // ------------------------------------------------------------------------------------------------
 // stage 3: verification.  One wave = one segment = up to 64 slots x one line (line data wave-uniform).
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void sha1_blocks(uint32_t st[5], const uint32_t* __restrict__ w, uint32_t nblk) {
-    for (uint32_t b = 0; b < nblk; b++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) m[j] = w[b * 16 + j];
-        sha1_compress(st, m);
-    }
+// KW blocks (tables.hpp): wave-uniform blocks with host-expanded schedules, read with scalar loads.
+__device__ __forceinline__ void sha1_blocks_kw(uint32_t st[5], const uint32_t* __restrict__ kw, uint32_t nblk) {
+    for (uint32_t b = 0; b < nblk; b++) sha1_compress_kw(st, kw + b * SHA1_KW_WORDS);
 }
-__device__ __forceinline__ void sha256_blocks(uint32_t st[8], const uint32_t* __restrict__ w, uint32_t nblk) {
-    for (uint32_t b = 0; b < nblk; b++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) m[j] = w[b * 16 + j];
-        sha256_compress(st, m);
-    }
+__device__ __forceinline__ void sha256_blocks_kw(uint32_t st[8], const uint32_t* __restrict__ kw, uint32_t nblk) {
+    for (uint32_t b = 0; b < nblk; b++) sha256_compress_kw(st, kw + b * SHA256_KW_WORDS);
 }
-__device__ __forceinline__ void md5_blocks(uint32_t st[4], const uint32_t* __restrict__ w, uint32_t nblk) {
-    for (uint32_t b = 0; b < nblk; b++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) m[j] = w[b * 16 + j];
-        md5_compress(st, m);
-    }
+__device__ __forceinline__ void md5_blocks_km(uint32_t st[4], const uint32_t* __restrict__ km, uint32_t nblk) {
+    for (uint32_t b = 0; b < nblk; b++) md5_compress_km(st, km + b * MD5_KM_WORDS);
 }
 
 // HMAC outer hash over a 20-byte inner digest (generic state, no invariant folding).
@@ -221,19 +207,27 @@ __device__ __forceinline__ void eapol_key(const LineDev& L, const uint32_t* __re
         sha1_hmac_mid(kb, ip1, K.op1);
 #pragma unroll
         for (int k = 0; k < 5; k++) K.pre1[k] = ip1[k];
-        sha1_blocks(K.pre1, pool + L.pre_off, L.pre_nblk);
+        sha1_blocks_kw(K.pre1, pool + L.pre_off, L.pre_nblk);
     } else if constexpr (has3) {
         uint32_t ip2[8];
         sha256_hmac_mid(kb, ip2, K.op2);
 #pragma unroll
         for (int k = 0; k < 8; k++) K.pre2[k] = ip2[k];
-        sha256_blocks(K.pre2, pool + L.pre_off, L.pre_nblk);
+        sha256_blocks_kw(K.pre2, pool + L.pre_off, L.pre_nblk);
     }
+}
+
+// The attempt's PRF blocks after the shared prefix when the attempt is wave-uniform (key-parallel verifier): its
+// KW blocks (AttDev.kw_off), patched words included.
+__device__ __forceinline__ uint32_t att_nblk(const LineDev& L, const AttDev& at) {
+    return L.patch_w0 != NO_PATCH ? L.att_nblk : at.nblk;
 }
 
 // MIC of one nonce-correction attempt (common.php:250-300): PRF-512 (keyver 1/2: HMAC-SHA1, first 20 bytes;
 // keyver 3: KDF-SHA256) -> KCK -> HMAC-MD5 (1), HMAC-SHA1 (2) or AES-128-CMAC (3) over the EAPOL frame.
-template <uint32_t VC>
+// KP (key-parallel): `at` is the same for every lane, so its PRF blocks come as KW blocks; otherwise (attempt-
+// parallel, lanes hold different attempts) they are patched per lane.  The EAPOL frame's blocks are KW blocks.
+template <uint32_t VC, bool KP>
 __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __restrict__ pool, const EapolKey& K,
                                           const AttDev& at, const uint32_t* te, uint32_t mic[4]) {
     constexpr bool has1 = (VC & VC_KV1) != 0, has2 = (VC & VC_KV2) != 0, has3 = (VC & VC_KV3) != 0;
@@ -241,7 +235,8 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         uint32_t st[5], ptk[5];
 #pragma unroll
         for (int k = 0; k < 5; k++) st[k] = K.pre1[k];
-        prf_blocks(L, pool, at, [&](const uint32_t m[16]) { sha1_compress(st, m); });
+        if constexpr (KP) sha1_blocks_kw(st, pool + at.kw_off, att_nblk(L, at));
+        else prf_blocks(L, pool, at, [&](const uint32_t m[16]) { sha1_compress(st, m); });
         sha1_outer20(K.op1, st, ptk);  // PTK[0..19]; KCK = PTK[0..15]
         if (has2 && (!has1 || L.keyver == 2)) {
             // HMAC-SHA1(KCK, EAPOL): the opad midstate is computed after the inner hash so that the two key-pad
@@ -251,7 +246,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
             for (int k = 0; k < 16; k++) blk[k] = (k < 4 ? ptk[k] : 0u) ^ 0x36363636u;
             sha1_iv(mi);
             sha1_compress(mi, blk);
-            sha1_blocks(mi, pool + L.mic_off, L.mic_nblk);
+            sha1_blocks_kw(mi, pool + L.mic_off, L.mic_nblk);
 #pragma unroll
             for (int k = 0; k < 16; k++) blk[k] = (k < 4 ? ptk[k] : 0u) ^ 0x5c5c5c5cu;
             sha1_iv(mo);
@@ -264,7 +259,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
 #pragma unroll
             for (int k = 0; k < 16; k++) k1[k] = k < 4 ? bswap32(ptk[k]) : 0u;
             md5_hmac_mid(k1, mi, mo);
-            md5_blocks(mi, pool + L.mic_off, L.mic_nblk);
+            md5_blocks_km(mi, pool + L.mic_off, L.mic_nblk);
             uint32_t m[16] = {mi[0], mi[1], mi[2], mi[3], 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 640u, 0};
             md5_compress(mo, m);
             mic[0] = mo[0]; mic[1] = mo[1]; mic[2] = mo[2]; mic[3] = mo[3];
@@ -273,7 +268,8 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         uint32_t st[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) st[k] = K.pre2[k];
-        prf_blocks(L, pool, at, [&](const uint32_t m[16]) { sha256_compress(st, m); });
+        if constexpr (KP) sha256_blocks_kw(st, pool + at.kw_off, att_nblk(L, at));
+        else prf_blocks(L, pool, at, [&](const uint32_t m[16]) { sha256_compress(st, m); });
         uint32_t m[16] = {st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7],
                           0x80000000u, 0, 0, 0, 0, 0, 0, 768u};
         uint32_t ptk[8];
@@ -397,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
         sha1_hmac_mid(kb, ip, op);
 #pragma unroll
         for (int k = 0; k < 5; k++) st[k] = ip[k];
-        sha1_blocks(st, pool + L.msg_off, L.msg_nblk);
+        sha1_blocks_kw(st, pool + L.msg_off, L.msg_nblk);
         sha1_outer20(op, st, out);
         found = active && out[0] == L.target[0] && out[1] == L.target[1] && out[2] == L.target[2] &&
                 out[3] == L.target[3];
@@ -419,7 +415,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
             const AttDev* al = atts + L.list_off + list * L.natt;
             for (uint32_t a = 0; a < L.natt; a++) {
                 uint32_t mic[4];
-                eapol_mic<VC>(L, pool, K, al[a], te, mic);
+                eapol_mic<VC, true>(L, pool, K, al[a], te, mic);
                 if (mine && !found && mic_match(L, mic)) {
                     found = true;
                     found_att = a;
@@ -528,7 +524,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
     }
     const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
     uint32_t mic[4];
-    eapol_mic<VC>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic);
+    eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic);
     const bool found = active && mic_match(L, mic);
     report_hits(found, lane, cand, sg.line, a, pmk + slot, cap, hits, hitcnt, hitcap);
 }

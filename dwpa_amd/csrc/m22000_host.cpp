@@ -161,6 +161,71 @@ static uint32_t le32(const std::string& s, size_t o) {
            (uint32_t)(uint8_t)s[o + 3] << 24;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// KW blocks (tables.hpp): host-expanded schedules of wave-uniform message blocks
+// ---------------------------------------------------------------------------------------------------------
+static uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+static uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+// SHA-1: kw[t] = K_t + W_t for the 16-word big-endian block m
+static void sha1_kw(const uint32_t* m, std::vector<uint32_t>& out) {
+    uint32_t w[80];
+    for (int t = 0; t < 16; t++) w[t] = m[t];
+    for (int t = 16; t < 80; t++) w[t] = rol(w[t - 3] ^ w[t - 8] ^ w[t - 14] ^ w[t - 16], 1);
+    static const uint32_t K[4] = {0x5a827999u, 0x6ed9eba1u, 0x8f1bbcdcu, 0xca62c1d6u};
+    for (int t = 0; t < 80; t++) out.push_back(K[t / 20] + w[t]);
+}
+
+// SHA-256: kw[t] = K_t + W_t (FIPS 180-4 round constants)
+static void sha256_kw(const uint32_t* m, std::vector<uint32_t>& out) {
+    static const uint32_t K[64] = {
+        0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+        0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+        0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+        0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+        0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+        0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+        0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+        0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+    uint32_t w[64];
+    for (int t = 0; t < 16; t++) w[t] = m[t];
+    for (int t = 16; t < 64; t++) {
+        const uint32_t s0 = ror(w[t - 15], 7) ^ ror(w[t - 15], 18) ^ (w[t - 15] >> 3);
+        const uint32_t s1 = ror(w[t - 2], 17) ^ ror(w[t - 2], 19) ^ (w[t - 2] >> 10);
+        w[t] = w[t - 16] + s0 + w[t - 7] + s1;
+    }
+    for (int t = 0; t < 64; t++) out.push_back(K[t] + w[t]);
+}
+
+// MD5: km[i] = K_i + M[g(i)] for the 16-word little-endian block m (RFC 1321, K_i = floor(2^32 |sin(i + 1)|))
+static void md5_km(const uint32_t* m, std::vector<uint32_t>& out) {
+    static const uint32_t K[64] = {
+        0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u, 0xfd469501u,
+        0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u,
+        0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du, 0x02441453u, 0xd8a1e681u, 0xe7d3fbc8u,
+        0x21e1cde6u, 0xc33707d6u, 0xf4d50d87u, 0x455a14edu, 0xa9e3e905u, 0xfcefa3f8u, 0x676f02d9u, 0x8d2a4c8au,
+        0xfffa3942u, 0x8771f681u, 0x6d9d6122u, 0xfde5380cu, 0xa4beea44u, 0x4bdecfa9u, 0xf6bb4b60u, 0xbebfbc70u,
+        0x289b7ec6u, 0xeaa127fau, 0xd4ef3085u, 0x04881d05u, 0xd9d4d039u, 0xe6db99e5u, 0x1fa27cf8u, 0xc4ac5665u,
+        0xf4292244u, 0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
+        0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu, 0xeb86d391u};
+    for (int i = 0; i < 64; i++) {
+        const int g = i < 16 ? i : i < 32 ? (5 * i + 1) & 15 : i < 48 ? (3 * i + 5) & 15 : (7 * i) & 15;
+        out.push_back(K[i] + m[g]);
+    }
+}
+
+enum class Kw { Sha1, Sha256, Md5 };
+// Append blocks [b0, b1) of the 16-word-block stream w to the pool as KW blocks; returns their word offset.
+static uint32_t push_kw(std::vector<uint32_t>& pool, const uint32_t* w, size_t b0, size_t b1, Kw alg) {
+    const uint32_t off = (uint32_t)pool.size();
+    for (size_t b = b0; b < b1; b++) {
+        if (alg == Kw::Sha1) sha1_kw(w + 16 * b, pool);
+        else if (alg == Kw::Sha256) sha256_kw(w + 16 * b, pool);
+        else md5_km(w + 16 * b, pool);
+    }
+    return off;
+}
+
 // PHP 8 substr_replace($s, $r, $off, $len) with offset/length clamping
 static void php_substr_replace(std::string& s, const std::string& r, size_t off, size_t len) {
     if (off > s.size()) off = s.size();
@@ -204,7 +269,7 @@ static std::string nc_raw(const NcAtt& a, int64_t corrV, int64_t corrN) {
 // message of attempt a for the k-th non-null key; every attempt gets its own pre-padded blocks.
 static void add_explicit_attempts(TableBuilder& tb, LineDev& L, const std::vector<NcAtt>& order, const std::string& n0,
                                   const std::string& pre, const std::string& post, size_t patch, int nc_mode,
-                                  int64_t corrV, int64_t corrN) {
+                                  int64_t corrV, int64_t corrN, Kw alg, bool att_kw) {
     std::vector<std::vector<std::string>> lists;
     if (nc_mode == DWPA_NC_HASHCAT) {
         std::vector<std::string> lst;
@@ -248,9 +313,8 @@ static void add_explicit_attempts(TableBuilder& tb, LineDev& L, const std::vecto
         if (!same) break;
         prefix++;
     }
-    L.pre_off = (uint32_t)tb.pool.size();
+    L.pre_off = push_kw(tb.pool, ref.data(), 0, prefix, alg);
     L.pre_nblk = (uint32_t)prefix;
-    tb.pool.insert(tb.pool.end(), ref.begin(), ref.begin() + 16 * prefix);
     L.list_off = (uint32_t)tb.atts.size();
     L.nlists = (uint32_t)lists.size();
     for (size_t k = 0; k < lists.size(); k++)
@@ -263,6 +327,7 @@ static void add_explicit_attempts(TableBuilder& tb, LineDev& L, const std::vecto
             at.nc = a == 0 ? 0 : (int32_t)order[a].off;
             at.endian = a == 0 ? 0u : (order[a].big ? 1u : 2u);
             tb.pool.insert(tb.pool.end(), w.begin() + 16 * prefix, w.end());
+            at.kw_off = att_kw ? push_kw(tb.pool, w.data(), prefix, w.size() / 16, alg) : NO_KW;
             tb.atts.push_back(at);
         }
 
@@ -276,9 +341,8 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
     if (p.kind == LINE_PMKID) {
         std::string msg = std::string("PMK Name") + p.mac_ap + p.mac_sta;
         std::vector<uint32_t> w = md_stream_be(msg, 64);
-        L.msg_off = (uint32_t)pool.size();
         L.msg_nblk = (uint32_t)(w.size() / 16);
-        pool.insert(pool.end(), w.begin(), w.end());
+        L.msg_off = push_kw(pool, w.data(), 0, L.msg_nblk, Kw::Sha1);
         const bool ok = p.pmkid.size() >= 16;  // strncmp(20-byte digest, $pmkid, 16) needs >= 16 bytes
         for (int k = 0; k < 4; k++) L.target[k] = ok ? be32(p.pmkid, 4 * k) : 0;
         lines.push_back(L);
@@ -324,6 +388,8 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
 
     L.patch_w0 = L.patch_w1 = NO_PATCH;
     L.natt = (uint32_t)order.size();
+    const Kw prf_alg = kv3 ? Kw::Sha256 : Kw::Sha1;
+    const bool att_kw = att_kw_all || L.natt < ATT_PARALLEL_MIN;
     if (n0.size() >= patch + 4) {
         // Every attempt rewrites exactly bytes [patch, patch+4) of $n (common.php:255-259) and never changes its
         // length, so all attempts of all keys share one message apart from those 4 bytes: one list, one shared
@@ -333,9 +399,8 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
         const std::vector<uint32_t> w = md_stream_be(base, 64);
         const uint32_t W0 = (uint32_t)(o >> 2), W1 = (uint32_t)((o + 3) >> 2);
         const uint32_t prefix = W0 / 16;
-        L.pre_off = (uint32_t)pool.size();
+        L.pre_off = push_kw(pool, w.data(), 0, prefix, prf_alg);
         L.pre_nblk = prefix;
-        pool.insert(pool.end(), w.begin(), w.begin() + 16 * prefix);
         const uint32_t blk_off = (uint32_t)pool.size();
         pool.insert(pool.end(), w.begin() + 16 * prefix, w.end());
         L.patch_w0 = W0 - 16 * prefix;
@@ -365,10 +430,17 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
             at.endian = a == 0 ? 0u : (order[a].big ? 1u : 2u);
             at.v0 = v[0];
             at.v1 = v[1];
+            at.kw_off = NO_KW;
+            if (att_kw) {  // this attempt's blocks with its two words patched in, expanded
+                std::vector<uint32_t> pw(w.begin() + 16 * prefix, w.end());
+                pw[L.patch_w0] = v[0];
+                pw[L.patch_w1] = v[1];
+                at.kw_off = push_kw(pool, pw.data(), 0, pw.size() / 16, prf_alg);
+            }
             atts.push_back(at);
         }
     } else {
-        add_explicit_attempts(*this, L, order, n0, pre, post, patch, nc_mode, corrV, corrN);
+        add_explicit_attempts(*this, L, order, n0, pre, post, patch, nc_mode, corrV, corrN, prf_alg, att_kw);
     }
 
     // MIC input
@@ -376,7 +448,7 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
     if (p.keyver == 1 || p.keyver == 2) {
         std::vector<uint32_t> w = p.keyver == 1 ? md5_stream_le(p.eapol, 64) : md_stream_be(p.eapol, 64);
         L.mic_nblk = (uint32_t)(w.size() / 16);
-        pool.insert(pool.end(), w.begin(), w.end());
+        L.mic_off = push_kw(pool, w.data(), 0, L.mic_nblk, p.keyver == 1 ? Kw::Md5 : Kw::Sha1);
     } else {
         const size_t len = p.eapol.size();
         const size_t nb = (len + 15) / 16;

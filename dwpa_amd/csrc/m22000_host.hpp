@@ -36,6 +36,10 @@ struct TableBuilder {
     std::vector<uint32_t> pool;  // pre-padded hash blocks (16 words each) and CMAC blocks (4 words each)
     std::vector<uint8_t> never;  // per line: 1 if the line can never match (target shorter than 16 bytes)
 
+    // KW blocks of every attempt's PRF blocks for the key-parallel verifier: always (att_kw_all, scan API), else
+    // only for lines with fewer than ATT_PARALLEL_MIN attempts (the check path verifies the others attempt-parallel).
+    bool att_kw_all = false;
+
     // Adds a parsed (status 0) line; returns its index.
     uint32_t add_line(const ParsedLine& p, int nc, int nc_mode, int nec);
 };

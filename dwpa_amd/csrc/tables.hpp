@@ -5,6 +5,11 @@
 // ESSID per work unit, web/content/get_work.php:96-109).  Everything that is uniform across candidates -- the
 // PRF messages of every nonce-correction attempt, EAPOL frames, PMKID messages -- is pre-padded on the host into
 // hash blocks so that the verifier kernel reads it with wave-uniform (scalar) loads.
+//
+// KW blocks.  A block that every lane of a wave hashes alike has the same message schedule in every lane, so the
+// host expands it once: SHA-1 kw[t] = K_t + W_t (80 words per block), SHA-256 kw[t] = K_t + W_t (64 words), MD5
+// km[i] = K_i + M[g(i)] (64 words).  The kernels read them with scalar loads and skip the schedule (~1/3 of a
+// SHA-1 compression).  Blocks that differ per lane (the attempt-parallel verifier's patched PRF blocks) stay raw.
 #pragma once
 #include <stdint.h>
 
@@ -16,15 +21,15 @@ struct LineDev {
     uint32_t kind;        // LINE_PMKID / LINE_EAPOL
     uint32_t keyver;      // EAPOL key version 1/2/3 (key_information & 3, common.php:215-217)
     uint32_t target[4];   // PMKID or MIC (first 16 bytes): BE words (SHA1/CMAC) or LE words (MD5, keyver 1)
-    uint32_t msg_off;     // PMKID: pre-padded HMAC-SHA1 inner blocks of "PMK Name"||AP||STA (word offset in pool)
+    uint32_t msg_off;     // PMKID: HMAC-SHA1 inner blocks of "PMK Name"||AP||STA as SHA-1 KW blocks (pool words)
     uint32_t msg_nblk;
-    uint32_t pre_off;     // EAPOL: PRF message blocks shared by every attempt (pre-padded), word offset
+    uint32_t pre_off;     // EAPOL: PRF message blocks shared by every attempt, KW blocks (SHA-1, keyver 3 SHA-256)
     uint32_t pre_nblk;
     uint32_t list_off;    // EAPOL: attempt lists; list k = attempts [list_off + k*natt, +natt) in the attempt table
     uint32_t nlists;      // list k applies to the k-th non-null key (PHP mutates $n across keys); last list to the rest
     uint32_t natt;        // attempts per list (1 + 4*halfnc in PHP order, common.php:250-300)
-    uint32_t mic_off;     // EAPOL: HMAC inner blocks of the EAPOL frame (keyver 1/2), or CMAC blocks (keyver 3)
-    uint32_t mic_nblk;
+    uint32_t mic_off;     // EAPOL: HMAC inner blocks of the EAPOL frame as KW blocks (keyver 1 MD5 km, keyver 2 SHA-1
+    uint32_t mic_nblk;    // kw), or raw 4-word CMAC blocks (keyver 3)
     uint32_t cmac_complete;  // keyver 3: 1 if the last EAPOL block is complete (XOR K1), else padded (XOR K2)
     // Attempt patching: in the usual case every attempt's PRF message differs from the others only in the 4
     // nonce-correction bytes, so all attempts share one block stream (AttDev.blk_off) and each attempt carries
@@ -45,8 +50,11 @@ struct AttDev {
     int32_t nc;           // signed correction reported on a hit (0 for the first attempt)
     uint32_t endian;      // 0 none (exact), 1 BE ('N'), 2 LE ('V')
     uint32_t v0, v1;      // values of stream words patch_w0 / patch_w1 for this attempt (LineDev.patch_w0 != NO_PATCH)
-    uint32_t pad0, pad1;
+    uint32_t kw_off;      // this attempt's PRF blocks after the prefix as KW blocks (key-parallel verifier), or NO_KW
+    uint32_t pad1;
 };
+constexpr uint32_t NO_KW = 0xffffffffu;
+constexpr uint32_t SHA1_KW_WORDS = 80, SHA256_KW_WORDS = 64, MD5_KM_WORDS = 64;
 // Verify classes: kernels are instantiated per class so that each launch carries only one MAC's code and registers.
 enum : uint32_t { VC_PMKID = 1, VC_KV1 = 2, VC_KV2 = 4, VC_KV3 = 8, VC_ALL = 15 };
 inline uint32_t verify_class(const LineDev& L) {
