@@ -36,7 +36,11 @@ def main_loop_range(lines, kernel):
             lab = lines[h].split(":")[0].strip()
             if not lab.startswith(".LBB"):
                 lab = lines[h - 1].split(":")[0].strip()
-            e = next(n for n in range(h + 1, end) if "s_cbranch" in lines[n] and lines[n].split()[-1] == lab)
+            # the backedge is a conditional branch to the header below it; a loop entered by fallthrough from a
+            # latch placed above the header (an outer loop around the hot one) is skipped
+            e = next((n for n in range(h + 1, end) if "s_cbranch" in lines[n] and lines[n].split()[-1] == lab), None)
+            if e is None:
+                continue
             nv = sum(1 for l in lines[h:e] if re.match(r"\s+v_", l))
             if best is None or nv > best[2]:
                 best = (h, e, nv)

@@ -15,6 +15,13 @@ namespace dwpa {
 
 // One lane's PBKDF2 output block: T = U_1 ^ ... ^ U_4096 with U_1 = HMAC(P, S || INT(blk+1)).  `sb` points at
 // the nsalt pre-padded 16-word salt blocks of this output block.
+//
+// PRIO: progress-ordered wave priority.  A SIMD issues by priority, then age, so the oldest of its waves runs
+// almost alone-fast and the youngest gets leftovers: in a launch of one wave round (server checks, C1/C5) the waves
+// finish one after another and the last one runs its remaining iterations alone, latency-bound.  With PRIO a wave
+// lowers its priority as it passes iterations 3072, 3584 and 3840, so waves that are behind get the issue slots and
+// the waves of a SIMD reach the end together (spread <= 256 iterations instead of up to a whole wave).
+template <bool PRIO = false>
 __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
                                             uint32_t nsalt, uint32_t t[5]) {
     uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
@@ -30,12 +37,31 @@ __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t
     sha1_84(MO, st, u);
 #pragma unroll
     for (int k = 0; k < 5; k++) t[k] = u[k];
+    if constexpr (!PRIO) {
 #pragma unroll 1
-    for (int it = 1; it < 4096; it++) {
-        sha1_84(MI, u, x);
-        sha1_84(MO, x, u);
+        for (int it = 1; it < 4096; it++) {
+            sha1_84(MI, u, x);
+            sha1_84(MO, x, u);
 #pragma unroll
-        for (int k = 0; k < 5; k++) t[k] ^= u[k];
+            for (int k = 0; k < 5; k++) t[k] ^= u[k];
+        }
+    } else {
+        __builtin_amdgcn_s_setprio(3);
+        int it = 1;
+#pragma unroll 1
+        for (int phase = 0; phase < 4; phase++) {
+            const int end = phase == 0 ? 3072 : phase == 1 ? 3584 : phase == 2 ? 3840 : 4096;
+            if (phase == 1) __builtin_amdgcn_s_setprio(2);
+            else if (phase == 2) __builtin_amdgcn_s_setprio(1);
+            else if (phase == 3) __builtin_amdgcn_s_setprio(0);
+#pragma unroll 1
+            for (; it < end; it++) {
+                sha1_84(MI, u, x);
+                sha1_84(MO, x, u);
+#pragma unroll
+                for (int k = 0; k < 5; k++) t[k] ^= u[k];
+            }
+        }
     }
 }
 
@@ -60,6 +86,7 @@ __device__ __forceinline__ void store_block(uint32_t* __restrict__ pmk, uint32_t
 }
 
 // One ESSID for the whole launch: salt = [2 blocks][nsalt][16] words, read with scalar loads.
+template <bool PRIO = false>
 __device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base,
                                             uint32_t count, const uint32_t* __restrict__ counter,
                                             const uint32_t* __restrict__ salt, uint32_t nsalt,
@@ -70,13 +97,14 @@ __device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, ui
     if (s >= n) return;
     uint32_t hi[5], ho[5], t[5];
     load_mid(mid, cap, s, hi, ho);
-    pbkdf2_lane(hi, ho, salt + (size_t)blk * nsalt * 16, nsalt, t);
+    pbkdf2_lane<PRIO>(hi, ho, salt + (size_t)blk * nsalt * 16, nsalt, t);
     store_block(pmk, cap, s, blk, t);
 }
 
 // Many ESSIDs in one launch (server batches, common.php:902): slot s derives with the salt entry at
 // pool + sref[s] = {nsalt, [2 blocks][nsalt][16] words}.  Only the U_1 blocks differ per lane; the 4096 loop is
 // the same code as pbkdf2_body's.
+template <bool PRIO = false>
 __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
                                                const uint32_t* __restrict__ pool,
                                                const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk) {
@@ -87,7 +115,7 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
     load_mid(mid, cap, s, hi, ho);
     const uint32_t* e = pool + sref[s];
     const uint32_t nsalt = e[0];
-    pbkdf2_lane(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
+    pbkdf2_lane<PRIO>(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
     store_block(pmk, cap, s, blk, t);
 }
 
@@ -95,6 +123,7 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
 // lane i -> chunk group c = i / cap, slot s = i % cap.  cap is a multiple of 64, so c is wave-uniform and the
 // salt entry is read with scalar loads.  gsalt[c] = {word offset of the group's [2][nsalt][16] salt blocks, nsalt};
 // PMK word k of (c, s) lands at pmk[k * pstride + c * cap + s].
+template <bool PRIO = false>
 __device__ __forceinline__ void pbkdf2_body_mg(const uint32_t* __restrict__ mid, uint32_t cap,
                                                const uint32_t* __restrict__ counter, uint32_t ngroups,
                                                const uint32_t* __restrict__ salt, const uint32_t* __restrict__ gsalt,
@@ -107,7 +136,7 @@ __device__ __forceinline__ void pbkdf2_body_mg(const uint32_t* __restrict__ mid,
     uint32_t hi[5], ho[5], t[5];
     load_mid(mid, cap, s, hi, ho);
     const uint32_t off = gsalt[2 * c], nsalt = gsalt[2 * c + 1];
-    pbkdf2_lane(hi, ho, salt + off + (size_t)blk * nsalt * 16, nsalt, t);
+    pbkdf2_lane<PRIO>(hi, ho, salt + off + (size_t)blk * nsalt * 16, nsalt, t);
     store_block(pmk + (size_t)c * cap, pstride, s, blk, t);
 }
 

@@ -29,3 +29,25 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                                                                      uint32_t* __restrict__ pmk, uint32_t pstride) {
     dwpa::pbkdf2_body_mg(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride);
 }
+
+// Progress-ordered priority variants (pbkdf2_dev.hpp, PRIO): selected per launch by pbkdf2_module.cpp.
+extern "C" __global__ __launch_bounds__(256) void k_pbkdf2_gfx950_p(const uint32_t* __restrict__ mid, uint32_t cap,
+                                                                    uint32_t base, uint32_t count,
+                                                                    const uint32_t* __restrict__ counter,
+                                                                    const uint32_t* __restrict__ salt, uint32_t nsalt,
+                                                                    uint32_t* __restrict__ pmk) {
+    dwpa::pbkdf2_body<true>(mid, cap, base, count, counter, salt, nsalt, pmk);
+}
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_ms_p(
+    const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
+    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk) {
+    dwpa::pbkdf2_body_ms<true>(mid, cap, count, pool, sref, pmk);
+}
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_mg_p(
+    const uint32_t* __restrict__ mid, uint32_t cap, const uint32_t* __restrict__ counter, uint32_t ngroups,
+    const uint32_t* __restrict__ salt, const uint32_t* __restrict__ gsalt, uint32_t* __restrict__ pmk,
+    uint32_t pstride) {
+    dwpa::pbkdf2_body_mg<true>(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride);
+}

@@ -19,6 +19,7 @@ extern const size_t pbkdf2_gfx950_hsaco_size;
 
 struct Fns {
     hipFunction_t one, ms, mg;  // k_pbkdf2_gfx950 (one ESSID), _ms (per-slot salt), _mg (ESSID groups x batch)
+    hipFunction_t one_p, ms_p, mg_p;  // the same with progress-ordered wave priority (pbkdf2_dev.hpp PRIO)
     uint64_t level_lanes;       // lanes that give every SIMD of the device one wave: CUs x 4 SIMDs x 64
 };
 static std::mutex g_mod_mu;
@@ -35,6 +36,19 @@ static bool use_plain() {
 static bool force_issue() {
     static const bool issue = env_flag("DWPA_PBKDF2_ISSUE");
     return issue;
+}
+// Progress-ordered priority (pbkdf2_dev.hpp PRIO) for launches of at most one wave round (<= 8 waves per SIMD):
+// there the waves of a SIMD otherwise finish one after another and the last runs alone.  Measured on MI355X
+// (profiles/r02/prio/): 6 waves/SIMD 43.0 -> 40.7 ms, 4 waves 29.4 -> 26.5 ms, the C5 call 58.0 -> 54.6 ms; level on
+// 16-round launches (C2 844.3 vs 844.3 ms), so multi-round launches keep the plain-priority kernel.
+// DWPA_PBKDF2_PRIO=0/1 forces it off/on (A/B).
+static bool use_prio(const Fns& fn, uint64_t pmks) {
+    static const int forced = [] {
+        const char* e = getenv("DWPA_PBKDF2_PRIO");
+        return e && *e ? (*e != '0' ? 1 : 0) : -1;
+    }();
+    if (forced >= 0) return forced == 1;
+    return 2 * pmks <= 8 * fn.level_lanes;
 }
 
 // Workgroup size of the issue-pass launches (DWPA_PBKDF2_WG = 64/128/256, default 256): partial-round experiments.
@@ -62,6 +76,9 @@ static hipError_t tuned_functions(Fns* fn) {
     if ((e = hipModuleGetFunction(&fn->one, mod, "k_pbkdf2_gfx950")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->ms, mod, "k_pbkdf2_gfx950_ms")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->mg, mod, "k_pbkdf2_gfx950_mg")) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(&fn->one_p, mod, "k_pbkdf2_gfx950_p")) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(&fn->ms_p, mod, "k_pbkdf2_gfx950_ms_p")) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(&fn->mg_p, mod, "k_pbkdf2_gfx950_mg_p")) != hipSuccess) return e;
     int cus = 0;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     fn->level_lanes = (uint64_t)(cus > 0 ? cus : 256) * 4 * 64;
@@ -85,7 +102,9 @@ hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint3
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&base, (void*)&count, (void*)&counter,
                     (void*)&salt, (void*)&nsalt, (void*)&pmk};
     const uint32_t wg = wg_size();
-    return hipModuleLaunchKernel(fn.one, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(use_prio(fn, std::min<uint64_t>(count, cap > base ? cap - base : 0)) ? fn.one_p : fn.one,
+                                 (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args,
+                                 nullptr);
 }
 
 hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
@@ -98,7 +117,8 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
     if (lone_waves(fn, std::min(count, cap))) return launch_pbkdf2_ms_plain(mid, cap, count, pool, sref, pmk, s);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk};
     const uint32_t wg = wg_size();
-    return hipModuleLaunchKernel(fn.ms, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(use_prio(fn, std::min(count, cap)) ? fn.ms_p : fn.ms, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args,
+                                 nullptr);
 }
 
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
@@ -116,7 +136,8 @@ hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* c
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&counter, (void*)&ngroups, (void*)&salt, (void*)&gsalt,
                     (void*)&pmk, (void*)&pstride};
     const uint32_t wg = wg_size();
-    return hipModuleLaunchKernel(fn.mg, (uint32_t)((lanes + wg - 1) / wg), 2, 1, wg, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(use_prio(fn, lanes) ? fn.mg_p : fn.mg, (uint32_t)((lanes + wg - 1) / wg), 2, 1, wg, 1, 1, 0, s,
+                                 args, nullptr);
 }
 
 uint32_t pbkdf2_wave_unit() {
