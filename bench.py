@@ -43,10 +43,16 @@ PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
 # run, so the bench scales the measured per-PMK figure to its launches.
 #   c2/c4: k_pbkdf2_gfx950, profiles/r01/traffic (4,194,304-PMK launch): FETCH 167,954,944 B x 2 = 80 B/PMK (each of
 #          the two output-block lanes reads the 40-byte key midstate once) + WRITE 134,217,728 B = 32 B/PMK
-#   c3:    k_pbkdf2_gfx950_mg + k_verify per dwpa_scan_run, profiles/r02/traffic_c3 (TRAFFIC_C3 below)
-TRAFFIC_BYTES_PER_PMK = {"c2": (2 * 167954944 + 134217728) / 4194304, "c4": (2 * 167954944 + 134217728) / 4194304}
-TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950, profiles/r01/traffic",
-                  "c4": "k_pbkdf2_gfx950 per PMK as measured on c2, profiles/r01/traffic"}
+#   c3:    k_pbkdf2_gfx950_mg + k_verify<PMKID> + k_verify<keyver 2> per dwpa_scan_run (the roofline's events bracket
+#          all three), profiles/r02/traffic_post_kw/traffic_c3: 493.4 + 446.6 + 1,093.9 MB for 13,445,190 PMKs
+TRAFFIC_BYTES_PER_PMK = {"c2": (2 * 167954944 + 134217728) / 4194304, "c4": (2 * 167954944 + 134217728) / 4194304,
+                         "c3": (493.445e6 + 446.648e6 + 1093.881e6) / 13445190}
+TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950, profiles/r01/traffic (re-measured level in profiles/r02/traffic_post_kw)",
+                  "c4": "k_pbkdf2_gfx950 per PMK as measured on c2, profiles/r01/traffic",
+                  "c3": "k_pbkdf2_gfx950_mg + k_verify, profiles/r02/traffic_post_kw/traffic_c3"}
+# Algorithmic bytes per PMK: PBKDF2 reads the 40-byte key midstate twice (one lane per output block) and writes the
+# 32-byte PMK (c2/c4, the kernel the roofline names).  c3's events also bracket the verify, which reads each PMK
+# (32 B) and candidate id (8 B) once per hashline of its ESSID; its midstates are shared by all ESSID groups.
 ALGO_BYTES_PER_PMK = 80 + 32
 # Guide view (MI355X_MICROARCH.md: 4 SIMD-32 per CU, one VALU per 2 cycles = 128 int32 lane-ops/clk/CU at 2.4 GHz,
 # every op full rate).  Reported beside the issue-cost roofline, with SURVEY.md 8(d)'s ideal 617 ops per compression
@@ -138,6 +144,7 @@ def build_c2(args, local, S, Scan, Dictionary):
         return [raw[o[i] - o[0]:o[i + 1] - o[0]] for i in range(m)]
     w.load, w.check, w.plant_batch = load, check, w.plant // w.B
     w.cpu_line, w.cpu_keys, w.cpu_what = w.line, cpu_keys, "dictionary words"
+    w.algo_bytes_per_pmk = ALGO_BYTES_PER_PMK
     return w
 
 
@@ -169,6 +176,7 @@ def build_c4(args, local, S, Scan, Dictionary):
     w.load, w.check, w.plant_batch = load, check, w.plant // w.B
     w.cpu_line, w.cpu_keys = w.line, lambda m: [b"%08d" % v for v in range(w.plant - m + 1, w.plant + 1)]
     w.cpu_what = "8-digit candidates"
+    w.algo_bytes_per_pmk = ALGO_BYTES_PER_PMK
     return w
 
 
@@ -240,6 +248,7 @@ def build_c3(args, local, S, Scan, Dictionary):
     w.load, w.check = load, check
     w.cpu_line, w.cpu_keys = (lines[w.plants[0][0]], cpu_keys) if w.plants else (None, None)
     w.cpu_what = "rule candidates (word-major, 8..63) of one ESSID's line"
+    w.algo_bytes_per_pmk = 32 + 40 * len(lines) / w.groups
     w.plant_batch = (w.plants[0][1] // w.nrules) // w.words_per_step if w.plants else 0
     return w
 
@@ -373,7 +382,7 @@ def main():
                 "traffic": round(traffic_pmk * pmk_per_launch) if traffic_pmk else None,
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE of this workload, "
                                 + TRAFFIC_SOURCE.get(args.workload, "not measured") + ")",
-                "algorithmic_bytes": ALGO_BYTES_PER_PMK * pmk_per_launch,
+                "algorithmic_bytes": round(w.algo_bytes_per_pmk * pmk_per_launch),
                 "hbm_gbs": round(traffic_pmk * pmk_per_launch / (kernel_ms * 1e-3) / 1e9, 3) if traffic_pmk else None,
                 "kernel_ms": round(kernel_ms, 3),
                 "pmk_per_launch": pmk_per_launch,
