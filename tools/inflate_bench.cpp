@@ -3,10 +3,11 @@
 // stream can feed in the rules-less first pass (help_crack.py:929; a GPU scans ~4.9 M words/s at C2).
 //
 //   inflate_bench FILE.gz [FILE2.gz ...]
+//   inflate_bench --dump FILE... prints every word the reader yields, hex-encoded, one per line (tests/test_dict_reader.py)
 //
 // Prints one JSON line: raw gzread throughput of the first file (inflate only), DictReader words/s on the first
-// file (inflate + line cutting + $HEX[] decoding: one stream, one core), and ChunkSource words/s over all files
-// (up to 4 reader threads, as crack_files runs them).
+// file (one stream: an inflate thread feeding the line cutting + $HEX[] decoding thread), and ChunkSource words/s
+// over all files (up to 4 such streams, as crack_files runs them).
 #include <stdio.h>
 #include <zlib.h>
 
@@ -24,6 +25,25 @@ int main(int argc, char** argv) {
     if (argc < 2) {
         fprintf(stderr, "usage: %s FILE.gz [FILE2.gz ...]\n", argv[0]);
         return 2;
+    }
+    if (std::string(argv[1]) == "--dump") {
+        dwpa::DictReader rd(std::vector<std::string>(argv + 2, argv + argc));
+        dwpa::Chunk c;
+        bool err = false;
+        std::string line;
+        while (rd.next(c, 1000, (size_t)1 << 20, err)) {
+            for (size_t i = 0; i < c.words(); i++) {
+                line.clear();
+                for (uint64_t k = c.off[i]; k < c.off[i + 1]; k++) {
+                    static const char* d = "0123456789abcdef";
+                    line.push_back(d[(uint8_t)c.bytes[k] >> 4]);
+                    line.push_back(d[(uint8_t)c.bytes[k] & 15]);
+                }
+                line.push_back('\n');
+                fwrite(line.data(), 1, line.size(), stdout);
+            }
+        }
+        return err ? 1 : 0;
     }
     std::vector<std::string> paths(argv + 1, argv + argc);
     // 1. inflate only
