@@ -123,7 +123,7 @@ struct Device {
     hipStream_t side = nullptr;   // check path: table uploads while PBKDF2 runs on `stream`
     hipEvent_t side_done = nullptr;
     hipStream_t tail = nullptr;   // check path: the PBKDF2 remainder (< one wave per SIMD) + its verify
-    hipEvent_t head_done = nullptr, tail_done = nullptr;
+    hipEvent_t head_done = nullptr, tail_done = nullptr, prep_done = nullptr;
     PinnedArena stage;            // check path: host staging of the derive uploads
     std::mutex mu;
     Batch batch;
@@ -185,6 +185,7 @@ static int device_stream(Device& d) {
         HIPCHK(hipStreamCreateWithFlags(&d.tail, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&d.head_done, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.tail_done, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.prep_done, hipEventDisableTiming));
     }
     return 0;
 }
@@ -358,12 +359,13 @@ static bool check_split_enabled() {
 
 // Head/tail split of one derive.  PBKDF2 is issue-bound, so a launch takes as long as its fullest SIMD: nu unique
 // PMKs at k.f waves per SIMD cost k + 1 whole wave times (~7 ms each at C5 size), the last one with 1 - f of the
-// chip idle.  The head (k whole waves per SIMD) runs alone; the tail (< one wave per SIMD, the latency-bound plain
-// kernel) starts when the head ends and overlaps the head's verify on d.tail.  Below 4 waves per SIMD the lone
-// tail's ~8 ms chain costs more than the wave time it saves, so small derives stay in one launch.
+// chip idle.  The head (k whole waves per SIMD) runs at wave priority 3..1 (pbkdf2_dev.hpp PRIO); the tail
+// (< one wave per SIMD, the latency-bound plain kernel, priority 0) is launched beside it on d.tail and takes only
+// the issue slots the head leaves, then finishes alone while the head's verify runs.  From 2 whole waves per SIMD
+// up (the head's PRIO kernel; below that both kernels are lone-wave plain kernels) the split pays.
 static uint32_t head_pmks(uint32_t nu) {
     const uint32_t unit = pbkdf2_wave_unit();
-    if (!check_split_enabled() || !unit || nu < 4 * unit) return nu;
+    if (!check_split_enabled() || !unit || nu < 2 * unit) return nu;
     return nu / unit * unit;
 }
 
@@ -529,6 +531,11 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     if (nu) {
         HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, nu, 0, 0xffffffffu,
                                 (uint32_t*)d.batch.mid.p, nullptr, nullptr, cap, false, s));
+        if (nh < nu) {  // the tail first, beside the head (it only gets the head's leftover issue slots)
+            HIPCHK(hipEventRecord(d.prep_done, s));
+            HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
+            HIPCHK(launch_pbkdf2_ms(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh, d.tail));
+        }
         HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
     }
     // SoA rows keep their stride (cap), so a sub-range is the same launch on offset base pointers
@@ -536,10 +543,9 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     if (sp)
         HIPCHK(launch_gather_pmk(upmk, cap, (const uint32_t*)d.cpmk.p, (const uint32_t*)d.src.p, sp,
                                  (uint32_t*)d.batch.pmk.p, cap, s));
-    if (sp < n) {
+    if (sp < n) {  // tail slots may also read head PMKs: their gather waits for both derives
         HIPCHK(hipEventRecord(d.head_done, s));
         HIPCHK(hipStreamWaitEvent(d.tail, d.head_done, 0));
-        HIPCHK(launch_pbkdf2_ms(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh, d.tail));
         HIPCHK(launch_gather_pmk(upmk, cap, (const uint32_t*)d.cpmk.p, (const uint32_t*)d.src.p + sp, n - sp,
                                  (uint32_t*)d.batch.pmk.p + sp, cap, d.tail));
     }
@@ -577,12 +583,13 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
             bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, row0 + i, j - i, 0});
         i = j;
     }
-    // attempt-parallel buckets: pad = the segment's first wave in its launch (ceil(count * natt / 64) waves each)
+    // attempt-parallel buckets: pad = the segment's first wave in its launch (ceil(count * natt / (64 * ATT_ITEMS))
+    // waves each)
     uint32_t nwaves[8] = {0}, kwords = 0, kstride = 0;
     for (int k = 4; k < 8; k++) {
         for (SegDev& sg : bucket[k]) {
             sg.pad = nwaves[k];
-            nwaves[k] += (uint32_t)(((uint64_t)sg.count * tb.lines[sg.line].natt + 63) / 64);
+            nwaves[k] += (uint32_t)(((uint64_t)sg.count * tb.lines[sg.line].natt + 64 * ATT_ITEMS - 1) / (64 * ATT_ITEMS));
         }
         if (!bucket[k].empty()) {
             kwords = std::max(kwords, eapol_key_words(1u << (k & 3)));
@@ -1187,8 +1194,9 @@ void dwpa_shutdown(void) {
         if (d->tail) (void)hipStreamDestroy(d->tail);
         if (d->head_done) (void)hipEventDestroy(d->head_done);
         if (d->tail_done) (void)hipEventDestroy(d->tail_done);
+        if (d->prep_done) (void)hipEventDestroy(d->prep_done);
         d->stream = d->side = d->tail = nullptr;
-        d->side_done = d->head_done = d->tail_done = nullptr;
+        d->side_done = d->head_done = d->tail_done = d->prep_done = nullptr;
     }
     g_dev.clear();
     g_init = false;

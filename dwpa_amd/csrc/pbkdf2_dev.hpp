@@ -19,8 +19,9 @@ namespace dwpa {
 // PRIO: progress-ordered wave priority.  A SIMD issues by priority, then age, so the oldest of its waves runs
 // almost alone-fast and the youngest gets leftovers: in a launch of one wave round (server checks, C1/C5) the waves
 // finish one after another and the last one runs its remaining iterations alone, latency-bound.  With PRIO a wave
-// lowers its priority as it passes iterations 3072, 3584 and 3840, so waves that are behind get the issue slots and
-// the waves of a SIMD reach the end together (spread <= 256 iterations instead of up to a whole wave).
+// starts at priority 3 and drops to 2 at iteration 3584 and to 1 at 3968, so waves that are behind get the issue
+// slots and the waves of a SIMD reach the end together (spread <= ~128 iterations instead of up to a whole wave).
+// Priority 0 stays free for work that should only take the slots these waves leave (the check path's tail).
 template <bool PRIO = false>
 __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
                                             uint32_t nsalt, uint32_t t[5]) {
@@ -49,11 +50,10 @@ __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t
         __builtin_amdgcn_s_setprio(3);
         int it = 1;
 #pragma unroll 1
-        for (int phase = 0; phase < 4; phase++) {
-            const int end = phase == 0 ? 3072 : phase == 1 ? 3584 : phase == 2 ? 3840 : 4096;
+        for (int phase = 0; phase < 3; phase++) {
+            const int end = phase == 0 ? 3584 : phase == 1 ? 3968 : 4096;
             if (phase == 1) __builtin_amdgcn_s_setprio(2);
             else if (phase == 2) __builtin_amdgcn_s_setprio(1);
-            else if (phase == 3) __builtin_amdgcn_s_setprio(0);
 #pragma unroll 1
             for (; it < end; it++) {
                 sha1_84(MI, u, x);
