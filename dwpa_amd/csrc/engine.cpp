@@ -583,13 +583,12 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
             bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, row0 + i, j - i, 0});
         i = j;
     }
-    // attempt-parallel buckets: pad = the segment's first wave in its launch (ceil(count * natt / (64 * ATT_ITEMS))
-    // waves each)
+    // attempt-parallel buckets: pad = the segment's first wave in its launch (ceil(count * natt / 64) waves each)
     uint32_t nwaves[8] = {0}, kwords = 0, kstride = 0;
     for (int k = 4; k < 8; k++) {
         for (SegDev& sg : bucket[k]) {
             sg.pad = nwaves[k];
-            nwaves[k] += (uint32_t)(((uint64_t)sg.count * tb.lines[sg.line].natt + 64 * ATT_ITEMS - 1) / (64 * ATT_ITEMS));
+            nwaves[k] += (uint32_t)(((uint64_t)sg.count * tb.lines[sg.line].natt + 63) / 64);
         }
         if (!bucket[k].empty()) {
             kwords = std::max(kwords, eapol_key_words(1u << (k & 3)));

@@ -433,9 +433,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
 // the attempt (HMAC key midstates, PRF prefix: EapolKey) once per pair into a SoA scratch array, word w of pair
 // (segment i, key k) at keys[w * kstride + 64 i + k].
 //
-// k_verify_att: the (key, attempt) items of a segment are laid out key-major and cut into waves of 64 x ATT_ITEMS,
-// so every lane runs ATT_ITEMS attempts (one per pass) and a wave ends only where the segment does (segs[i].pad =
-// the segment's first wave within the launch).  A wave spans at most two keys (natt >= ATT_PARALLEL_MIN = 64); each lane loads its key's
+// k_verify_att: the (key, attempt) items of a segment are laid out key-major and cut into waves of 64 lanes, so
+// every lane runs one attempt and a wave ends only where the segment does (segs[i].pad = the segment's first wave
+// within the launch).  A wave spans at most two keys (natt >= ATT_PARALLEL_MIN = 64); each lane loads its key's
 // EapolKey.  One wave per key with 64 attempts per pass left 59 of 64 lanes idle in the fifth pass of a 261-attempt
 // list and recomputed the key state in every wave; here no lane idles before the segment's last wave.  Every
 // matching attempt is reported (at most two per key: one BE, one LE value can equal the true nonce); the host
@@ -501,37 +501,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
     const uint32_t segi = lo;
     const SegDev sg = segs[segi];
     const LineDev L = lines[sg.line];
-    // ATT_ITEMS passes over 64 consecutive items each: a pass spans at most two keys, as before
-#pragma unroll 1
-    for (uint32_t r = 0; r < ATT_ITEMS; r++) {
-        const uint32_t item = ((gw - sg.pad) * ATT_ITEMS + r) * 64 + lane;
-        const uint32_t k = item / L.natt, a = item - k * L.natt;
-        const bool active = k < sg.count;
-        if (!__any(active)) break;                      // past the segment's last item
-        const uint32_t kk = active ? k : sg.count - 1;  // idle lanes of the segment's last pass repeat a real key
-        const uint32_t slot = sg.slot + kk;
-        const uint64_t cand = ids ? ids[slot] : (uint64_t)slot;
-        EapolKey K;
-        const uint32_t* kp = keys + (size_t)segi * 64 + kk;
-        if ((VC & VC_KV3) && L.keyver == 3) {
+    const uint32_t item = (gw - sg.pad) * 64 + lane;
+    const uint32_t k = item / L.natt, a = item - k * L.natt;
+    const bool active = k < sg.count;
+    const uint32_t kk = active ? k : sg.count - 1;  // idle lanes of the segment's last wave repeat a real key
+    const uint32_t slot = sg.slot + kk;
+    const uint64_t cand = ids ? ids[slot] : (uint64_t)slot;
+    EapolKey K;
+    const uint32_t* kp = keys + (size_t)segi * 64 + kk;
+    if ((VC & VC_KV3) && L.keyver == 3) {
 #pragma unroll
-            for (int w = 0; w < 8; w++) {
-                K.op2[w] = kp[(size_t)w * kstride];
-                K.pre2[w] = kp[(size_t)(8 + w) * kstride];
-            }
-        } else {
-#pragma unroll
-            for (int w = 0; w < 5; w++) {
-                K.op1[w] = kp[(size_t)w * kstride];
-                K.pre1[w] = kp[(size_t)(5 + w) * kstride];
-            }
+        for (int w = 0; w < 8; w++) {
+            K.op2[w] = kp[(size_t)w * kstride];
+            K.pre2[w] = kp[(size_t)(8 + w) * kstride];
         }
-        const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
-        uint32_t mic[4];
-        eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + (active ? a : 0u)], te, mic);
-        const bool found = active && mic_match(L, mic);
-        report_hits(found, lane, cand, sg.line, a, pmk + slot, cap, hits, hitcnt, hitcap);
+    } else {
+#pragma unroll
+        for (int w = 0; w < 5; w++) {
+            K.op1[w] = kp[(size_t)w * kstride];
+            K.pre1[w] = kp[(size_t)(5 + w) * kstride];
+        }
     }
+    const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
+    uint32_t mic[4];
+    eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic);
+    const bool found = active && mic_match(L, mic);
+    report_hits(found, lane, cand, sg.line, a, pmk + slot, cap, hits, hitcnt, hitcap);
 }
 
 // ------------------------------------------------------------------------------------------------

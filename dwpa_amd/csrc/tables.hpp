@@ -62,10 +62,6 @@ inline uint32_t verify_class(const LineDev& L) {
 }
 // attempt-parallel verification (one wave = one key x 64 attempts) pays off once a list has this many attempts
 constexpr uint32_t ATT_PARALLEL_MIN = 64;
-// (key, attempt) items per lane of the attempt-parallel verifier: a wave covers 64 x ATT_ITEMS consecutive items in
-// ATT_ITEMS passes.  With one item per lane a wave lived ~60 us, and the dispatcher kept only ~4.4 of 8 waves per
-// SIMD resident (PMC SQ_WAVE_CYCLES, profiles/r02/pmc_c5): the kernels issued VALU at ~50 % of the SIMDs' rate.
-constexpr uint32_t ATT_ITEMS = 4;
 
 // One wave (64 lanes) verifies up to 64 consecutive candidate slots against one line.
 struct SegDev {
