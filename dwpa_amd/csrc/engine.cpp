@@ -114,6 +114,7 @@ struct Slot {
     uint32_t job;
     uint32_t ordinal;         // index among the job's non-null keys
     const std::string* essid;
+    uint64_t hash;            // hash_bytes(key): computed where the key is first read (dedup never re-reads it)
     bool pbkdf2;              // false: PMK supplied by the caller
 };
 
@@ -372,25 +373,18 @@ static uint32_t head_pmks(uint32_t nu) {
 // Derive the PMKs of slots [b, e) into batch.pmk (slot order) and their key ordinals into batch.ids.  Unique
 // (ESSID, key) pairs are derived once, all ESSIDs in one PBKDF2 launch (server batches fan one key out to every
 // net of an ESSID, common.php:879-902); each slot then gathers its PMK from them or from the caller's $pmk
-// (common.php:178).  Slots arrive grouped by ESSID.  The uploads are queued ahead of the launches: a pageable
+// (common.php:178).  Slots arrive grouped by ESSID: `runs` holds the starts of the ESSID runs relative to b plus
+// n = e - b, and keybytes the key bytes of the range.  The uploads are queued ahead of the launches: a pageable
 // upload queued behind a running kernel would block the host until that kernel ends.
 static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
-                        const std::vector<const uint8_t*>& job_pmk, DeriveStage& st) {
+                        const std::vector<const uint8_t*>& job_pmk, const std::vector<uint32_t>& runs,
+                        size_t keybytes, DeriveStage& st) {
     PhaseTrace tr;
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
     RCHK(d.batch.reserve(n, 2 * n + 64));  // attempt-parallel verify: <= 2 matching attempts per (key, line)
-    // ESSID runs of this chunk (slots arrive grouped by ESSID)
-    std::vector<uint32_t> runs{0};
-    size_t keybytes = 0, saltwords = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        keybytes += slots[b + i].key.size();
-        if (i && slots[b + i].essid != slots[b + i - 1].essid && *slots[b + i].essid != *slots[b + i - 1].essid)
-            runs.push_back(i);
-    }
-    runs.push_back(n);
+    size_t saltwords = 0;
     const size_t nruns = runs.size() - 1;
-    tr.mark("  runs");
     for (size_t r = 0; r < nruns; r++)  // count word + [2][nblk][16], nblk = SHA-1 blocks of ESSID || INT(i) || pad
         saltwords += 1 + 32 * ((slots[b + runs[r]].essid->size() + 4 + 9 + 63) / 64);
     // pinned staging, sized by upper bounds: <= n unique keys, <= keybytes key bytes, <= n caller PMKs
@@ -427,7 +421,7 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
             uint32_t cur_ref = UINT32_MAX;
             for (uint32_t i = i0; i < i1; i++) {
                 const Slot& sl = slots[b + i];
-                if (i + 16 < i1) __builtin_prefetch(slots[b + i + 16].key.data());
+                st.ids[i] = sl.ordinal;  // selects the PHP attempt list of the key
                 if (!sl.pbkdf2) {
                     const uint8_t* p = job_pmk[sl.job];
                     st.src[i] = GATHER_CALLER | (uint32_t)(P.cpmk.size() / 8);
@@ -443,7 +437,7 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
                     P.spool.push_back(nb);
                     P.spool.insert(P.spool.end(), sb.begin(), sb.end());
                 }
-                const uint64_t h = hash_bytes(sl.key.data(), sl.key.size(), 0);
+                const uint64_t h = sl.hash;
                 size_t pos = h & (tcap - 1);
                 uint32_t u;
                 while ((u = table[pos]) != UINT32_MAX && !(uhash[u - u0] == h && P.ukeys[u] == sl.key))
@@ -498,8 +492,6 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     });
     st.off[nu] = nbytes;
     tr.mark("  concat");
-    // ids = key ordinals (select the PHP attempt list of each key)
-    for (uint32_t i = 0; i < n; i++) st.ids[i] = slots[b + i].ordinal;
 
     RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
     // head = unique PMKs [0, nh); unique ids are numbered in first-occurrence slot order, so slots [0, split) only
@@ -678,6 +670,8 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     std::vector<const uint8_t*> job_pmk(njobs, nullptr);
     std::vector<std::vector<std::string_view>> keys(njobs);
     std::vector<std::vector<uint32_t>> key_index(njobs);
+    std::vector<std::vector<uint64_t>> key_hash(njobs);  // hash_bytes of each key, taken while its bytes are in cache
+    std::vector<size_t> job_bytes(njobs, 0);
     const size_t TP = host_threads(njobs, 64);
     std::vector<std::deque<std::string>> unhexed(TP);  // decoded $HEX[] keys (stable addresses), per thread
     parallel_for(TP, [&](size_t t) {
@@ -694,6 +688,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         if (!line_can_match(parsed[j])) continue;  // PMKID/MIC shorter than 16 bytes never verifies
         keys[j].reserve(jobs[j].nkeys);
         key_index[j].reserve(jobs[j].nkeys);
+        key_hash[j].reserve(jobs[j].nkeys);
         for (size_t k = 0; k < jobs[j].nkeys; k++) {
             // caller keys are scattered (one PHP string / Python bytes object each): prefetch ahead
             if (k + 16 < jobs[j].nkeys && jobs[j].keys[k + 16].ptr) __builtin_prefetch(jobs[j].keys[k + 16].ptr);
@@ -706,6 +701,8 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
             }
             keys[j].push_back(key);
             key_index[j].push_back((uint32_t)k);
+            key_hash[j].push_back(hash_bytes(key.data(), key.size(), 0));
+            job_bytes[j] += key.size();
         }
         job_pmk[j] = jobs[j].pmk;
       }
@@ -742,7 +739,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
             size_t i = gbase[g];
             for (uint32_t j : by_essid[g])
                 for (uint32_t o = 0; o < keys[j].size(); o++)
-                    slots[i++] = {keys[j][o], j, o, &parsed[j].essid, !(o == 0 && job_pmk[j])};
+                    slots[i++] = {keys[j][o], j, o, &parsed[j].essid, key_hash[j][o], !(o == 0 && job_pmk[j])};
         }
     });
     tr.mark("slots");
@@ -751,10 +748,24 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     TableBuilder tb;
     std::vector<HitDev> hits;
     const size_t chunk = default_batch();
+    std::vector<size_t> gbytes(by_essid.size(), 0);
+    for (size_t g = 0; g < by_essid.size(); g++)
+        for (uint32_t j : by_essid[g]) gbytes[g] += job_bytes[j];
     for (size_t b = 0; b < nslots; b += chunk) {
         const size_t e = std::min(nslots, b + chunk);
+        // the ESSID runs of [b, e) are the groups' slot ranges clipped to it
+        std::vector<uint32_t> runs{0};
+        size_t keybytes = 0;
+        for (size_t g = 0; g < by_essid.size(); g++) {
+            if (gbase[g + 1] <= b || gbase[g] >= e) continue;
+            if (gbase[g] > b) runs.push_back((uint32_t)(gbase[g] - b));
+            keybytes += gbase[g] >= b && gbase[g + 1] <= e ? gbytes[g] : 0;
+            if (gbase[g] < b || gbase[g + 1] > e)  // a group cut by the chunk: count its bytes inside
+                for (size_t i = std::max(b, gbase[g]); i < std::min(e, gbase[g + 1]); i++) keybytes += slots[i].key.size();
+        }
+        runs.push_back((uint32_t)(e - b));
         DeriveStage st;
-        RCHK(derive_slots(d, slots, b, e, job_pmk, st));
+        RCHK(derive_slots(d, slots, b, e, job_pmk, runs, keybytes, st));
         if (b == 0) {
             for (const auto& js : by_essid)
                 for (uint32_t j : js) job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
@@ -813,15 +824,19 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
     RCHK(device_stream(d));
     std::string es((const char*)essid, essid_len);
     std::vector<Slot> slots(nkeys);
-    for (size_t i = 0; i < nkeys; i++)
-        slots[i] = {keys[i].ptr ? std::string_view((const char*)keys[i].ptr, keys[i].len) : std::string_view(), 0,
-                    (uint32_t)i, &es, true};
+    for (size_t i = 0; i < nkeys; i++) {
+        const std::string_view k = keys[i].ptr ? std::string_view((const char*)keys[i].ptr, keys[i].len)
+                                               : std::string_view();
+        slots[i] = {k, 0, (uint32_t)i, &es, hash_bytes(k.data(), k.size(), 0), true};
+    }
     const size_t chunk = default_batch();
     std::vector<const uint8_t*> jp(1, nullptr);
     for (size_t b = 0; b < nkeys; b += chunk) {
         const size_t e = std::min(nkeys, b + chunk);
+        size_t keybytes = 0;
+        for (size_t i = b; i < e; i++) keybytes += slots[i].key.size();
         DeriveStage st;
-        RCHK(derive_slots(d, slots, b, e, jp, st));
+        RCHK(derive_slots(d, slots, b, e, jp, {0u, (uint32_t)(e - b)}, keybytes, st));
         RCHK(join_tail(d));
         std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
         HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, d.stream));

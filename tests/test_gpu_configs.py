@@ -135,6 +135,40 @@ def test_batch_fanout_dedup_and_mixed_salt_lengths():
     assert sum(1 for e in exp if e) >= len(jobs) // 2
 
 
+def test_batch_chunked_across_essid_groups():
+    """dwpa_init(batch=...) caps the slots per derive, so one call runs in several chunks whose boundaries cut
+    through ESSID groups (the per-group dedup and key-byte counts are then clipped to the chunk); the results
+    equal the oracle's job by job."""
+    import ctypes
+    import random
+    from dwpa_amd import _lib as L
+    rng = random.Random(93)
+    nets = [S.random_net(rng) for _ in range(5)]
+    jobs = []
+    for i in range(60):
+        essid, ap, sta, an, sn = nets[i % 5]
+        psk = S.fast_psk(rng)
+        line = (S.pmkid_line(psk, essid, rng.randbytes(6), sta) if i % 3 == 0 else
+                S.eapol_line(psk, essid, rng.randbytes(6), sta, rng.randbytes(32), rng.randbytes(32), 1 + i % 3,
+                             rng.randint(-4, 4), rng.choice(["LE", "BE"]), rng=rng))
+        keys = [S.fast_psk(rng, 8, 12) for _ in range(rng.randint(20, 90))]
+        keys[rng.randrange(len(keys))] = psk
+        keys += keys[:5]  # duplicates inside the job, and (same ESSID) across jobs
+        jobs.append((line, keys, False, rng.choice([8, 128])))
+    lib = L.load()
+    cfg = L.Config(ctypes.sizeof(L.Config), 0, 1000, 0)
+    assert lib.dwpa_init(ctypes.byref(cfg)) == 0
+    try:
+        got = dwpa_amd.check_batch(jobs)
+    finally:
+        cfg = L.Config(ctypes.sizeof(L.Config), 0, 0, 0)
+        lib.dwpa_init(ctypes.byref(cfg))
+    with ThreadPoolExecutor(THREADS) as ex:
+        exp = list(ex.map(lambda j: O.c_check_key_m22000(*j), jobs))
+    assert got == exp
+    assert all(exp)
+
+
 def test_pbkdf2_pmk_duplicate_keys():
     keys = [b"password", b"password", b"12345678", b"password", b"x" * 63, b"12345678"]
     essid = b"linksys"
