@@ -68,7 +68,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1 << 22, help="candidates per step per GPU")
+    ap.add_argument("--batch", type=int, default=1 << 24,
+                    help="candidates per step per GPU (one PBKDF2 launch of 64 wave rounds; 4M-candidate steps "
+                         "measured 0.2 %% slower per PMK: one launch tail per 16 rounds, profiles/r02/batch_size)")
     ap.add_argument("--dict-words", type=int, default=DICT_WORDS)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -209,10 +211,10 @@ def build_c3(args, local, S, Scan, Dictionary):
                 lines.append(S.pmkid_line(psk, essid, rng.randbytes(6), sta))
             else:
                 lines.append(S.eapol_line(psk, essid, ap, sta, an, sn, 2, rng.randint(-3, 3), "LE", rng=rng))
-    # one step = 4 x args.batch PMKs spread over every ESSID: 4*batch/E candidates x E ESSID groups, derived by
+    # one step = args.batch PMKs spread over every ESSID: batch/E candidates x E ESSID groups, derived by
     # multi-group PBKDF2 launches (dwpa_scan_run).  Rule filtering makes the per-step count data-dependent, so the
-    # last wave round of each launch is partial; 4x the C2 step keeps that tail near 2 %.
-    w.B = max(len(rules) + 63, 4 * args.batch // max(1, args.essids)) // 64 * 64
+    # last wave round of each launch is partial; a 16M-candidate step keeps that tail near 2 %.
+    w.B = max(len(rules) + 63, args.batch // max(1, args.essids)) // 64 * 64
     w.scans = [Scan(lines, device=local, nc=NC, nc_mode=NC_MODE, batch=w.B) for _ in range(args.pipeline)]
     w.nrules = [sc.set_rules("\n".join(rules)) for sc in w.scans][0]
     w.words_per_step = max(1, w.B // w.nrules)

@@ -328,7 +328,6 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     std::vector<std::thread> th;
     if (rc >= 0)
         for (size_t k = 0; k < G; k++) {
-            DevWork& w = *work[k];
             th.emplace_back([&, k] {  // stager
                 DevWork& w = *work[k];
                 for (int slot = 0;; slot ^= 1) {
@@ -387,7 +386,6 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
                     }
                 }
             });
-            (void)w;
         }
     for (auto& t : th) t.join();
     source.cancel();
