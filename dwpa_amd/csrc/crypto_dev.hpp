@@ -437,16 +437,9 @@ constexpr AesTables make_aes_tables() {
 }
 __constant__ static const AesTables AES_TABLES = make_aes_tables();
 
-// Table lookups go through aes_te<SH>: te[x << SH].  SH = 0 reads a plain 256-entry table; SH = 6 reads a
-// lane-sliced copy (entry x of lane l at word 64 x + l, te pre-offset by l), so the 64 lanes of a wave always hit 64
-// different LDS banks (kernels.hip aes_table_lds).
-template <int SH>
-__device__ __forceinline__ uint32_t aes_te(const uint32_t* te, uint32_t x) { return te[x << SH]; }
-template <int SH = 0>
-__device__ __forceinline__ uint32_t aes_sb(const uint32_t* te, uint32_t x) { return (aes_te<SH>(te, x & 0xff) >> 8) & 0xff; }
+__device__ __forceinline__ uint32_t aes_sb(const uint32_t* te, uint32_t x) { return (te[x & 0xff] >> 8) & 0xff; }
 
 // rk[44] from a 16-byte key given as 4 big-endian words
-template <int SH = 0>
 __device__ __forceinline__ void aes128_expand(const uint32_t* te, const uint32_t key[4], uint32_t rk[44]) {
     rk[0] = key[0]; rk[1] = key[1]; rk[2] = key[2]; rk[3] = key[3];
     uint32_t rcon = 0x01;
@@ -454,8 +447,7 @@ __device__ __forceinline__ void aes128_expand(const uint32_t* te, const uint32_t
     for (int i = 4; i < 44; i++) {
         uint32_t t = rk[i - 1];
         if ((i & 3) == 0) {
-            t = (aes_sb<SH>(te, t >> 16) << 24) | (aes_sb<SH>(te, t >> 8) << 16) | (aes_sb<SH>(te, t) << 8) |
-                aes_sb<SH>(te, t >> 24);
+            t = (aes_sb(te, t >> 16) << 24) | (aes_sb(te, t >> 8) << 16) | (aes_sb(te, t) << 8) | aes_sb(te, t >> 24);
             t ^= rcon << 24;
             rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x11b : 0);
         }
@@ -463,23 +455,20 @@ __device__ __forceinline__ void aes128_expand(const uint32_t* te, const uint32_t
     }
 }
 
-template <int SH = 0>
 __device__ __forceinline__ void aes128_encrypt(const uint32_t* te, const uint32_t rk[44], uint32_t s[4]) {
     uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
-#define DWPA_TE(x) aes_te<SH>(te, (x))
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        uint32_t t0 = DWPA_TE(s0 >> 24) ^ rotr(DWPA_TE((s1 >> 16) & 0xff), 8) ^ rotr(DWPA_TE((s2 >> 8) & 0xff), 16) ^ rotr(DWPA_TE(s3 & 0xff), 24) ^ rk[4 * r];
-        uint32_t t1 = DWPA_TE(s1 >> 24) ^ rotr(DWPA_TE((s2 >> 16) & 0xff), 8) ^ rotr(DWPA_TE((s3 >> 8) & 0xff), 16) ^ rotr(DWPA_TE(s0 & 0xff), 24) ^ rk[4 * r + 1];
-        uint32_t t2 = DWPA_TE(s2 >> 24) ^ rotr(DWPA_TE((s3 >> 16) & 0xff), 8) ^ rotr(DWPA_TE((s0 >> 8) & 0xff), 16) ^ rotr(DWPA_TE(s1 & 0xff), 24) ^ rk[4 * r + 2];
-        uint32_t t3 = DWPA_TE(s3 >> 24) ^ rotr(DWPA_TE((s0 >> 16) & 0xff), 8) ^ rotr(DWPA_TE((s1 >> 8) & 0xff), 16) ^ rotr(DWPA_TE(s2 & 0xff), 24) ^ rk[4 * r + 3];
+        uint32_t t0 = te[s0 >> 24] ^ rotr(te[(s1 >> 16) & 0xff], 8) ^ rotr(te[(s2 >> 8) & 0xff], 16) ^ rotr(te[s3 & 0xff], 24) ^ rk[4 * r];
+        uint32_t t1 = te[s1 >> 24] ^ rotr(te[(s2 >> 16) & 0xff], 8) ^ rotr(te[(s3 >> 8) & 0xff], 16) ^ rotr(te[s0 & 0xff], 24) ^ rk[4 * r + 1];
+        uint32_t t2 = te[s2 >> 24] ^ rotr(te[(s3 >> 16) & 0xff], 8) ^ rotr(te[(s0 >> 8) & 0xff], 16) ^ rotr(te[s1 & 0xff], 24) ^ rk[4 * r + 2];
+        uint32_t t3 = te[s3 >> 24] ^ rotr(te[(s0 >> 16) & 0xff], 8) ^ rotr(te[(s1 >> 8) & 0xff], 16) ^ rotr(te[s2 & 0xff], 24) ^ rk[4 * r + 3];
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-#undef DWPA_TE
-    s[0] = (aes_sb<SH>(te, s0 >> 24) << 24 | aes_sb<SH>(te, s1 >> 16) << 16 | aes_sb<SH>(te, s2 >> 8) << 8 | aes_sb<SH>(te, s3)) ^ rk[40];
-    s[1] = (aes_sb<SH>(te, s1 >> 24) << 24 | aes_sb<SH>(te, s2 >> 16) << 16 | aes_sb<SH>(te, s3 >> 8) << 8 | aes_sb<SH>(te, s0)) ^ rk[41];
-    s[2] = (aes_sb<SH>(te, s2 >> 24) << 24 | aes_sb<SH>(te, s3 >> 16) << 16 | aes_sb<SH>(te, s0 >> 8) << 8 | aes_sb<SH>(te, s1)) ^ rk[42];
-    s[3] = (aes_sb<SH>(te, s3 >> 24) << 24 | aes_sb<SH>(te, s0 >> 16) << 16 | aes_sb<SH>(te, s1 >> 8) << 8 | aes_sb<SH>(te, s2)) ^ rk[43];
+    s[0] = (aes_sb(te, s0 >> 24) << 24 | aes_sb(te, s1 >> 16) << 16 | aes_sb(te, s2 >> 8) << 8 | aes_sb(te, s3)) ^ rk[40];
+    s[1] = (aes_sb(te, s1 >> 24) << 24 | aes_sb(te, s2 >> 16) << 16 | aes_sb(te, s3 >> 8) << 8 | aes_sb(te, s0)) ^ rk[41];
+    s[2] = (aes_sb(te, s2 >> 24) << 24 | aes_sb(te, s3 >> 16) << 16 | aes_sb(te, s0 >> 8) << 8 | aes_sb(te, s1)) ^ rk[42];
+    s[3] = (aes_sb(te, s3 >> 24) << 24 | aes_sb(te, s0 >> 16) << 16 | aes_sb(te, s1 >> 8) << 8 | aes_sb(te, s2)) ^ rk[43];
 }
 
 // CMAC subkey doubling on a 128-bit big-endian value held in 4 words

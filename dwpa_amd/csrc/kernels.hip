@@ -130,14 +130,6 @@ __global__ void k_set_pmk(uint32_t* __restrict__ pmk, uint32_t cap, uint32_t slo
 // ------------------------------------------------------------------------------------------------
 // stage 3: verification.  One wave = one segment = up to 64 slots x one line (line data wave-uniform).
 // ------------------------------------------------------------------------------------------------
-// AES T-table for the keyver-3 classes, lane-sliced in LDS: entry x of lane l at word 64 x + l, so the 64 lanes of a
-// wave always read 64 different banks.  The plain 256-entry table put 68 % of the kernel's LDS cycles into bank-
-// conflict stalls on random S-box indices (PMC SQ_LDS_BANK_CONFLICT vs SQ_LDS_IDX_ACTIVE, profiles/r02/pmc_c5_lds).
-// 64 KiB per workgroup: the keyver-3 launches use 1024-thread workgroups, one per CU, 4 waves per SIMD.
-constexpr int AES_SLICE_SH = 6;
-constexpr uint32_t vc_lds_words(uint32_t vc) { return (vc & VC_KV3) ? (256u << AES_SLICE_SH) : 1u; }
-constexpr uint32_t vc_block(uint32_t vc) { return (vc & VC_KV3) ? 1024u : 256u; }
-
 // KW blocks (tables.hpp): wave-uniform blocks with host-expanded schedules, read with scalar loads.
 __device__ __forceinline__ void sha1_blocks_kw(uint32_t st[5], const uint32_t* __restrict__ kw, uint32_t nblk) {
     for (uint32_t b = 0; b < nblk; b++) sha1_compress_kw(st, kw + b * SHA1_KW_WORDS);
@@ -286,9 +278,9 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         sha256_compress(ptk, m);
         // AES-128-CMAC(KCK = PTK[0..15], EAPOL)  (common.php:72-112)
         uint32_t rk[44];
-        aes128_expand<AES_SLICE_SH>(te, ptk, rk);
+        aes128_expand(te, ptk, rk);
         uint32_t Lb[4] = {0, 0, 0, 0}, K1[4], K2[4];
-        aes128_encrypt<AES_SLICE_SH>(te, rk, Lb);
+        aes128_encrypt(te, rk, Lb);
         cmac_dbl(Lb, K1);
         cmac_dbl(K1, K2);
         uint32_t c[4] = {0, 0, 0, 0};
@@ -301,7 +293,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
                 if (last) v ^= L.cmac_complete ? K1[k] : K2[k];
                 c[k] ^= v;
             }
-            aes128_encrypt<AES_SLICE_SH>(te, rk, c);
+            aes128_encrypt(te, rk, c);
         }
         mic[0] = c[0]; mic[1] = c[1]; mic[2] = c[2]; mic[3] = c[3];
     }
@@ -340,21 +332,21 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
 template <uint32_t VC>
 __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     if constexpr ((VC & VC_KV3) != 0) {
-        for (uint32_t k = threadIdx.x; k < (256u << AES_SLICE_SH); k += blockDim.x)
-            te[k] = AES_TABLES.te0[k >> AES_SLICE_SH];
+        for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) te[k] = AES_TABLES.te0[k];
         __syncthreads();
     }
-    return te + (threadIdx.x & 63);
+    return te;
 }
 
 // Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
 // wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
-// Occupancy target per class: PMKID, keyver 1 and keyver 2 fit 64 VGPRs (8 waves/SIMD; keyver 2 since its uniform
-// blocks are KW blocks); keyver 3 keeps 44 AES round-key registers and its 1024-thread workgroups (4 waves/SIMD).
-constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? 4 : 8; }
+// Occupancy target per class: PMKID and keyver 1 fit 64 VGPRs (8 waves/SIMD); keyver 2 is held at 64 too and spills
+// 9 VGPRs, which measured level with a 6-wave, spill-free build (profiles/r01/verify_waves_ab); keyver 3 keeps 44 AES
+// round-key registers (2 waves).
+constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? 2 : 8; }
 
 template <uint32_t VC>
-__global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify(
                                                 const uint32_t* __restrict__ pmk, uint32_t cap,
                                                 const uint64_t* __restrict__ ids, const uint32_t* __restrict__ counter,
                                                 const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t line_base,
@@ -363,7 +355,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                 const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                 uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
-    __shared__ uint32_t te_lds[vc_lds_words(VC)];
+    __shared__ uint32_t te_lds[256];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -485,7 +477,7 @@ __global__ __launch_bounds__(256) void k_eapol_keys(const uint32_t* __restrict__
 }
 
 template <uint32_t VC>
-__global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify_att(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify_att(
                                                     const uint32_t* __restrict__ pmk, uint32_t cap,
                                                     const uint64_t* __restrict__ ids,
                                                     const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t nwaves,
@@ -494,7 +486,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                     const uint32_t* __restrict__ pool,
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                     uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
-    __shared__ uint32_t te_lds[vc_lds_words(VC)];
+    __shared__ uint32_t te_lds[256];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
@@ -603,10 +595,10 @@ hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids,
                          uint32_t pstride) {
     if (nsegs == 0 || nlines == 0) return hipSuccess;
     if (!pstride) pstride = cap;
+    const dim3 grid(cdiv(nsegs, 4), segs ? 1 : nlines);
 #define DWPA_LAUNCH_VERIFY(V)                                                                                  \
-    hipLaunchKernelGGL(k_verify<V>, dim3(cdiv(nsegs, vc_block(V) / 64), segs ? 1 : nlines), dim3(vc_block(V)), 0, s, \
-                       pmk, cap, ids, counter, segs, nsegs, line_base, line_list, line_poff, pstride, lines, pool,     \
-                       atts, hits, hitcnt, hitcap)
+    hipLaunchKernelGGL(k_verify<V>, grid, dim3(256), 0, s, pmk, cap, ids, counter, segs, nsegs, line_base,      \
+                       line_list, line_poff, pstride, lines, pool, atts, hits, hitcnt, hitcap)
     DWPA_VC_DISPATCH(vc, DWPA_LAUNCH_VERIFY)
 #undef DWPA_LAUNCH_VERIFY
     return hipGetLastError();
@@ -623,8 +615,7 @@ hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* 
 #define DWPA_LAUNCH_VERIFY_ATT(V)                                                                                 \
     hipLaunchKernelGGL(k_eapol_keys<V>, dim3(cdiv((uint64_t)nsegs * 64, 256)), dim3(256), 0, s, pmk, cap, segs,   \
                        nsegs, lines, pool, keys, kstride);                                                         \
-    hipLaunchKernelGGL(k_verify_att<V>, dim3(cdiv(nwaves, vc_block(V) / 64)), dim3(vc_block(V)), 0, s, pmk, cap, ids, \
-                       segs, nsegs, nwaves,                                                                       \
+    hipLaunchKernelGGL(k_verify_att<V>, dim3(cdiv(nwaves, 4)), dim3(256), 0, s, pmk, cap, ids, segs, nsegs, nwaves, \
                        keys, kstride, lines, pool, atts, hits, hitcnt, hitcap)
     DWPA_VC_DISPATCH(vc & ~VC_PMKID, DWPA_LAUNCH_VERIFY_ATT)
 #undef DWPA_LAUNCH_VERIFY_ATT
