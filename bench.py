@@ -85,6 +85,9 @@ def parse():
                          "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
                          "dwpa_crack_files from a gz dictionary on disk (the help_crack client path)")
     ap.add_argument("--essids", type=int, default=1000, help="c3: number of ESSIDs (BASELINE: 1000)")
+    ap.add_argument("--scan-run", action="store_true",
+                    help="c2/c4: derive + verify through dwpa_scan_run (the multi-group kernel C3 uses) instead of "
+                         "the per-group calls (A/B of the two PBKDF2 entry points)")
     ap.add_argument("--short-words", action="store_true",
                     help="c2files: lengths geometric(0.3)+6 so ~30 %% of the words are shorter than 8 and dropped "
                          "by the m22000 filter (as in real wordlists); PMK/s counts only 8..63-byte words")
@@ -298,7 +301,7 @@ def main():
         sc, stream = w.scans[k], streams[k]
         hs = stream.handle
         cnt = w.load(i, hs, sc)
-        if w.groups > 1:
+        if w.groups > 1 or args.scan_run:
             # all ESSID groups per launch; the events bracket PBKDF2 + verify (conservative for the roofline)
             if ev is not None:
                 ev[0].record(stream)
