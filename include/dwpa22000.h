@@ -97,7 +97,9 @@ typedef struct {
 
 /* ---- library ------------------------------------------------------------------------------------------------ */
 int dwpa_abi_version(void);
-/* Optional: select devices / batch size.  Lazy and idempotent; every entry point initialises on first use. */
+/* Optional: select devices / batch size for the whole process (check path, PBKDF2 and scan calls that follow).
+ * Lazy and idempotent; every entry point initialises on first use.  dwpa_crack_files' own cfg applies to that call
+ * only and leaves this selection unchanged. */
 int dwpa_init(const dwpa_config *cfg);
 int dwpa_device_count(void);
 const char *dwpa_strerror(int code);
@@ -140,7 +142,10 @@ int dwpa_hash_m22000(const char *line, size_t line_len, uint8_t out[16]);
 /* Reads hash_file (one m22000 line per line), the dictionaries (plain text or .gz, one word per line, $HEX[]
  * decoded), applies rules_file (hashcat rule syntax, may be NULL) and writes one outfile record per cracked line:
  *   <PMKID|MIC hex>:<MAC_AP hex>:<MAC_STA hex>:<ESSID>:<PSK>   (ESSID/PSK as $HEX[..] when not printable)
- * Returns a hashcat exit code (DWPA_RC_*).  nonce_error_corrections as --nonce-error-corrections. */
+ * Returns a hashcat exit code (DWPA_RC_*).  nonce_error_corrections as --nonce-error-corrections.  cfg (nullable):
+ * device_mask / batch / nc_mode for this call only (device_mask 0 = the dwpa_init selection, default all devices).
+ * Lines that can never match (PMKID or MIC shorter than 16 bytes, which hashcat does not load) do not count
+ * towards "every hashline cracked".  DWPA_CRACK_SHARDS_PER_DEVICE=k runs k shard workers per device. */
 int dwpa_crack_files(const char *hash_file, const char *const *dicts, size_t ndicts, const char *rules_file,
                      int nonce_error_corrections, const char *out_file, const dwpa_config *cfg);
 
