@@ -106,7 +106,8 @@ const char *dwpa_strerror(int code);
 void dwpa_shutdown(void);
 
 /* ---- server-side check: PHP FFI replacement of check_key_m22000 (web/common.php:157-307) -------------------- */
-/* Returns DWPA_HIT and fills *out, DWPA_MISS, or a negative code (all of which PHP reads as False). */
+/* Returns DWPA_HIT and fills *out, DWPA_MISS, or a negative code (php/dwpa22000.php: MISS and -1..-4 -> False,
+ * codes <= -10 -> the original PHP check_key_m22000, never False). */
 int dwpa_check_m22000(const char *line, size_t line_len, const dwpa_bytes *keys, size_t nkeys,
                       const uint8_t *pmk /* nullable, 32 bytes */, int nc, dwpa_result *out);
 /* Bulk form (put_work's per-candidate loop, rkg.php's per-net loop): jobs grouped by ESSID internally so
