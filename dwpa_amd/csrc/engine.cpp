@@ -995,7 +995,7 @@ int scan_pbkdf2(dwpa_scan* sc, int group, void* stream) {
     if (!any) return 0;
     HIPCHK(launch_pbkdf2((const uint32_t*)sc->batch.mid.p, sc->batch_cap, 0, sc->batch_cap,
                          (const uint32_t*)sc->batch.counters.p, (const uint32_t*)sc->salt.p + g.salt_off, g.nsalt,
-                         (uint32_t*)sc->batch.pmk.p, as_stream(stream)));
+                         (uint32_t*)sc->batch.pmk.p, as_stream(stream), (uint32_t*)sc->batch.counters.p + 2));
     return 0;
 }
 

@@ -23,7 +23,7 @@ struct Batch {
     DevBuf pmk;       // [8][cap]  u32 PMKs
     DevBuf ids;       // [cap]     u64 candidate ids
     DevBuf hits;      // [hitcap]  HitDev
-    DevBuf counters;  // [0] loaded slots, [1] hit count
+    DevBuf counters;  // [0] loaded slots, [1] hit count, [2] PBKDF2 work-queue counter
     int reserve(uint32_t cap, uint32_t hitcap);
 };
 

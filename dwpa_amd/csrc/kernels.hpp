@@ -13,8 +13,9 @@ hipError_t launch_prep_dict(const uint64_t* off, const uint8_t* bytes, uint64_t 
 hipError_t launch_prep_numeric(uint64_t first, uint32_t count, uint32_t digits, uint32_t* mid, uint64_t* ids,
                                uint32_t cap, hipStream_t s);
 // product launch: issue-pass code object (pbkdf2_module.cpp); DWPA_PBKDF2_PLAIN=1 -> launch_pbkdf2_plain
+// work (nullable): a 4-byte device counter the work-queue kernel may use (zeroed here before the launch)
 hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
-                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s);
+                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s, uint32_t* work = nullptr);
 hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count,
                                const uint32_t* counter, const uint32_t* salt, uint32_t nsalt, uint32_t* pmk,
                                hipStream_t s);

@@ -101,6 +101,34 @@ __device__ __forceinline__ void pbkdf2_body(const uint32_t* __restrict__ mid, ui
     store_block(pmk, cap, s, blk, t);
 }
 
+// Work-queue form of pbkdf2_body: a fixed grid of 8 waves per SIMD, each wave taking (output block, 64-slot) items
+// from the counter at `work` (zeroed before the launch) until they run out.  Workgroups go to the 8 XCDs round-robin
+// whatever their progress, so a regular launch ends with its slowest XCD; here every wave keeps taking items, so a
+// faster XCD takes more of them.  Every wave exits once the counter passes the item count.
+__device__ __forceinline__ void pbkdf2_body_queue(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base,
+                                                  uint32_t count, const uint32_t* __restrict__ counter,
+                                                  const uint32_t* __restrict__ salt, uint32_t nsalt,
+                                                  uint32_t* __restrict__ pmk, uint32_t* __restrict__ work) {
+    const uint32_t n = counter ? min(*counter, cap) : min(base + count, cap);
+    const uint32_t nitems = base < n ? 2u * ((n - base + 63u) / 64u) : 0u;
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll 1
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(work, 1u);
+        item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
+        if (item >= nitems) break;
+        const uint32_t blk = item & 1u;  // both output blocks of a slot range are taken back to back
+        const uint32_t s = base + (item >> 1) * 64u + lane;
+        if (s < n) {
+            uint32_t hi[5], ho[5], t[5];
+            load_mid(mid, cap, s, hi, ho);
+            pbkdf2_lane(hi, ho, salt + (size_t)blk * nsalt * 16, nsalt, t);
+            store_block(pmk, cap, s, blk, t);
+        }
+    }
+}
+
 // Many ESSIDs in one launch (server batches, common.php:902): slot s derives with the salt entry at
 // pool + sref[s] = {nsalt, [2 blocks][nsalt][16] words}.  Only the U_1 blocks differ per lane; the 4096 loop is
 // the same code as pbkdf2_body's.

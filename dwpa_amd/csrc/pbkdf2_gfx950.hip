@@ -51,3 +51,10 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     uint32_t pstride) {
     dwpa::pbkdf2_body_mg<true>(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride);
 }
+
+// Work-queue variant of k_pbkdf2_gfx950 (pbkdf2_dev.hpp pbkdf2_body_queue): XCD-balanced multi-round launches.
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_q(
+    const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* __restrict__ counter,
+    const uint32_t* __restrict__ salt, uint32_t nsalt, uint32_t* __restrict__ pmk, uint32_t* __restrict__ work) {
+    dwpa::pbkdf2_body_queue(mid, cap, base, count, counter, salt, nsalt, pmk, work);
+}

@@ -20,6 +20,7 @@ extern const size_t pbkdf2_gfx950_hsaco_size;
 struct Fns {
     hipFunction_t one, ms, mg;  // k_pbkdf2_gfx950 (one ESSID), _ms (per-slot salt), _mg (ESSID groups x batch)
     hipFunction_t one_p, ms_p, mg_p;  // the same with progress-ordered wave priority (pbkdf2_dev.hpp PRIO)
+    hipFunction_t one_q;              // k_pbkdf2_gfx950 as a work queue (pbkdf2_dev.hpp pbkdf2_body_queue)
     uint64_t level_lanes;       // lanes that give every SIMD of the device one wave: CUs x 4 SIMDs x 64
 };
 static std::mutex g_mod_mu;
@@ -79,6 +80,7 @@ static hipError_t tuned_functions(Fns* fn) {
     if ((e = hipModuleGetFunction(&fn->one_p, mod, "k_pbkdf2_gfx950_p")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->ms_p, mod, "k_pbkdf2_gfx950_ms_p")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->mg_p, mod, "k_pbkdf2_gfx950_mg_p")) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(&fn->one_q, mod, "k_pbkdf2_gfx950_q")) != hipSuccess) return e;
     int cus = 0;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     fn->level_lanes = (uint64_t)(cus > 0 ? cus : 256) * 4 * 64;
@@ -89,8 +91,14 @@ static hipError_t tuned_functions(Fns* fn) {
 // At most one wave per SIMD (both output blocks counted): latency-bound, the plain schedule is faster.
 static bool lone_waves(const Fns& fn, uint64_t pmks) { return !force_issue() && 2 * pmks <= fn.level_lanes; }
 
+// DWPA_PBKDF2_QUEUE=1: multi-round one-ESSID launches as the work-queue kernel (A/B switch)
+static bool use_queue() {
+    static const bool q = env_flag("DWPA_PBKDF2_QUEUE");
+    return q;
+}
+
 hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
-                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s) {
+                         const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s, uint32_t* work) {
     if (count == 0) return hipSuccess;
     if (use_plain()) return launch_pbkdf2_plain(mid, cap, base, count, counter, salt, nsalt, pmk, s);
     Fns fn;
@@ -99,6 +107,16 @@ hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint3
     // with a device counter the host only knows the upper bound min(count, cap - base)
     if (lone_waves(fn, std::min<uint64_t>(count, cap > base ? cap - base : 0)))
         return launch_pbkdf2_plain(mid, cap, base, count, counter, salt, nsalt, pmk, s);
+    const uint64_t pmks = std::min<uint64_t>(count, cap > base ? cap - base : 0);
+    if (work && use_queue() && !use_prio(fn, pmks)) {
+        // one resident round (8 waves per SIMD) that drains the item counter
+        e = hipMemsetAsync(work, 0, 4, s);
+        if (e != hipSuccess) return e;
+        void* qargs[] = {(void*)&mid, (void*)&cap, (void*)&base, (void*)&count, (void*)&counter,
+                         (void*)&salt, (void*)&nsalt, (void*)&pmk, (void*)&work};
+        const uint32_t blocks = (uint32_t)(8 * fn.level_lanes / 256);
+        return hipModuleLaunchKernel(fn.one_q, blocks, 1, 1, 256, 1, 1, 0, s, qargs, nullptr);
+    }
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&base, (void*)&count, (void*)&counter,
                     (void*)&salt, (void*)&nsalt, (void*)&pmk};
     const uint32_t wg = wg_size();
