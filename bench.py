@@ -91,6 +91,10 @@ def parse():
     ap.add_argument("--short-words", action="store_true",
                     help="c2files: lengths geometric(0.3)+6 so ~30 %% of the words are shorter than 8 and dropped "
                          "by the m22000 filter (as in real wordlists); PMK/s counts only 8..63-byte words")
+    ap.add_argument("--callers", type=int, default=1,
+                    help="c1/c5: concurrent callers (host threads, as PHP ZTS workers or a threaded server), each "
+                         "making the step's call on its own argument block; the library runs up to "
+                         "DWPA_CALLS_PER_DEVICE (default 2) calls per GPU at once.  value = all callers' PMKs / wall")
     return ap.parse_args()
 
 
@@ -447,21 +451,48 @@ def main_ffi(args, world, rank, local):
         jobs = S.c5_jobs()
         desc = ("C5: 250 PMKID + 250 x keyver 1/2/3 EAPOL lines (NC offsets 0..+-8, LE/BE) + 10 zero-PMK jobs, "
                 "202 keys per job, nc=128 (261 attempts), dwpa_check_batch per step (FFI, host buffers)")
-    batch = dwpa_amd.BatchJobs(jobs)
+    import threading
+    callers = max(1, args.callers)
+    batches = [dwpa_amd.BatchJobs(jobs) for _ in range(callers)]
+    batch = batches[0]
+    go = threading.Barrier(callers)  # the main thread is caller 0
+    errors = []
+
+    def caller(b):  # warmup, wait for the start, then args.steps calls back to back (ctypes drops the GIL)
+        try:
+            for _ in range(args.warmup):
+                b.run()
+            go.wait()
+            for _ in range(args.steps):
+                b.run()
+        except Exception as e:  # noqa: BLE001 -- reported below, the run fails
+            errors.append(e)
+            go.abort()
+
+    threads = [threading.Thread(target=caller, args=(b,)) for b in batches[1:]]
+    for t in threads:
+        t.start()
     for _ in range(args.warmup):
         batch.run()
     if world > 1:
         dist.barrier()
+    go.wait()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         batch.run()
+    for t in threads:
+        t.join()
     elapsed = time.perf_counter() - t0
+    if errors:
+        raise errors[0]
+    keys_all = float(batch.nkeys * args.steps * callers)
     if world > 1:
         dist.barrier()
-        elapsed, total = reduce_timing(dist, time.perf_counter() - t0, float(batch.nkeys * args.steps))
+        elapsed, total = reduce_timing(dist, time.perf_counter() - t0, keys_all)
     else:
-        total = float(batch.nkeys * args.steps)
+        total = keys_all
     got = batch.results()
+    same = all(b.results() == got for b in batches[1:])
     if args.workload == "c1":
         verified = bool(got[0]) and got[0][0] == psk and got[0][3] == S.pmk(psk, bytes.fromhex(line.split(b"*")[5].decode()))
     else:
@@ -478,6 +509,7 @@ def main_ffi(args, world, rank, local):
         with ThreadPoolExecutor(host_cpu()["threads_all"]) as ex:
             exact = sum(ex.map(hit_alone, hit_jobs))
         verified = exact == len(hit_jobs) and len(hit_jobs) >= 0.85 * len(jobs)
+    verified = verified and same
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -486,8 +518,8 @@ def main_ffi(args, world, rank, local):
             "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": desc, "jobs": len(jobs), "keys_per_step": batch.nkeys,
-                       "parallelism": f"replicas x{world}"},
+            "config": {"workload": desc, "jobs": len(jobs), "keys_per_step": batch.nkeys * callers,
+                       "callers": callers, "parallelism": f"replicas x{world}"},
             "roofline": None, "cpu_baseline": cpu, "hits_verified": verified,
             "hits": sum(1 for g in got if g),
             "hits_checked": "every hit's [PSK, NC, endian, PMK] re-derived by the CPU oracle" if args.workload == "c5"

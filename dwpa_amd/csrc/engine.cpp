@@ -139,10 +139,23 @@ static bool g_init = false;
 static int g_ndev = 0;
 static uint32_t g_mask = 0;
 static uint32_t g_batch = 0;
-static std::vector<std::unique_ptr<Device>> g_dev;
+static std::vector<std::unique_ptr<Device>> g_dev;  // call contexts: [device * calls_per_device() + k]
 static std::atomic<uint32_t> g_rr{0};
 
 static uint32_t default_batch() { return g_batch ? g_batch : (1u << 20); }
+
+// Check-path calls in flight per device (DWPA_CALLS_PER_DEVICE, 1..8, default 2).  Each call context has its own
+// streams and buffers, so concurrent callers (PHP ZTS threads, a threaded Python server) overlap on one GPU: one
+// call's host phases, lone-wave PBKDF2 remainder and verify run beside the next call's PBKDF2 head instead of
+// leaving SIMDs idle.  With one caller only context 0 is used.
+static int calls_per_device() {
+    static const int k = [] {
+        const char* e = getenv("DWPA_CALLS_PER_DEVICE");
+        const int v = e ? atoi(e) : 2;
+        return v < 1 ? 1 : v > 8 ? 8 : v;
+    }();
+    return k;
+}
 
 static int init_locked(const dwpa_config* cfg) {
     if (cfg) {
@@ -154,11 +167,12 @@ static int init_locked(const dwpa_config* cfg) {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DWPA_E_NODEV;
     g_ndev = n;
     g_dev.clear();
-    for (int d = 0; d < n; d++) {
-        auto dev = std::make_unique<Device>();
-        dev->id = d;
-        g_dev.push_back(std::move(dev));
-    }
+    for (int d = 0; d < n; d++)
+        for (int k = 0; k < calls_per_device(); k++) {
+            auto dev = std::make_unique<Device>();
+            dev->id = d;
+            g_dev.push_back(std::move(dev));
+        }
     g_init = true;
     return 0;
 }
@@ -639,18 +653,32 @@ static int collect_hits(Device& d, std::vector<HitDev>& hits_out) {
     return 0;
 }
 
+// A call context, locked: an idle one of the device with the fewest calls in flight (ties: round-robin from
+// g_rr; within a device the lowest context, so one caller keeps reusing context 0's buffers), else wait for the
+// first context of the next device in round-robin order.
 static Device* pick_device() {
     std::vector<int> act = active_devices();
     if (act.empty()) return nullptr;
-    // prefer an idle device, else round-robin
-    for (size_t k = 0; k < act.size(); k++) {
-        Device* d = g_dev[act[(g_rr + k) % act.size()]].get();
-        if (d->mu.try_lock()) {
-            g_rr++;
-            return d;
+    const int K = calls_per_device();
+    const uint32_t r0 = g_rr++;
+    for (int busy = 0; busy < K; busy++)  // first pass: devices with no call in flight, then one, ...
+        for (size_t k = 0; k < act.size(); k++) {
+            const int dev = act[(r0 + k) % act.size()];
+            int n_busy = 0;
+            Device* idle = nullptr;
+            for (int c = 0; c < K; c++) {
+                Device* d = g_dev[(size_t)dev * K + c].get();
+                if (d->mu.try_lock()) {
+                    if (!idle) idle = d;
+                    else d->mu.unlock();
+                } else {
+                    n_busy++;
+                }
+            }
+            if (idle && n_busy <= busy) return idle;
+            if (idle) idle->mu.unlock();
         }
-    }
-    Device* d = g_dev[act[g_rr++ % act.size()]].get();
+    Device* d = g_dev[(size_t)act[r0 % act.size()] * K].get();
     d->mu.lock();
     return d;
 }
@@ -1088,7 +1116,7 @@ int scan_run(dwpa_scan* sc, void* stream) {
         if ((uint64_t)ch.ngroups * cap > pstride || sc->mg_pmk.n < (size_t)PMK_WORDS * pstride * 4) return DWPA_E_ARG;
         HIPCHK(launch_pbkdf2_mg((const uint32_t*)sc->batch.mid.p, cap, (const uint32_t*)sc->batch.counters.p,
                                 ch.ngroups, (const uint32_t*)sc->salt.p, (const uint32_t*)sc->mg_gsalt.p + 2 * ch.g0,
-                                (uint32_t*)sc->mg_pmk.p, pstride, s));
+                                (uint32_t*)sc->mg_pmk.p, pstride, s, (uint32_t*)sc->batch.counters.p + 2));
         for (uint32_t c = 0; c < 4; c++)  // one launch per verify class (grid.y <= 65535 lines)
             for (uint32_t l = ch.cls[c]; l < ch.cls[c + 1]; l += 65535u) {
                 const uint32_t nl = std::min<uint32_t>(65535u, ch.cls[c + 1] - l);

@@ -39,7 +39,7 @@ hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* 
 // PMK word k of (c, slot) at pmk[k * pstride + c * cap + slot]
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
                             const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
-                            hipStream_t s);
+                            hipStream_t s, uint32_t* work = nullptr);
 hipError_t launch_pbkdf2_mg_plain(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
                                   const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
                                   hipStream_t s);

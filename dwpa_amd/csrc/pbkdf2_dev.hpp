@@ -169,3 +169,37 @@ __device__ __forceinline__ void pbkdf2_body_mg(const uint32_t* __restrict__ mid,
 }
 
 }  // namespace dwpa
+
+namespace dwpa {
+
+// Work-queue form of pbkdf2_body_mg: items are (output block, 64-lane wave of the ngroups x cap lane space); waves
+// past a group's loaded slots take the next item at once.
+__device__ __forceinline__ void pbkdf2_body_mg_queue(const uint32_t* __restrict__ mid, uint32_t cap,
+                                                     const uint32_t* __restrict__ counter, uint32_t ngroups,
+                                                     const uint32_t* __restrict__ salt,
+                                                     const uint32_t* __restrict__ gsalt, uint32_t* __restrict__ pmk,
+                                                     uint32_t pstride, uint32_t* __restrict__ work) {
+    const uint32_t n = min(*counter, cap);
+    const uint32_t nitems = 2u * ngroups * (cap / 64u);
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll 1
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(work, 1u);
+        item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
+        if (item >= nitems) break;
+        const uint32_t blk = item & 1u;
+        const uint32_t i = (item >> 1) * 64u + lane;
+        const uint32_t c = __builtin_amdgcn_readfirstlane(i / cap);
+        const uint32_t s = i - c * cap;
+        if (s < n) {
+            uint32_t hi[5], ho[5], t[5];
+            load_mid(mid, cap, s, hi, ho);
+            const uint32_t off = gsalt[2 * c], nsalt = gsalt[2 * c + 1];
+            pbkdf2_lane(hi, ho, salt + off + (size_t)blk * nsalt * 16, nsalt, t);
+            store_block(pmk + (size_t)c * cap, pstride, s, blk, t);
+        }
+    }
+}
+
+}  // namespace dwpa

@@ -58,3 +58,10 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     const uint32_t* __restrict__ salt, uint32_t nsalt, uint32_t* __restrict__ pmk, uint32_t* __restrict__ work) {
     dwpa::pbkdf2_body_queue(mid, cap, base, count, counter, salt, nsalt, pmk, work);
 }
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_mg_q(
+    const uint32_t* __restrict__ mid, uint32_t cap, const uint32_t* __restrict__ counter, uint32_t ngroups,
+    const uint32_t* __restrict__ salt, const uint32_t* __restrict__ gsalt, uint32_t* __restrict__ pmk,
+    uint32_t pstride, uint32_t* __restrict__ work) {
+    dwpa::pbkdf2_body_mg_queue(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride, work);
+}

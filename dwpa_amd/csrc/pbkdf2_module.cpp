@@ -20,7 +20,7 @@ extern const size_t pbkdf2_gfx950_hsaco_size;
 struct Fns {
     hipFunction_t one, ms, mg;  // k_pbkdf2_gfx950 (one ESSID), _ms (per-slot salt), _mg (ESSID groups x batch)
     hipFunction_t one_p, ms_p, mg_p;  // the same with progress-ordered wave priority (pbkdf2_dev.hpp PRIO)
-    hipFunction_t one_q;              // k_pbkdf2_gfx950 as a work queue (pbkdf2_dev.hpp pbkdf2_body_queue)
+    hipFunction_t one_q, mg_q;        // the one-ESSID and group kernels as work queues (pbkdf2_dev.hpp *_queue)
     uint64_t level_lanes;       // lanes that give every SIMD of the device one wave: CUs x 4 SIMDs x 64
 };
 static std::mutex g_mod_mu;
@@ -81,6 +81,7 @@ static hipError_t tuned_functions(Fns* fn) {
     if ((e = hipModuleGetFunction(&fn->ms_p, mod, "k_pbkdf2_gfx950_ms_p")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->mg_p, mod, "k_pbkdf2_gfx950_mg_p")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->one_q, mod, "k_pbkdf2_gfx950_q")) != hipSuccess) return e;
+    if ((e = hipModuleGetFunction(&fn->mg_q, mod, "k_pbkdf2_gfx950_mg_q")) != hipSuccess) return e;
     int cus = 0;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     fn->level_lanes = (uint64_t)(cus > 0 ? cus : 256) * 4 * 64;
@@ -91,9 +92,14 @@ static hipError_t tuned_functions(Fns* fn) {
 // At most one wave per SIMD (both output blocks counted): latency-bound, the plain schedule is faster.
 static bool lone_waves(const Fns& fn, uint64_t pmks) { return !force_issue() && 2 * pmks <= fn.level_lanes; }
 
-// DWPA_PBKDF2_QUEUE=1: multi-round one-ESSID launches as the work-queue kernel (A/B switch)
+// Multi-round scan launches (one ESSID, ESSID groups) run as work queues: one resident round of 8 waves per SIMD
+// taking 64-lane items from a counter, so a faster XCD takes more of them.  Measured (profiles/r02/queue/): C2
+// 4.898 -> 4.907 M PMK/s, C4 4.980 -> 4.996 M.  DWPA_PBKDF2_QUEUE=0 switches back to grid launches (A/B).
 static bool use_queue() {
-    static const bool q = env_flag("DWPA_PBKDF2_QUEUE");
+    static const bool q = [] {
+        const char* e = getenv("DWPA_PBKDF2_QUEUE");
+        return !(e && *e == '0');
+    }();
     return q;
 }
 
@@ -141,7 +147,7 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
 
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
                             const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
-                            hipStream_t s) {
+                            hipStream_t s, uint32_t* work) {
     if (ngroups == 0 || cap == 0) return hipSuccess;
     if (cap % 64) return hipErrorInvalidValue;  // chunk group must be wave-uniform
     if (use_plain()) return launch_pbkdf2_mg_plain(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride, s);
@@ -151,6 +157,14 @@ hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* c
     const uint64_t lanes = (uint64_t)ngroups * cap;
     if (lanes > 0xffffffffull - 255) return hipErrorInvalidValue;
     if (lone_waves(fn, lanes)) return launch_pbkdf2_mg_plain(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride, s);
+    if (work && use_queue() && !use_prio(fn, lanes)) {
+        e = hipMemsetAsync(work, 0, 4, s);
+        if (e != hipSuccess) return e;
+        void* qargs[] = {(void*)&mid, (void*)&cap, (void*)&counter, (void*)&ngroups, (void*)&salt, (void*)&gsalt,
+                         (void*)&pmk, (void*)&pstride, (void*)&work};
+        const uint32_t blocks = (uint32_t)(8 * fn.level_lanes / 256);
+        return hipModuleLaunchKernel(fn.mg_q, blocks, 1, 1, 256, 1, 1, 0, s, qargs, nullptr);
+    }
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&counter, (void*)&ngroups, (void*)&salt, (void*)&gsalt,
                     (void*)&pmk, (void*)&pstride};
     const uint32_t wg = wg_size();

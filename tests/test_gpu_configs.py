@@ -174,3 +174,43 @@ def test_pbkdf2_pmk_duplicate_keys():
     essid = b"linksys"
     got = dwpa_amd.pbkdf2_pmk(keys, essid)
     assert got == [O.c_pbkdf2(k, essid) for k in keys]
+
+
+def test_batch_concurrent_callers():
+    """Concurrent dwpa_check_batch calls (PHP ZTS threads, a threaded server) run on separate call contexts of one
+    device (DWPA_CALLS_PER_DEVICE, default 2) and overlap on the GPU.  Four threads call three times each, on job
+    sets large enough for the head/tail split (>= 2 waves per SIMD of unique keys); every call must equal the
+    single-caller result, whose hits are re-derived by the oracle from the winning key alone."""
+    import random
+    import threading
+    rng = random.Random(95)
+    sets = []
+    for t in range(4):
+        jobs = []
+        for e in range(3):
+            essid, ap, sta, an, sn = S.random_net(rng, essid_len=5 + t + e)
+            keys = [b"c%d%d-%06d-" % (t, e, i) + S.fast_psk(rng, 8, 12) for i in range(24000)]
+            hit = rng.randrange(len(keys))
+            line = (S.pmkid_line(keys[hit], essid, ap, sta) if e == 0 else
+                    S.eapol_line(keys[hit], essid, ap, sta, an, sn, e, rng.randint(-6, 6),
+                                 rng.choice(["LE", "BE"]), rng=rng))
+            jobs.append((line, keys, False, 16))
+        sets.append(jobs)
+    serial = [dwpa_amd.check_batch(j) for j in sets]
+    for jobs, got in zip(sets, serial):
+        for (line, keys, pmk, nc), g in zip(jobs, got):
+            assert g, line[:30]
+            assert O.c_check_key_m22000(line, [g[0]], False, nc) == g
+    results = [[] for _ in sets]
+
+    def caller(t):
+        for _ in range(3):
+            results[t].append(dwpa_amd.check_batch(sets[t]))
+
+    threads = [threading.Thread(target=caller, args=(t,)) for t in range(len(sets))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    for t in range(len(sets)):
+        assert len(results[t]) == 3 and all(r == serial[t] for r in results[t]), t
