@@ -294,16 +294,16 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], const uint32_t m
         if (t < 16) wt = w[t];
         else {
             uint32_t x = w[(t - 15) & 15], y = w[(t - 2) & 15];
-            uint32_t s0 = rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3);
-            uint32_t s1 = rotr(y, 17) ^ rotr(y, 19) ^ (y >> 10);
+            uint32_t s0 = xor3(rotr(x, 7), rotr(x, 18), x >> 3);
+            uint32_t s1 = xor3(rotr(y, 17), rotr(y, 19), y >> 10);
             wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
             w[t & 15] = wt;
         }
-        uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-        uint32_t ch = ((f ^ g) & e) ^ g;
+        uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+        uint32_t ch = ch3(e, f, g);
         uint32_t t1 = h + S1 + ch + SHA256_K[t] + wt;
-        uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-        uint32_t mj = (a & b) | ((a | b) & c);
+        uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+        uint32_t mj = maj3(a, b, c);
         uint32_t t2 = S0 + mj;
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
@@ -315,11 +315,11 @@ __device__ __forceinline__ void sha256_compress_kw(uint32_t st[8], const uint32_
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
     for (int t = 0; t < 64; t++) {
-        uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-        uint32_t ch = ((f ^ g) & e) ^ g;
+        uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+        uint32_t ch = ch3(e, f, g);
         uint32_t t1 = h + S1 + ch + kw[t];
-        uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-        uint32_t mj = (a & b) | ((a | b) & c);
+        uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+        uint32_t mj = maj3(a, b, c);
         uint32_t t2 = S0 + mj;
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
@@ -408,8 +408,8 @@ __device__ __forceinline__ void md5_hmac_mid(const uint32_t kb[16], uint32_t ipa
 }
 
 // ------------------------------------------------------------------------------------------------
-// AES-128 encryption (keyver 3 MIC = AES-128-CMAC(KCK, EAPOL)), T-table in LDS.
-// Te0[x] = (2s, s, s, 3s) big-endian bytes of s = S(x); Te1..3 are byte rotations; the S-box is byte 1 of Te0.
+// AES-128 encryption (keyver 3 MIC = AES-128-CMAC(KCK, EAPOL)), T-tables in LDS.
+// Te0[x] = (2s, s, s, 3s) big-endian bytes of s = S(x); Te1..3 are its byte rotations.
 // The table is built at compile time from GF(2^8) arithmetic (no table copied from anywhere).
 // ------------------------------------------------------------------------------------------------
 struct AesTables {
@@ -437,39 +437,46 @@ constexpr AesTables make_aes_tables() {
 }
 __constant__ static const AesTables AES_TABLES = make_aes_tables();
 
-__device__ __forceinline__ uint32_t aes_sb(const uint32_t* te, uint32_t x) { return (te[x & 0xff] >> 8) & 0xff; }
-
-// rk[44] from a 16-byte key given as 4 big-endian words
-__device__ __forceinline__ void aes128_expand(const uint32_t* te, const uint32_t key[4], uint32_t rk[44]) {
-    rk[0] = key[0]; rk[1] = key[1]; rk[2] = key[2]; rk[3] = key[3];
-    uint32_t rcon = 0x01;
-#pragma unroll
-    for (int i = 4; i < 44; i++) {
-        uint32_t t = rk[i - 1];
-        if ((i & 3) == 0) {
-            t = (aes_sb(te, t >> 16) << 24) | (aes_sb(te, t >> 8) << 16) | (aes_sb(te, t) << 8) | aes_sb(te, t >> 24);
-            t ^= rcon << 24;
-            rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x11b : 0);
-        }
-        rk[i] = rk[i - 4] ^ t;
-    }
+// AES-128 encryption over four T-tables in LDS (te4 = Te0..Te3, Te_k = Te0 rotated right by 8k: no rotate per
+// lookup), with the key schedule computed round by round (FIPS-197 5.2) instead of held as rk[44] (40 fewer live
+// registers; 40 more lookups per block).  S-box bytes come out of the T-tables already in place: S[x] is byte 3
+// of Te2/Te3, byte 2 of Te0/Te3, byte 1 of Te0/Te1 and byte 0 of Te1/Te2, so a SubWord is 4 lookups + 3 v_perm.
+__device__ __forceinline__ uint32_t aes4_subword(const uint32_t* te4, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    // bytes (S[a], S[b], S[c], S[d]) from most to least significant; a..d are byte values (0..255)
+    const uint32_t hi = __builtin_amdgcn_perm(te4[512 + a], te4[768 + b], 0x07020100u);  // S[a]:b3, S[b]:b2
+    const uint32_t lo = __builtin_amdgcn_perm(te4[c], te4[256 + d], 0x07060500u);        // S[c]:b1, S[d]:b0
+    return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
 }
-
-__device__ __forceinline__ void aes128_encrypt(const uint32_t* te, const uint32_t rk[44], uint32_t s[4]) {
-    uint32_t s0 = s[0] ^ rk[0], s1 = s[1] ^ rk[1], s2 = s[2] ^ rk[2], s3 = s[3] ^ rk[3];
+__device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te4, const uint32_t key[4], uint32_t s[4]) {
+    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+    const uint32_t* T0 = te4;
+    const uint32_t* T1 = te4 + 256;
+    const uint32_t* T2 = te4 + 512;
+    const uint32_t* T3 = te4 + 768;
+    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
+    uint32_t s0 = s[0] ^ k0, s1 = s[1] ^ k1, s2 = s[2] ^ k2, s3 = s[3] ^ k3;
 #pragma unroll
     for (int r = 1; r < 10; r++) {
-        uint32_t t0 = te[s0 >> 24] ^ rotr(te[(s1 >> 16) & 0xff], 8) ^ rotr(te[(s2 >> 8) & 0xff], 16) ^ rotr(te[s3 & 0xff], 24) ^ rk[4 * r];
-        uint32_t t1 = te[s1 >> 24] ^ rotr(te[(s2 >> 16) & 0xff], 8) ^ rotr(te[(s3 >> 8) & 0xff], 16) ^ rotr(te[s0 & 0xff], 24) ^ rk[4 * r + 1];
-        uint32_t t2 = te[s2 >> 24] ^ rotr(te[(s3 >> 16) & 0xff], 8) ^ rotr(te[(s0 >> 8) & 0xff], 16) ^ rotr(te[s1 & 0xff], 24) ^ rk[4 * r + 2];
-        uint32_t t3 = te[s3 >> 24] ^ rotr(te[(s0 >> 16) & 0xff], 8) ^ rotr(te[(s1 >> 8) & 0xff], 16) ^ rotr(te[s2 & 0xff], 24) ^ rk[4 * r + 3];
+        k0 ^= aes4_subword(te4, (k3 >> 16) & 0xff, (k3 >> 8) & 0xff, k3 & 0xff, k3 >> 24) ^ (RCON[r - 1] << 24);
+        k1 ^= k0;
+        k2 ^= k1;
+        k3 ^= k2;
+        const uint32_t t0 = xor3(xor3(T0[s0 >> 24], T1[(s1 >> 16) & 0xff], T2[(s2 >> 8) & 0xff]), T3[s3 & 0xff], k0);
+        const uint32_t t1 = xor3(xor3(T0[s1 >> 24], T1[(s2 >> 16) & 0xff], T2[(s3 >> 8) & 0xff]), T3[s0 & 0xff], k1);
+        const uint32_t t2 = xor3(xor3(T0[s2 >> 24], T1[(s3 >> 16) & 0xff], T2[(s0 >> 8) & 0xff]), T3[s1 & 0xff], k2);
+        const uint32_t t3 = xor3(xor3(T0[s3 >> 24], T1[(s0 >> 16) & 0xff], T2[(s1 >> 8) & 0xff]), T3[s2 & 0xff], k3);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
-    s[0] = (aes_sb(te, s0 >> 24) << 24 | aes_sb(te, s1 >> 16) << 16 | aes_sb(te, s2 >> 8) << 8 | aes_sb(te, s3)) ^ rk[40];
-    s[1] = (aes_sb(te, s1 >> 24) << 24 | aes_sb(te, s2 >> 16) << 16 | aes_sb(te, s3 >> 8) << 8 | aes_sb(te, s0)) ^ rk[41];
-    s[2] = (aes_sb(te, s2 >> 24) << 24 | aes_sb(te, s3 >> 16) << 16 | aes_sb(te, s0 >> 8) << 8 | aes_sb(te, s1)) ^ rk[42];
-    s[3] = (aes_sb(te, s3 >> 24) << 24 | aes_sb(te, s0 >> 16) << 16 | aes_sb(te, s1 >> 8) << 8 | aes_sb(te, s2)) ^ rk[43];
+    k0 ^= aes4_subword(te4, (k3 >> 16) & 0xff, (k3 >> 8) & 0xff, k3 & 0xff, k3 >> 24) ^ (RCON[9] << 24);
+    k1 ^= k0;
+    k2 ^= k1;
+    k3 ^= k2;
+    s[0] = aes4_subword(te4, s0 >> 24, (s1 >> 16) & 0xff, (s2 >> 8) & 0xff, s3 & 0xff) ^ k0;
+    s[1] = aes4_subword(te4, s1 >> 24, (s2 >> 16) & 0xff, (s3 >> 8) & 0xff, s0 & 0xff) ^ k1;
+    s[2] = aes4_subword(te4, s2 >> 24, (s3 >> 16) & 0xff, (s0 >> 8) & 0xff, s1 & 0xff) ^ k2;
+    s[3] = aes4_subword(te4, s3 >> 24, (s0 >> 16) & 0xff, (s1 >> 8) & 0xff, s2 & 0xff) ^ k3;
 }
+
 
 // CMAC subkey doubling on a 128-bit big-endian value held in 4 words
 __device__ __forceinline__ void cmac_dbl(const uint32_t in[4], uint32_t out[4]) {

@@ -118,14 +118,44 @@ struct Slot {
     bool pbkdf2;              // false: PMK supplied by the caller
 };
 
+// Host-mapped pinned buffer that kernels write directly (hit copy-out, k_hits_out).
+struct MappedHost {
+    uint8_t* p = nullptr;
+    void* dev = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (cap >= bytes && p) return 0;
+        release();
+        if (hipHostMalloc((void**)&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            p = nullptr;
+            return DWPA_E_NOMEM;
+        }
+        if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) {
+            release();
+            return DWPA_E_NOMEM;
+        }
+        cap = bytes;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        dev = nullptr;
+        cap = 0;
+    }
+};
+
 struct Device {
     int id = 0;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;   // check path: table uploads while PBKDF2 runs on `stream`
     hipEvent_t side_done = nullptr;
     hipStream_t tail = nullptr;   // check path: the PBKDF2 remainder (< one wave per SIMD) + its verify
+    hipEvent_t vs_go = nullptr, vs_done = nullptr;  // check path: fan-out of the keyver-3 verify onto `side`
     hipEvent_t head_done = nullptr, tail_done = nullptr, prep_done = nullptr;
+    hipEvent_t head_end = nullptr;  // check path: this context's last PBKDF2 head (the device's head fence)
     PinnedArena stage;            // check path: host staging of the derive uploads
+    MappedHost hits_host;         // check path: hit count + hits written by k_hits_out
     std::mutex mu;
     Batch batch;
     DevBuf lines, atts, pool, segs, segs_tail, salt, koff, kbytes, idsup;
@@ -140,6 +170,16 @@ static int g_ndev = 0;
 static uint32_t g_mask = 0;
 static uint32_t g_batch = 0;
 static std::vector<std::unique_ptr<Device>> g_dev;  // call contexts: [device * calls_per_device() + k]
+
+// Head fence of one physical device: concurrent calls launch their PBKDF2 heads one after another (each head
+// stream waits for the previous head's end event), so two heads never split the SIMDs' wave slots; a call's tail
+// and verify then run beside the next call's head.  Wait + launch + publish happen under the mutex, so a context
+// re-recording its event for a later head can never be waited on by an earlier one (no cycle).
+struct HeadFence {
+    std::mutex mu;
+    hipEvent_t last = nullptr;
+};
+static std::vector<std::unique_ptr<HeadFence>> g_fence;  // [device]
 static std::atomic<uint32_t> g_rr{0};
 
 static uint32_t default_batch() { return g_batch ? g_batch : (1u << 20); }
@@ -167,6 +207,8 @@ static int init_locked(const dwpa_config* cfg) {
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DWPA_E_NODEV;
     g_ndev = n;
     g_dev.clear();
+    g_fence.clear();
+    for (int d = 0; d < n; d++) g_fence.push_back(std::make_unique<HeadFence>());
     for (int d = 0; d < n; d++)
         for (int k = 0; k < calls_per_device(); k++) {
             auto dev = std::make_unique<Device>();
@@ -191,9 +233,25 @@ static std::vector<int> active_devices(uint32_t mask = 0) {
     return v;
 }
 
+static int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* e = getenv(name);
+    const int v = e && *e ? atoi(e) : dflt;
+    return v < lo ? lo : v > hi ? hi : v;
+}
+// Check-path scheduling knobs (A/B switches; the defaults are the measured best):
+//   DWPA_CHECK_PRIO    wave priority of the post-derive kernels (0)
+//   DWPA_TAIL_PRIO     priority the PBKDF2 tail raises itself to once the head has ended (2; 0 = stays at 0)
+//   DWPA_HEAD_FENCE    concurrent calls on one device launch their heads one after another (1)
+//   DWPA_VERIFY_FANOUT the head slots' keyver-3 verify runs on its own stream beside the other classes (1)
+static int check_prio_knob() { static const int v = env_int("DWPA_CHECK_PRIO", 0, 0, 3); return v; }
+static int tail_prio_knob() { static const int v = env_int("DWPA_TAIL_PRIO", 2, 0, 3); return v; }
+static bool head_fence_knob() { static const bool v = env_int("DWPA_HEAD_FENCE", 1, 0, 1) != 0; return v; }
+static bool verify_fanout_knob() { static const bool v = env_int("DWPA_VERIFY_FANOUT", 1, 0, 1) != 0; return v; }
+
 static int device_stream(Device& d) {
     if (!d.stream) {
         HIPCHK(hipSetDevice(d.id));
+        HIPCHK(set_check_prio((uint32_t)check_prio_knob()));
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&d.side_done, hipEventDisableTiming));
@@ -201,6 +259,9 @@ static int device_stream(Device& d) {
         HIPCHK(hipEventCreateWithFlags(&d.head_done, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.tail_done, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.prep_done, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.head_end, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.vs_go, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.vs_done, hipEventDisableTiming));
     }
     return 0;
 }
@@ -255,11 +316,17 @@ static uint64_t hash_bytes(const char* p, size_t n, uint64_t seed) {
     return h ^ (h >> 29);
 }
 
-// Host threads for the check path's host work: at least `min_per_thread` items each, at most 8 threads (the box
-// shares its cores; hardware_concurrency() reports the whole machine).
+// Host threads for the check path's host work: at least `min_per_thread` items each, at most DWPA_HOST_THREADS
+// (default 16, the MI355X box's host share per GPU; 8 measured ~1 ms slower per C5 call).  hardware_concurrency()
+// reports the whole machine, so it only caps this.
 static size_t host_threads(size_t n, size_t min_per_thread) {
+    static const size_t cap = [] {
+        const char* e = getenv("DWPA_HOST_THREADS");
+        const int v = e && *e ? atoi(e) : 16;
+        return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
+    }();
     const unsigned hw = std::thread::hardware_concurrency();
-    return std::max<size_t>(1, std::min<size_t>({8, hw ? hw : 1, n / std::max<size_t>(1, min_per_thread)}));
+    return std::max<size_t>(1, std::min<size_t>({cap, hw ? hw : 1, n / std::max<size_t>(1, min_per_thread)}));
 }
 
 // Host worker pool of the check path: a C5 call runs four parallel phases, and spawning 7 threads per phase cost
@@ -537,12 +604,20 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     if (nu) {
         HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, nu, 0, 0xffffffffu,
                                 (uint32_t*)d.batch.mid.p, nullptr, nullptr, cap, false, s));
-        if (nh < nu) {  // the tail first, beside the head (it only gets the head's leftover issue slots)
+        HeadFence& f = *g_fence[d.id];
+        std::lock_guard<std::mutex> fl(f.mu);
+        if (head_fence_knob() && f.last && f.last != d.head_end) HIPCHK(hipStreamWaitEvent(s, f.last, 0));
+        uint32_t* head_flag = (uint32_t*)d.batch.counters.p + 3;  // zeroed with the counters above
+        if (nh < nu) {  // the tail first, beside the head (priority 0 until the head has ended: pbkdf2_lane_tail)
             HIPCHK(hipEventRecord(d.prep_done, s));
             HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
-            HIPCHK(launch_pbkdf2_ms(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh, d.tail));
+            HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh,
+                                         head_flag, (uint32_t)tail_prio_knob(), d.tail));
         }
         HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
+        if (nh < nu) HIPCHK(launch_set_flag(head_flag, s));
+        HIPCHK(hipEventRecord(d.head_end, s));
+        f.last = d.head_end;
     }
     // SoA rows keep their stride (cap), so a sub-range is the same launch on offset base pointers
     const uint32_t sp = st.split;
@@ -571,11 +646,14 @@ static int join_tail(Device& d) {
 // one; segments are runs of <= 64 consecutive slots of one job.  Hits are appended on the device (collect_hits).
 static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, size_t b, size_t e,
                         const std::vector<uint32_t>& job_line, const TableBuilder& tb, bool upload_tables,
-                        hipStream_t s, DevBuf& segbuf, DevBuf& keybuf) {
+                        hipStream_t s, DevBuf& segbuf, DevBuf& keybuf, bool fanout) {
     const uint32_t n = (uint32_t)(e - b), row0 = (uint32_t)(b - base);
     if (!n && !upload_tables) return 0;
-    // bucket = mode * 4 + class index; mode 1 = attempt-parallel (EAPOL lines with >= ATT_PARALLEL_MIN attempts)
+    // bucket = mode * 4 + class index; mode 1 = attempt-parallel (EAPOL lines with >= ATT_PARALLEL_MIN attempts).
+    // Attempt-parallel keyver 1 and 2 share bucket 5 (one launch of the combined kernel): every verify launch that
+    // runs while the PBKDF2 tail holds some SIMDs ends only with the tail, so fewer launches in a row end sooner.
     std::vector<SegDev> bucket[8];
+    auto bucket_vc = [](int k) { return k == 5 ? (uint32_t)(VC_KV1 | VC_KV2) : 1u << (k & 3); };
     for (uint32_t i = 0; i < n;) {
         uint32_t j = i;
         const uint32_t job = slots[b + i].job;
@@ -585,24 +663,27 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
         const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
         // the key-parallel kernel reads every attempt's KW blocks (built for lines under ATT_PARALLEL_MIN)
         if (L.kind == LINE_EAPOL && !att && tb.atts[L.list_off].kw_off == NO_KW) return DWPA_E_ARG;
-        if (!tb.never[li])
-            bucket[(att ? 4 : 0) + __builtin_ctz(verify_class(L))].push_back({li, row0 + i, j - i, 0});
+        if (!tb.never[li]) {
+            const int k = (att ? 4 : 0) + __builtin_ctz(verify_class(L));
+            bucket[k == 6 ? 5 : k].push_back({li, row0 + i, j - i, 0});
+        }
         i = j;
     }
     // attempt-parallel buckets: pad = the segment's first wave in its launch (ceil(count * natt / 64) waves each)
-    uint32_t nwaves[8] = {0}, kwords = 0, kstride = 0;
-    for (int k = 4; k < 8; k++) {
+    uint32_t nwaves[8] = {0};
+    for (int k = 4; k < 8; k++)
         for (SegDev& sg : bucket[k]) {
             sg.pad = nwaves[k];
             nwaves[k] += (uint32_t)(((uint64_t)sg.count * tb.lines[sg.line].natt + 63) / 64);
         }
-        if (!bucket[k].empty()) {
-            kwords = std::max(kwords, eapol_key_words(1u << (k & 3)));
-            kstride = std::max(kstride, (uint32_t)bucket[k].size() * 64);
-        }
+    // per-key EapolKey state scratch of the attempt-parallel launches: one region per class (the classes may run
+    // on parallel streams), class k's stride = 64 x its segments
+    size_t koff[8] = {0}, ktotal = 0;
+    for (int k = 4; k < 8; k++) {
+        koff[k] = ktotal;
+        ktotal += (size_t)eapol_key_words(bucket_vc(k)) * bucket[k].size() * 64;
     }
-    // one scratch of per-key EapolKey states for the stream's attempt-parallel launches (they run in order)
-    if (kwords) RCHK(keybuf.ensure((size_t)kwords * kstride * 4));
+    if (ktotal) RCHK(keybuf.ensure(ktotal * 4));
     std::vector<SegDev> segs;
     size_t bstart[9];
     for (int k = 0; k < 8; k++) {
@@ -618,20 +699,34 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
     RCHK(upload(segbuf, segs, d.side));
     HIPCHK(hipEventRecord(d.side_done, d.side));
     HIPCHK(hipStreamWaitEvent(s, d.side_done, 0));
+    // fan-out: the keyver-3 launches (the longest class) on the side stream, idle once the tables are up, beside
+    // the other classes on s, which then waits for them.  Verify waves that land on the SIMDs of the tail's lone
+    // waves hold back only their own stream.  (A fourth stream of its own would share a hardware queue with the
+    // tail's: a process gets GPU_MAX_HW_QUEUES = 4, one of them the null stream's.)
+    const bool fan = fanout && verify_fanout_knob() && (!bucket[3].empty() || !bucket[7].empty());
+    if (fan) {
+        HIPCHK(hipEventRecord(d.vs_go, s));
+        HIPCHK(hipStreamWaitEvent(d.side, d.vs_go, 0));
+    }
     uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
     for (int k = 0; k < 8; k++) {
-        const uint32_t nb = (uint32_t)(bstart[k + 1] - bstart[k]), vc = 1u << (k & 3);
+        const uint32_t nb = (uint32_t)(bstart[k + 1] - bstart[k]), vc = bucket_vc(k);
         const SegDev* sg = (const SegDev*)segbuf.p + bstart[k];
         if (!nb) continue;
+        hipStream_t vsk = fan && (k & 3) == 3 ? d.side : s;
         if (k < 4)
             HIPCHK(launch_verify((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, nullptr,
                                  sg, nb, 0, 1, (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p,
-                                 (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc, s));
+                                 (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc, vsk));
         else
             HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, sg,
-                                     nb, nwaves[k], (uint32_t*)keybuf.p, kstride, (const LineDev*)d.lines.p,
-                                     (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p,
-                                     hitcnt, d.batch.hitcap, vc, s));
+                                     nb, nwaves[k], (uint32_t*)keybuf.p + koff[k], (uint32_t)bucket[k].size() * 64,
+                                     (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p,
+                                     (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc, vsk));
+    }
+    if (fan) {
+        HIPCHK(hipEventRecord(d.vs_done, d.side));
+        HIPCHK(hipStreamWaitEvent(s, d.vs_done, 0));
     }
     return 0;
 }
@@ -641,15 +736,16 @@ static int collect_hits(Device& d, std::vector<HitDev>& hits_out) {
     PhaseTrace tr;
     hipStream_t s = d.stream;
     RCHK(join_tail(d));
-    uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
-    uint32_t nh = 0;
-    HIPCHK(hipMemcpyAsync(&nh, hitcnt, 4, hipMemcpyDeviceToHost, s));
+    const uint32_t* hitcnt = (const uint32_t*)d.batch.counters.p + 1;
+    RCHK(d.hits_host.ensure(16 + (size_t)d.batch.hitcap * sizeof(HitDev)));
+    HIPCHK(launch_hits_out(hitcnt, (const HitDev*)d.batch.hits.p, d.batch.hitcap, (uint32_t*)d.hits_host.dev, s));
     HIPCHK(hipStreamSynchronize(s));
     tr.mark("  device wait");
+    const uint32_t nh = *(volatile const uint32_t*)d.hits_host.p;
     if (nh > d.batch.hitcap) return DWPA_E_OVERFLOW;
     size_t old = hits_out.size();
     hits_out.resize(old + nh);
-    if (nh) HIPCHK(hipMemcpy(hits_out.data() + old, d.batch.hits.p, nh * sizeof(HitDev), hipMemcpyDeviceToHost));
+    if (nh) memcpy(hits_out.data() + old, d.hits_host.p + 16, nh * sizeof(HitDev));
     return 0;
 }
 
@@ -799,8 +895,11 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
                 for (uint32_t j : js) job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
             tr.mark("tables (overlapped)");
         }
-        RCHK(queue_verify(d, slots, b, b, b + st.split, job_line, tb, b == 0, d.stream, d.segs, d.keys));
-        RCHK(queue_verify(d, slots, b, b + st.split, e, job_line, tb, false, d.tail, d.segs_tail, d.keys_tail));
+        // the tail slots' verify first: its segment upload goes up the side stream ahead of the head's keyver-3
+        // verify, which that stream then runs (fan-out)
+        RCHK(queue_verify(d, slots, b, b + st.split, e, job_line, tb, b == 0, d.tail, d.segs_tail, d.keys_tail,
+                          false));
+        RCHK(queue_verify(d, slots, b, b, b + st.split, job_line, tb, false, d.stream, d.segs, d.keys, true));
         tr.mark("  verify queued");
         RCHK(collect_hits(d, hits));
     }
@@ -1230,6 +1329,12 @@ void dwpa_shutdown(void) {
             b->release();
         d->batch.cap = d->batch.hitcap = 0;
         d->stage.release();
+        d->hits_host.release();
+        if (d->head_end) (void)hipEventDestroy(d->head_end);
+        d->head_end = nullptr;
+        if (d->vs_go) (void)hipEventDestroy(d->vs_go);
+        if (d->vs_done) (void)hipEventDestroy(d->vs_done);
+        d->vs_go = d->vs_done = nullptr;
         if (d->stream) (void)hipStreamDestroy(d->stream);
         if (d->side) (void)hipStreamDestroy(d->side);
         if (d->side_done) (void)hipEventDestroy(d->side_done);
@@ -1241,6 +1346,7 @@ void dwpa_shutdown(void) {
         d->side_done = d->head_done = d->tail_done = d->prep_done = nullptr;
     }
     g_dev.clear();
+    g_fence.clear();
     g_init = false;
 }
 

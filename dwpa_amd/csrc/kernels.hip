@@ -98,12 +98,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     pbkdf2_body_mg(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride);
 }
 
+// The check path's PBKDF2 tail (pbkdf2_lane_tail): same slots and salt entries as k_pbkdf2_ms.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_ms_tail(
+    const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
+    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, const uint32_t* __restrict__ flag, uint32_t prio) {
+    const uint32_t blk = blockIdx.y;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= min(count, cap)) return;
+    uint32_t hi[5], ho[5], t[5];
+    load_mid(mid, cap, s, hi, ho);
+    const uint32_t* e = pool + sref[s];
+    const uint32_t nsalt = e[0];
+    pbkdf2_lane_tail(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t, flag, prio);
+    store_block(pmk, cap, s, blk, t);
+}
+
+// Sets the tail's head-done flag (agent scope: the tail's waves poll it from every XCD).
+__global__ void k_set_flag(uint32_t* __restrict__ flag) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave priority of the check path's post-derive kernels (DWPA_CHECK_PRIO, set per device by set_check_prio).
+__device__ uint32_t g_check_prio = 0;
+__device__ __forceinline__ void check_prio() { set_wave_prio(g_check_prio); }
+
 // Slot PMKs from the derived unique (ESSID, key) PMKs or from caller-supplied PMKs:
 // src[i] = u -> upmk[.][u];  src[i] = GATHER_CALLER | c -> cpmk[c][0..7] (check_key_m22000's $pmk, common.php:178).
 __global__ __launch_bounds__(256) void k_gather_pmk(const uint32_t* __restrict__ upmk, uint32_t ucap,
                                                     const uint32_t* __restrict__ cpmk,
                                                     const uint32_t* __restrict__ src, uint32_t n,
                                                     uint32_t* __restrict__ pmk, uint32_t cap) {
+    check_prio();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t r = src[i];
@@ -115,6 +140,22 @@ __global__ __launch_bounds__(256) void k_gather_pmk(const uint32_t* __restrict__
 #pragma unroll
         for (int k = 0; k < 8; k++) pmk[(size_t)k * cap + i] = upmk[(size_t)k * ucap + r];
     }
+}
+
+// Hit count and hits -> host-mapped pinned memory (word 0 = count, the min(count, hitcap) HitDev records from byte
+// 16): the check path reads its results without a device-to-host copy, whose runtime blit kernel would run at wave
+// priority 0 and starve beside another call's PBKDF2 head.
+__global__ __launch_bounds__(256) void k_hits_out(const uint32_t* __restrict__ hitcnt,
+                                                  const HitDev* __restrict__ hits, uint32_t hitcap,
+                                                  uint32_t* __restrict__ out) {
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t n = min(*hitcnt, hitcap);
+    constexpr uint32_t W = sizeof(HitDev) / 4;
+    const uint32_t* src = (const uint32_t*)hits;
+    const uint32_t total = n * W;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
+        out[4 + i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = *hitcnt;
 }
 
 // Caller-supplied PMK for one slot (check_key_m22000's $pmk argument, common.php:157,178).
@@ -277,10 +318,8 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         for (int k = 0; k < 8; k++) ptk[k] = K.op2[k];
         sha256_compress(ptk, m);
         // AES-128-CMAC(KCK = PTK[0..15], EAPOL)  (common.php:72-112)
-        uint32_t rk[44];
-        aes128_expand(te, ptk, rk);
         uint32_t Lb[4] = {0, 0, 0, 0}, K1[4], K2[4];
-        aes128_encrypt(te, rk, Lb);
+        aes128_encrypt_te4(te, ptk, Lb);
         cmac_dbl(Lb, K1);
         cmac_dbl(K1, K2);
         uint32_t c[4] = {0, 0, 0, 0};
@@ -293,7 +332,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
                 if (last) v ^= L.cmac_complete ? K1[k] : K2[k];
                 c[k] ^= v;
             }
-            aes128_encrypt(te, rk, c);
+            aes128_encrypt_te4(te, ptk, c);
         }
         mic[0] = c[0]; mic[1] = c[1]; mic[2] = c[2]; mic[3] = c[3];
     }
@@ -329,24 +368,33 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
     }
 }
 
+// Te0..Te3 (crypto_dev.hpp aes128_encrypt_te4) into the workgroup's LDS, for kernels that verify keyver 3.
+constexpr uint32_t AES_LDS_WORDS = 1024;
 template <uint32_t VC>
 __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     if constexpr ((VC & VC_KV3) != 0) {
-        for (uint32_t k = threadIdx.x; k < 256; k += blockDim.x) te[k] = AES_TABLES.te0[k];
+        for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) te[k] = rotr(AES_TABLES.te0[k & 255], 8 * (k >> 8));
         __syncthreads();
     }
     return te;
 }
+// keyver-3 kernels keep 256-thread workgroups: a lane-sliced Te0 (64 KiB, 1024-thread workgroups, no bank
+// conflicts) measured level (profiles/r02/c5_sched/aes_sliced_ab)
+constexpr uint32_t vc_block(uint32_t) { return 256; }
 
 // Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
 // wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
 // Occupancy target per class: PMKID and keyver 1 fit 64 VGPRs (8 waves/SIMD); keyver 2 is held at 64 too and spills
-// 9 VGPRs, which measured level with a 6-wave, spill-free build (profiles/r01/verify_waves_ab); keyver 3 keeps 44 AES
-// round-key registers (2 waves).
-constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? 2 : 8; }
+// 9 VGPRs, which measured level with a 6-wave, spill-free build (profiles/r01/verify_waves_ab); keyver 3 runs at 4
+// waves (106 VGPRs, AES round keys computed on the fly; 2 and 6 waves level, 8 waves with 18 spilled VGPRs slower:
+// profiles/r02/c5_sched/kv3_waves).
+#ifndef DWPA_KV3_WAVES
+#define DWPA_KV3_WAVES 4
+#endif
+constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? DWPA_KV3_WAVES : 8; }
 
 template <uint32_t VC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify(
+__global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify(
                                                 const uint32_t* __restrict__ pmk, uint32_t cap,
                                                 const uint64_t* __restrict__ ids, const uint32_t* __restrict__ counter,
                                                 const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t line_base,
@@ -355,7 +403,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
                                                 const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                 uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
-    __shared__ uint32_t te_lds[256];
+    check_prio();
+    __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -449,6 +498,7 @@ __global__ __launch_bounds__(256) void k_eapol_keys(const uint32_t* __restrict__
                                                     const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool, uint32_t* __restrict__ keys,
                                                     uint32_t kstride) {
+    check_prio();
     const uint32_t segi = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t k = threadIdx.x & 63;
     if (segi >= nsegs) return;
@@ -477,7 +527,7 @@ __global__ __launch_bounds__(256) void k_eapol_keys(const uint32_t* __restrict__
 }
 
 template <uint32_t VC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify_att(
+__global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify_att(
                                                     const uint32_t* __restrict__ pmk, uint32_t cap,
                                                     const uint64_t* __restrict__ ids,
                                                     const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t nwaves,
@@ -486,7 +536,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(vc_waves(VC
                                                     const uint32_t* __restrict__ pool,
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                     uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
-    __shared__ uint32_t te_lds[256];
+    check_prio();
+    __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
@@ -573,6 +624,30 @@ hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t
     return hipGetLastError();
 }
 
+hipError_t launch_hits_out(const uint32_t* hitcnt, const HitDev* hits, uint32_t hitcap, uint32_t* out,
+                           hipStream_t s) {
+    const uint32_t blocks = cdiv((uint64_t)hitcap * (sizeof(HitDev) / 4), 256);
+    hipLaunchKernelGGL(k_hits_out, dim3(blocks < 1 ? 1 : blocks > 64 ? 64 : blocks), dim3(256), 0, s, hitcnt, hits,
+                       hitcap, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_pbkdf2_ms_tail(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
+                                 const uint32_t* sref, uint32_t* pmk, const uint32_t* flag, uint32_t prio,
+                                 hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pbkdf2_ms_tail, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, count, pool, sref, pmk,
+                       flag, prio);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_flag(uint32_t* flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(64), 0, s, flag);
+    return hipGetLastError();
+}
+
+hipError_t set_check_prio(uint32_t prio) { return hipMemcpyToSymbol(HIP_SYMBOL(g_check_prio), &prio, 4); }
+
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s) {
     uint4 lo = make_uint4(w[0], w[1], w[2], w[3]), hi = make_uint4(w[4], w[5], w[6], w[7]);
     hipLaunchKernelGGL(k_set_pmk, dim3(1), dim3(64), 0, s, pmk, cap, slot, lo, hi);
@@ -585,6 +660,7 @@ hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint
     case VC_KV1: CALL(VC_KV1); break;     \
     case VC_KV2: CALL(VC_KV2); break;     \
     case VC_KV3: CALL(VC_KV3); break;     \
+    case VC_KV1 | VC_KV2: CALL(VC_KV1 | VC_KV2); break; \
     default: CALL(VC_ALL); break;         \
     }
 
@@ -595,10 +671,10 @@ hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids,
                          uint32_t pstride) {
     if (nsegs == 0 || nlines == 0) return hipSuccess;
     if (!pstride) pstride = cap;
-    const dim3 grid(cdiv(nsegs, 4), segs ? 1 : nlines);
 #define DWPA_LAUNCH_VERIFY(V)                                                                                  \
-    hipLaunchKernelGGL(k_verify<V>, grid, dim3(256), 0, s, pmk, cap, ids, counter, segs, nsegs, line_base,      \
-                       line_list, line_poff, pstride, lines, pool, atts, hits, hitcnt, hitcap)
+    hipLaunchKernelGGL(k_verify<V>, dim3(cdiv(nsegs, vc_block(V) / 64), segs ? 1 : nlines), dim3(vc_block(V)),  \
+                       0, s, pmk, cap, ids, counter, segs, nsegs, line_base, line_list, line_poff, pstride, lines,  \
+                       pool, atts, hits, hitcnt, hitcap)
     DWPA_VC_DISPATCH(vc, DWPA_LAUNCH_VERIFY)
 #undef DWPA_LAUNCH_VERIFY
     return hipGetLastError();
@@ -615,8 +691,8 @@ hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* 
 #define DWPA_LAUNCH_VERIFY_ATT(V)                                                                                 \
     hipLaunchKernelGGL(k_eapol_keys<V>, dim3(cdiv((uint64_t)nsegs * 64, 256)), dim3(256), 0, s, pmk, cap, segs,   \
                        nsegs, lines, pool, keys, kstride);                                                         \
-    hipLaunchKernelGGL(k_verify_att<V>, dim3(cdiv(nwaves, 4)), dim3(256), 0, s, pmk, cap, ids, segs, nsegs, nwaves, \
-                       keys, kstride, lines, pool, atts, hits, hitcnt, hitcap)
+    hipLaunchKernelGGL(k_verify_att<V>, dim3(cdiv(nwaves, vc_block(V) / 64)), dim3(vc_block(V)), 0, s, pmk, cap, \
+                       ids, segs, nsegs, nwaves, keys, kstride, lines, pool, atts, hits, hitcnt, hitcap)
     DWPA_VC_DISPATCH(vc & ~VC_PMKID, DWPA_LAUNCH_VERIFY_ATT)
 #undef DWPA_LAUNCH_VERIFY_ATT
     return hipGetLastError();

@@ -43,9 +43,21 @@ hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* c
 hipError_t launch_pbkdf2_mg_plain(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
                                   const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
                                   hipStream_t s);
+// Check-path tail: PBKDF2 of slots [0, count) like launch_pbkdf2_ms_plain, at wave priority 0 until *flag != 0,
+// then at `prio` (0 = never raised).  launch_set_flag sets the flag (queue it after the head).
+hipError_t launch_pbkdf2_ms_tail(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
+                                 const uint32_t* sref, uint32_t* pmk, const uint32_t* flag, uint32_t prio,
+                                 hipStream_t s);
+hipError_t launch_set_flag(uint32_t* flag, hipStream_t s);
+// Wave priority (0..3) of the check path's post-derive kernels (PMK gather, EAPOL key states, verifies) on the
+// current device; the hit copy-out always runs at 3.
+hipError_t set_check_prio(uint32_t prio);
 constexpr uint32_t GATHER_CALLER = 0x80000000u;
 hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t* cpmk, const uint32_t* src,
                              uint32_t n, uint32_t* pmk, uint32_t cap, hipStream_t s);
+// out: host-mapped, >= 16 + hitcap * sizeof(HitDev) bytes (word 0 = hit count, HitDev records from byte 16)
+hipError_t launch_hits_out(const uint32_t* hitcnt, const HitDev* hits, uint32_t hitcap, uint32_t* out,
+                           hipStream_t s);
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s);
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,

@@ -65,6 +65,58 @@ __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t
     }
 }
 
+__device__ __forceinline__ void set_wave_prio(uint32_t p) {
+    switch (p) {  // s_setprio takes an immediate
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+
+// The check path's tail lane (the PBKDF2 remainder of under one wave per SIMD, launched beside the head): wave
+// priority 0 while *flag == 0, so it takes only the issue slots the head leaves; once the head has ended (the
+// engine sets the flag from the head's stream) it raises itself to `prio`, ahead of the verify waves that share its
+// SIMDs.  The flag is polled every 64 iterations with an agent-scope load (the writer may sit on another XCD).
+__device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
+                                                 uint32_t nsalt, uint32_t t[5], const uint32_t* flag, uint32_t prio) {
+    uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
+    for (uint32_t b = 0; b < nsalt; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) m[j] = sb[b * 16 + j];
+        sha1_compress(st, m);
+    }
+    const Sha1Mid MI = sha1_mid(hi);
+    const Sha1Mid MO = sha1_mid(ho);
+    uint32_t u[5], x[5];
+    sha1_84(MO, st, u);
+#pragma unroll
+    for (int k = 0; k < 5; k++) t[k] = u[k];
+    int it = 1;
+    if (prio) {
+#pragma unroll 1
+        for (; it < 4096; it++) {
+            if ((it & 63) == 0 &&
+                __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                set_wave_prio(prio);
+                break;
+            }
+            sha1_84(MI, u, x);
+            sha1_84(MO, x, u);
+#pragma unroll
+            for (int k = 0; k < 5; k++) t[k] ^= u[k];
+        }
+    }
+#pragma unroll 1
+    for (; it < 4096; it++) {
+        sha1_84(MI, u, x);
+        sha1_84(MO, x, u);
+#pragma unroll
+        for (int k = 0; k < 5; k++) t[k] ^= u[k];
+    }
+}
+
 __device__ __forceinline__ void load_mid(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t s, uint32_t hi[5],
                                          uint32_t ho[5]) {
 #pragma unroll
@@ -167,10 +219,6 @@ __device__ __forceinline__ void pbkdf2_body_mg(const uint32_t* __restrict__ mid,
     pbkdf2_lane<PRIO>(hi, ho, salt + off + (size_t)blk * nsalt * 16, nsalt, t);
     store_block(pmk + (size_t)c * cap, pstride, s, blk, t);
 }
-
-}  // namespace dwpa
-
-namespace dwpa {
 
 // Work-queue form of pbkdf2_body_mg: items are (output block, 64-lane wave of the ngroups x cap lane space); waves
 // past a group's loaded slots take the next item at once.
