@@ -580,7 +580,7 @@ def main_files(args, world, rank, local):
     with open(hpath, "wb") as f:
         f.write(line + b"\n")
     cracked = True
-    times = []
+    times, all_passes = [], []
     for rep in range(args.warmup + args.steps):
         if os.path.exists(opath):
             os.remove(opath)
@@ -589,6 +589,7 @@ def main_files(args, world, rank, local):
         t0 = time.perf_counter()
         rc = dwpa_amd.crack_files(hpath, [dpath], None, 8, opath, device_mask=1 << local, batch=args.batch)
         el = time.perf_counter() - t0
+        all_passes.append(round(el, 3))
         if rep >= args.warmup:
             times.append(el)
         recs = open(opath, "rb").read().strip().split(b"\n") if os.path.exists(opath) else []
@@ -609,7 +610,11 @@ def main_files(args, world, rank, local):
                                    + (", ~30 % of the words shorter than 8" if args.short_words else ""),
                        "dict_words": n, "gz_bytes": gz_bytes, "gz_write_s": round(gz_s, 2),
                        "words_scanned_per_pass": words, "batch": args.batch,
-                       "parallelism": f"replicas x{world}"},
+                       "parallelism": f"replicas x{world}",
+                       "dict_cache": "passes after the first replay the decoded dictionary from the library's "
+                                     "DictCache (no inflate)" if os.environ.get("DWPA_DICT_CACHE_MB", "") != "0"
+                                     else "off"},
+            "pass_s": all_passes,
             "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked), "reader": reader}), flush=True)
     for x in (dpath, hpath, opath):
         if os.path.exists(x):

@@ -65,13 +65,11 @@ class ItemQueue {
         std::lock_guard<std::mutex> lk(mu_);
         while (!cur_ || pos_ >= cur_->words()) {
             if (done_) return false;
-            Chunk c;
-            if (!src_.next(c, err_)) {
+            if (!src_.next(cur_, err_)) {
                 done_ = true;
                 cur_.reset();
                 return false;
             }
-            cur_ = std::make_shared<const Chunk>(std::move(c));
             pos_ = 0;
         }
         const size_t n = std::min(size_, cur_->words() - pos_);
@@ -392,6 +390,7 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     const bool ioerr = items.io_error();
     if (trace_on()) {
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        fprintf(stderr, "[dwpa] crack dictionary cache: %zu files replayed from memory so far\n", DictCache::get().hits());
         for (size_t k = 0; k < G; k++)
             fprintf(stderr, "[dwpa] crack worker %zu (device %d): %zu items, %zu words, %.3f s waiting for input of %.3f s\n",
                     k, work[k]->device, work[k]->items, work[k]->words, work[k]->wait_s, el);

@@ -2,13 +2,18 @@
 // wordlists, one candidate per line, $HEX[...] for non-printable words, maint.php:55-60).  Header-only so that
 // tools/inflate_bench.cpp measures exactly the reader the library runs.
 #pragma once
+#include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <zlib.h>
 
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <list>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -174,10 +179,76 @@ class DictReader {
     std::string partial_;
 };
 
-// Dictionary chunks from several files at once: worker t reads files t, t+T, ... with its own DictReader and
-// queues its chunks (first chunk small, then doubling to max_words), so inflating several gz dictionaries uses
-// several host cores.  Chunks arrive in completion order; candidate order only decides which of two identical
-// PSKs is written, so the outfile is the same as hashcat's.
+// Decoded dictionaries kept in host memory between dwpa_crack_files calls of one process.  help_crack downloads a
+// dictionary once and runs many work units over it (help_crack.py:520-552), and one gzip stream inflates at only
+// ~28 M words/s -- under six GPUs' worth of one-ESSID candidates.  A file read to its end is kept
+// whole (its chunks are shared with the work items that scan them), keyed by path, size, mtime and inode, so the
+// next work unit over it streams from memory.  DWPA_DICT_CACHE_MB bounds the total (default 4096, 0 = off); the
+// least recently used files go first.
+class DictCache {
+  public:
+    using Chunks = std::vector<std::shared_ptr<const Chunk>>;
+    static DictCache& get() {
+        static DictCache* c = new DictCache();  // never destroyed: chunks may outlive static destructors
+        return *c;
+    }
+    // "" when the file cannot be stat()ed or the cache is off (never cached then).
+    std::string key(const std::string& path) const {
+        struct stat st;
+        if (budget_ == 0 || stat(path.c_str(), &st) != 0) return std::string();
+        return path + '\0' + std::to_string((long long)st.st_size) + ':' + std::to_string((long long)st.st_mtim.tv_sec) +
+               '.' + std::to_string((long long)st.st_mtim.tv_nsec) + ':' + std::to_string((unsigned long long)st.st_ino);
+    }
+    std::shared_ptr<const Chunks> find(const std::string& k) {
+        if (k.empty()) return nullptr;
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = map_.find(k);
+        if (it == map_.end()) return nullptr;
+        lru_.splice(lru_.begin(), lru_, it->second.pos);
+        hits_++;
+        return it->second.chunks;
+    }
+    void put(const std::string& k, std::shared_ptr<const Chunks> chunks) {
+        if (k.empty()) return;
+        size_t bytes = 0;
+        for (const auto& c : *chunks) bytes += c->off.size() * sizeof(uint64_t) + c->bytes.size();
+        std::lock_guard<std::mutex> lk(mu_);
+        if (bytes > budget_ || map_.count(k)) return;
+        while (total_ + bytes > budget_ && !lru_.empty()) {  // evict least recently used
+            auto it = map_.find(lru_.back());
+            total_ -= it->second.bytes;
+            map_.erase(it);
+            lru_.pop_back();
+        }
+        lru_.push_front(k);
+        map_[k] = Entry{std::move(chunks), bytes, lru_.begin()};
+        total_ += bytes;
+    }
+    bool can_hold(size_t bytes) const { return bytes <= budget_; }
+    size_t hits() const { return hits_.load(); }
+
+  private:
+    DictCache() {
+        const char* e = getenv("DWPA_DICT_CACHE_MB");
+        budget_ = (size_t)(e && *e ? atoll(e) : 4096) << 20;
+    }
+    struct Entry {
+        std::shared_ptr<const Chunks> chunks;
+        size_t bytes;
+        std::list<std::string>::iterator pos;
+    };
+    std::mutex mu_;
+    std::map<std::string, Entry> map_;
+    std::list<std::string> lru_;
+    size_t total_ = 0, budget_ = 0;
+    std::atomic<size_t> hits_{0};
+};
+
+// Dictionary chunks from several files at once: worker t reads files t, t+T, ... (one DictReader per file, so a
+// chunk never spans two files) and queues its chunks (first chunk small, then doubling to max_words), so inflating
+// several gz dictionaries uses several host cores.  A file in the DictCache is replayed from memory instead.
+// Chunks arrive in completion order; candidate order only decides which of two identical PSKs is written, so the
+// outfile is the same as hashcat's.
 class ChunkSource {
   public:
     ChunkSource(const std::vector<std::string>& paths, size_t first_words, size_t max_words) {
@@ -204,7 +275,7 @@ class ChunkSource {
         cv_.notify_all();
     }
     // Blocks until a chunk is ready; false once every file is read (or on an I/O error: err is set).
-    bool next(Chunk& c, bool& err) {
+    bool next(std::shared_ptr<const Chunk>& c, bool& err) {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return !q_.empty() || live_ == 0 || stop_; });
         err = err || err_;
@@ -214,21 +285,51 @@ class ChunkSource {
         cv_.notify_all();
         return true;
     }
+    bool next(Chunk& c, bool& err) {  // by value (tools/inflate_bench)
+        std::shared_ptr<const Chunk> p;
+        if (!next(p, err)) return false;
+        c = *p;
+        return true;
+    }
 
   private:
+    bool push(std::shared_ptr<const Chunk> c) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return q_.size() < cap_ || stop_; });
+        if (stop_) return false;
+        q_.push_back(std::move(c));
+        cv_.notify_all();
+        return true;
+    }
     void work(const std::vector<std::string>& paths, size_t words, size_t max_words) {
-        DictReader reader(paths, &cancel_);
+        DictCache& cache = DictCache::get();
         bool err = false;
-        for (;;) {
-            Chunk c;
-            const bool have = reader.next(c, words, (size_t)1 << 31, err, &cancel_);
-            words = std::min(max_words, 2 * words);
-            std::unique_lock<std::mutex> lk(mu_);
-            if (!have || err || stop_) break;
-            cv_.wait(lk, [&] { return q_.size() < cap_ || stop_; });
-            if (stop_) break;
-            q_.push_back(std::move(c));
-            cv_.notify_all();
+        for (const std::string& path : paths) {
+            if (cancel_.load() || err) break;
+            const std::string key = cache.key(path);
+            if (auto hit = cache.find(key)) {  // decoded before: replay from memory
+                for (const auto& c : *hit)
+                    if (!push(c)) break;
+                continue;
+            }
+            auto keep = std::make_shared<DictCache::Chunks>();
+            size_t kept = 0;
+            bool whole = !key.empty();
+            DictReader reader({path}, &cancel_);
+            for (;;) {
+                auto c = std::make_shared<Chunk>();
+                const bool have = reader.next(*c, words, (size_t)1 << 31, err, &cancel_);
+                words = std::min(max_words, 2 * words);
+                if (!have || err) break;
+                if (whole) {
+                    kept += c->off.size() * sizeof(uint64_t) + c->bytes.size();
+                    whole = cache.can_hold(kept);
+                    if (whole) keep->push_back(c);
+                    else keep->clear();
+                }
+                if (!push(std::move(c))) break;
+            }
+            if (whole && !err && !cancel_.load()) cache.put(key, std::move(keep));  // read to its end
         }
         std::lock_guard<std::mutex> lk(mu_);
         err_ = err_ || err;
@@ -237,7 +338,7 @@ class ChunkSource {
     }
     std::mutex mu_;
     std::condition_variable cv_;
-    std::deque<Chunk> q_;
+    std::deque<std::shared_ptr<const Chunk>> q_;
     size_t cap_ = 2, live_ = 0;
     bool stop_ = false, err_ = false;
     std::atomic<bool> cancel_{false};

@@ -13,6 +13,10 @@
  * Plain C types only.  The caller owns every buffer; the library keeps no caller pointer after a call returns and
  * returns no heap memory.  All entry points are thread-safe.  There is no CPU fallback: without a usable gfx950
  * device every compute entry point returns DWPA_E_NODEV.
+ *
+ * Concurrent check calls (dwpa_check_m22000 / dwpa_check_batch / dwpa_pbkdf2_pmk from several threads) run on up to
+ * DWPA_CALLS_PER_DEVICE (default 2) call contexts per device at once and overlap on the GPU; more callers wait for
+ * a free context.  Separate processes (PHP-FPM workers) each hold their own contexts.
  */
 #ifndef DWPA22000_H
 #define DWPA22000_H

@@ -53,3 +53,40 @@ def test_reader_words_match(tmp_path):
     exp = _expected([d for _, d in files])
     assert len(got) == len(exp)
     assert got == exp
+
+
+def test_reader_cache_replays_same_words(tmp_path):
+    """crack_files' ChunkSource keeps each dictionary it read to the end in the process-wide DictCache
+    (dict_reader.hpp) and replays it on the next work unit: the second and third passes over the same files yield
+    exactly the words of the first and the cache reports one hit per file and pass; DWPA_DICT_CACHE_MB=0 turns it
+    off."""
+    subprocess.run(["make", "-s", "-C", ROOT, "tools/bin/inflate_bench"], check=True)
+    rng = random.Random(62)
+    files = []
+    for k in range(3):
+        words = [bytes(rng.choice(b"abcdefghij0123456789") for _ in range(rng.randint(0, 20))) for _ in range(30_000)]
+        data = b"\n".join(words) + (b"\n" if k != 1 else b"")
+        path = tmp_path / ("w%d.txt.gz" % k)
+        with gzip.open(path, "wb", compresslevel=1) as f:
+            f.write(data)
+        files.append((str(path), data))
+
+    def passes(k, env=None):
+        r = subprocess.run([TOOL, "--passes", str(k)] + [p for p, _ in files], capture_output=True, check=True,
+                           env=env)
+        out, cur = [], None
+        for line in r.stdout.decode().split("\n")[:-1]:
+            if line.startswith("#pass"):
+                cur = [int(line.split()[3]), []]
+                out.append(cur)
+            else:
+                cur[1].append(bytes.fromhex(line))
+        return out
+
+    exp = sorted(_expected([d for _, d in files]))
+    got = passes(3)
+    assert [h for h, _ in got] == [0, 3, 6]
+    for _, words in got:
+        assert sorted(words) == exp
+    off = passes(2, env=dict(os.environ, DWPA_DICT_CACHE_MB="0"))
+    assert [h for h, _ in off] == [0, 0] and all(sorted(w) == exp for _, w in off)

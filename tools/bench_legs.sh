@@ -6,7 +6,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/legs}
 mkdir -p $OUT
-LEGS=${LEGS:-"peak c2 c4 c3 c5 c1 c2files"}
+LEGS=${LEGS:-"peak c2 c4 c3 c5 c5k2 c1 c2files c2files_warm"}
 for leg in $LEGS; do
   case $leg in
     peak)    OUT=$OUT/peak tools/regen_peak.sh > /dev/null ;;
@@ -14,9 +14,13 @@ for leg in $LEGS; do
     c4)      timeout -k 10 240 python3 bench.py --workload c4 --steps 8 --warmup 2 > $OUT/c4.json 2> $OUT/c4.err ;;
     c3)      timeout -k 10 300 python3 bench.py --workload c3 --steps 4 --warmup 1 > $OUT/c3.json 2> $OUT/c3.err ;;
     c5)      timeout -k 10 240 python3 bench.py --workload c5 --steps 20 --warmup 3 > $OUT/c5.json 2> $OUT/c5.err ;;
+    c5k2)    timeout -k 10 240 python3 bench.py --workload c5 --callers 2 --steps 20 --warmup 3 --no-cpu-baseline \
+               > $OUT/c5k2.json 2> $OUT/c5k2.err ;;
     c1)      timeout -k 10 240 python3 bench.py --workload c1 --steps 20 --warmup 3 > $OUT/c1.json 2> $OUT/c1.err ;;
     c2files) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c2files --steps 1 --warmup 0 \
                > $OUT/c2files.json 2> $OUT/c2files.err ;;
+    c2files_warm) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c2files --steps 1 --warmup 1 \
+               > $OUT/c2files_warm.json 2> $OUT/c2files_warm.err ;;
     *) echo "unknown leg $leg" >&2; exit 2 ;;
   esac
   echo "leg $leg done" >&2

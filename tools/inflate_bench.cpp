@@ -4,6 +4,8 @@
 //
 //   inflate_bench FILE.gz [FILE2.gz ...]
 //   inflate_bench --dump FILE... prints every word the reader yields, hex-encoded, one per line (tests/test_dict_reader.py)
+//   inflate_bench --passes K FILE... runs crack_files' ChunkSource K times over the files in one process (the second
+//     pass onwards replays the DictCache) and prints "#pass i cache_hits h" then that pass's words, hex-encoded
 //
 // Prints one JSON line: raw gzread throughput of the first file (inflate only), DictReader words/s on the first
 // file (one stream: an inflate thread feeding the line cutting + $HEX[] decoding thread), and ChunkSource words/s
@@ -25,6 +27,35 @@ int main(int argc, char** argv) {
     if (argc < 2) {
         fprintf(stderr, "usage: %s FILE.gz [FILE2.gz ...]\n", argv[0]);
         return 2;
+    }
+    auto hex_line = [](const dwpa::Chunk& c, size_t i, std::string& line) {
+        line.clear();
+        for (uint64_t k = c.off[i]; k < c.off[i + 1]; k++) {
+            static const char* d = "0123456789abcdef";
+            line.push_back(d[(uint8_t)c.bytes[k] >> 4]);
+            line.push_back(d[(uint8_t)c.bytes[k] & 15]);
+        }
+        line.push_back('\n');
+    };
+    if (std::string(argv[1]) == "--passes" && argc > 3) {
+        const int K = atoi(argv[2]);
+        std::vector<std::string> paths(argv + 3, argv + argc);
+        std::string line;
+        for (int pass = 0; pass < K; pass++) {
+            dwpa::ChunkSource src(paths, 1000, 1 << 16);
+            std::shared_ptr<const dwpa::Chunk> c;
+            bool err = false;
+            std::vector<std::shared_ptr<const dwpa::Chunk>> got;
+            while (src.next(c, err)) got.push_back(c);
+            if (err) return 1;
+            printf("#pass %d cache_hits %zu\n", pass, dwpa::DictCache::get().hits());
+            for (const auto& ch : got)
+                for (size_t i = 0; i < ch->words(); i++) {
+                    hex_line(*ch, i, line);
+                    fwrite(line.data(), 1, line.size(), stdout);
+                }
+        }
+        return 0;
     }
     if (std::string(argv[1]) == "--dump") {
         dwpa::DictReader rd(std::vector<std::string>(argv + 2, argv + argc));
