@@ -41,19 +41,20 @@ PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
 # over that workload's bench command (FETCH_SIZE doubled as MI355X_MICROARCH.md "HBM [CDNA4]" prescribes, plus
 # WRITE_SIZE; per-launch medians divided by the PMKs of the launch).  PMC counters cannot be read inside a timed
 # run, so the bench scales the measured per-PMK figure to its launches.
-#   c2/c4: k_pbkdf2_gfx950, profiles/r01/traffic (4,194,304-PMK launch): FETCH 167,954,944 B x 2 = 80 B/PMK (each of
-#          the two output-block lanes reads the 40-byte key midstate once) + WRITE 134,217,728 B = 32 B/PMK
-#   c3:    k_pbkdf2_gfx950_mg + k_verify<PMKID> + k_verify<keyver 2> per dwpa_scan_run (the roofline's events bracket
-#          all three), profiles/r02/traffic_post_kw/traffic_c3: 493.4 + 446.6 + 1,093.9 MB for 13,445,190 PMKs
-TRAFFIC_BYTES_PER_PMK = {"c2": (2 * 167954944 + 134217728) / 4194304, "c4": (2 * 167954944 + 134217728) / 4194304,
-                         "c3": (493.445e6 + 446.648e6 + 1093.881e6) / 13445190}
-TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950, profiles/r01/traffic (re-measured level in profiles/r02/traffic_post_kw)",
-                  "c4": "k_pbkdf2_gfx950 per PMK as measured on c2, profiles/r01/traffic",
-                  "c3": "k_pbkdf2_gfx950_mg + k_verify, profiles/r02/traffic_post_kw/traffic_c3"}
-# Algorithmic bytes per PMK: PBKDF2 reads the 40-byte key midstate twice (one lane per output block) and writes the
-# 32-byte PMK (c2/c4, the kernel the roofline names).  c3's events also bracket the verify, which reads each PMK
-# (32 B) and candidate id (8 B) once per hashline of its ESSID; its midstates are shared by all ESSID groups.
-ALGO_BYTES_PER_PMK = 80 + 32
+#   c2/c4: k_pbkdf2_gfx950_q (the work-queue kernel multi-round scans run), profiles/r02/traffic_q (16,777,216-PMK
+#          launch): FETCH 365,219,648 B x 2 = 43.5 B/PMK (a slot range's two output-block items are taken back to
+#          back, so the second read of each 40-byte key midstate is an L2 hit) + WRITE 553,910,272 B = 33.0 B/PMK
+#   c3:    k_pbkdf2_gfx950_mg_q + k_verify<PMKID> + k_verify<keyver 2> per dwpa_scan_run (the roofline's events
+#          bracket all three), profiles/r02/traffic_q3: 463.9 + 446.6 + 1,093.9 MB for 13,445,190 PMKs
+TRAFFIC_BYTES_PER_PMK = {"c2": (2 * 365219648 + 553910272) / 16777216, "c4": (2 * 365219648 + 553910272) / 16777216,
+                         "c3": (463.935e6 + 446.650e6 + 1093.884e6) / 13445190}
+TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950_q, profiles/r02/traffic_q",
+                  "c4": "k_pbkdf2_gfx950_q per PMK as measured on c2, profiles/r02/traffic_q",
+                  "c3": "k_pbkdf2_gfx950_mg_q + k_verify, profiles/r02/traffic_q3"}
+# Algorithmic bytes per PMK: PBKDF2 reads the 40-byte key midstate once and writes the 32-byte PMK (c2/c4, the
+# kernel the roofline names).  c3's events also bracket the verify, which reads each PMK (32 B) and candidate id
+# (8 B) once per hashline of its ESSID; its midstates are shared by all ESSID groups.
+ALGO_BYTES_PER_PMK = 40 + 32
 # Guide view (MI355X_MICROARCH.md: 4 SIMD-32 per CU, one VALU per 2 cycles = 128 int32 lane-ops/clk/CU at 2.4 GHz,
 # every op full rate).  Reported beside the issue-cost roofline, with SURVEY.md 8(d)'s ideal 617 ops per compression
 # and with the 575.5 VALU the kernel issues per compression (4,714,742 per wave / 8,192 compressions, PMC).  Not

@@ -433,6 +433,41 @@ def test_crack_files_several_shard_workers(tmp_path, capfd, monkeypatch):
     assert all(int(l.split(": ")[1].split(" items")[0]) > 0 for l in workers), workers
 
 
+def test_crack_files_dictionary_cache_next_work_unit(tmp_path, capfd, monkeypatch):
+    """Two work units over the same gz dictionary (help_crack keeps its dictionaries between work units,
+    help_crack.py:520-552): the first reads the file to its end (nothing cracks: rc 1) and leaves it decoded in the
+    process-wide DictCache; the second, against other nets, replays it from memory (the trace counts one more
+    replayed file) and finds its planted PSKs, including the file's last word."""
+    monkeypatch.setenv("DWPA_TRACE", "1")
+    rng = random.Random(53)
+    alnum = b"abcdefghijklmnopqrstuvwxyz0123456789"
+    words = [b"u%06d" % i + bytes(rng.choice(alnum) for _ in range(4)) for i in range(150_000)]
+    d = tmp_path / "dict.txt.gz"
+    with gzip.open(d, "wb", compresslevel=1) as f:
+        f.write(b"\n".join(words) + b"\n")
+
+    def unit(name, lines):
+        hf = tmp_path / (name + ".hash")
+        hf.write_bytes(b"\n".join(lines) + b"\n")
+        out = tmp_path / (name + ".key")
+        rc = dwpa_amd.crack_files(str(hf), [str(d)], None, 8, str(out), batch=1 << 14)
+        recs = out.read_bytes().strip().split(b"\n") if out.exists() and out.stat().st_size else []
+        err = capfd.readouterr().err
+        replayed = [int(l.split("cache: ")[1].split()[0]) for l in err.splitlines() if "dictionary cache" in l]
+        return rc, recs, replayed[-1]
+
+    essid, ap, sta, an, sn = S.random_net(rng)
+    rc, recs, before = unit("u1", [S.pmkid_line(b"not-in-the-dictionary", essid, ap, sta)])
+    assert rc == 1 and recs == []
+    essid2, ap2, sta2, an2, sn2 = S.random_net(rng)
+    psks = [words[70_001], words[-1]]
+    lines = [S.pmkid_line(psks[0], essid2, ap2, sta2),
+             S.eapol_line(psks[1], essid2, rng.randbytes(6), sta2, an2, sn2, 2, -2, "BE", rng=rng)]
+    rc, recs, after = unit("u2", lines)
+    assert rc == 0 and sorted(r.rsplit(b":", 1)[1] for r in recs) == sorted(psks)
+    assert after == before + 1
+
+
 @pytest.mark.skipif(os.environ.get("DWPA_PBKDF2_ISSUE") == "1", reason="already the forced issue-pass run")
 def test_issue_pass_kernels_at_small_sizes():
     """Launches of at most one wave per SIMD take the plain-schedule PBKDF2 kernel (pbkdf2_module.cpp), so the
