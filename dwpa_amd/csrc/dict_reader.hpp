@@ -4,7 +4,9 @@
 #pragma once
 #include <stdlib.h>
 #include <string.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -19,6 +21,7 @@
 #include <thread>
 #include <vector>
 
+#include "inflate.hpp"
 #include "m22000_host.hpp"
 
 namespace dwpa {
@@ -30,18 +33,25 @@ struct Chunk {
 };
 
 // Inflates files in order on a thread of its own into blocks of raw text, so that a single gz stream costs the line
-// cutting no inflate time: on the GPU box's EPYC 9575F one gzip stream inflates at ~320 MB/s (~28 M words/s of
-// C2-shaped words), while inflate + line cutting on one core reached 20-24 M words/s (profiles/r02/legs,
-// tools/inflate_bench).  A block with file_end set closes a file (its last line may lack the '\n').
+// cutting no inflate time.  gzip files go through GzipDecoder (inflate.hpp: ~2x zlib 1.2.11's inflate on a host
+// core; DWPA_INFLATE=zlib switches back to gzread for A/B), other files are read as they are.  A block with file_end
+// set closes a file (its last line may lack the '\n').  Block buffers are recycled (next() hands the previous one
+// back), so a 4 MiB block is neither allocated nor zero-filled per block.
 class BlockInflater {
   public:
+    static constexpr size_t BLOCK = 4u << 20, DEPTH = 4;
     struct Block {
-        std::string data;
+        std::vector<uint8_t> buf;  // [0, WIN): history for back-references; text at [begin, end)
+        size_t begin = 0, end = 0;
         bool file_end = false;
         bool err = false;
+        const char* data() const { return (const char*)buf.data() + begin; }
+        size_t size() const { return end - begin; }
     };
     BlockInflater(std::vector<std::string> paths, const std::atomic<bool>* cancel)
         : paths_(std::move(paths)), cancel_(cancel) {
+        const char* e = getenv("DWPA_INFLATE");
+        zlib_ = e && !strcmp(e, "zlib");
         th_ = std::thread([this] { run(); });
     }
     ~BlockInflater() {
@@ -52,9 +62,10 @@ class BlockInflater {
         cv_.notify_all();
         th_.join();
     }
-    // Blocks until the next block; false once every file has been delivered.
+    // Blocks until the next block (b's previous buffer goes back to the pool); false once every file is delivered.
     bool next(Block& b) {
         std::unique_lock<std::mutex> lk(mu_);
+        if (!b.buf.empty()) free_.push_back(std::move(b.buf));
         cv_.wait(lk, [&] { return !q_.empty() || done_; });
         if (q_.empty()) return false;
         b = std::move(q_.front());
@@ -64,7 +75,7 @@ class BlockInflater {
     }
 
   private:
-    static constexpr size_t BLOCK = 4u << 20, DEPTH = 4;
+    static constexpr size_t BUFSZ = GzipDecoder::WIN + BLOCK + GzipDecoder::SLACK;
     bool push(Block&& b) {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return q_.size() < DEPTH || stop_; });
@@ -73,46 +84,97 @@ class BlockInflater {
         cv_.notify_all();
         return true;
     }
-    bool cancelled() const { return (cancel_ && cancel_->load(std::memory_order_relaxed)); }
-    void run() {
-        for (const std::string& path : paths_) {
-            gzFile gz = gzopen(path.c_str(), "rb");
-            if (!gz) {
-                Block e;
-                e.err = true;
-                push(std::move(e));
-                break;
+    Block fresh() {
+        Block b;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!free_.empty()) {
+                b.buf = std::move(free_.back());
+                free_.pop_back();
             }
-            gzbuffer(gz, 1 << 20);
-            bool ok = true, eof = false;
-            while (ok && !eof && !cancelled()) {
-                Block b;
-                b.data.resize(BLOCK);
-                size_t n = 0;
-                while (n < BLOCK) {
-                    const int r = gzread(gz, &b.data[n], (unsigned)(BLOCK - n));
+        }
+        if (b.buf.size() != BUFSZ) b.buf.resize(BUFSZ);
+        b.begin = b.end = GzipDecoder::WIN;
+        return b;
+    }
+    bool cancelled() const { return (cancel_ && cancel_->load(std::memory_order_relaxed)); }
+    bool error_block() {
+        Block e;
+        e.err = true;
+        push(std::move(e));
+        return false;
+    }
+    // one file; false ends the stream (error or cancel)
+    bool file(const std::string& path) {
+        const int fd = open(path.c_str(), O_RDONLY);
+        if (fd < 0) return error_block();
+        uint8_t magic[2] = {0, 0};
+        const bool gz = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+        bool ok = true;
+        if (gz && zlib_) {
+            ok = file_zlib(fd);
+        } else if (gz) {
+            GzipDecoder dec(fd);
+            for (bool end = false; ok && !end && !cancelled();) {
+                Block b = fresh();
+                b.end = b.begin + dec.read(b.buf.data(), BLOCK);
+                b.err = dec.failed();
+                end = dec.done() || b.err;
+                b.file_end = end;
+                ok = push(std::move(b)) && !dec.failed();
+            }
+        } else {
+            for (bool end = false; ok && !end && !cancelled();) {
+                Block b = fresh();
+                while (b.end < b.begin + BLOCK) {
+                    const ssize_t r = ::read(fd, b.buf.data() + b.end, b.begin + BLOCK - b.end);
                     if (r < 0) { b.err = true; break; }
-                    if (r == 0) { eof = true; break; }
-                    n += (size_t)r;
+                    if (r == 0) { end = true; break; }
+                    b.end += (size_t)r;
                 }
-                b.data.resize(n);
-                b.file_end = eof;
+                b.file_end = end || b.err;
                 const bool err = b.err;
                 ok = push(std::move(b)) && !err;
             }
-            gzclose(gz);
-            if (!ok || cancelled()) break;
         }
+        close(fd);
+        return ok;
+    }
+    bool file_zlib(int fd) {
+        gzFile gz = gzdopen(dup(fd), "rb");
+        if (!gz) return error_block();
+        gzbuffer(gz, 1 << 20);
+        bool ok = true, eof = false;
+        while (ok && !eof && !cancelled()) {
+            Block b = fresh();
+            while (b.end < b.begin + BLOCK) {
+                const int r = gzread(gz, b.buf.data() + b.end, (unsigned)(b.begin + BLOCK - b.end));
+                if (r < 0) { b.err = true; break; }
+                if (r == 0) { eof = true; break; }
+                b.end += (size_t)r;
+            }
+            b.file_end = eof || b.err;
+            const bool err = b.err;
+            ok = push(std::move(b)) && !err;
+        }
+        gzclose(gz);
+        return ok;
+    }
+    void run() {
+        for (const std::string& path : paths_)
+            if (!file(path) || cancelled()) break;
         std::lock_guard<std::mutex> lk(mu_);
         done_ = true;
         cv_.notify_all();
     }
     std::vector<std::string> paths_;
     const std::atomic<bool>* cancel_;
+    bool zlib_ = false;
     std::thread th_;
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<Block> q_;
+    std::vector<std::vector<uint8_t>> free_;
     bool stop_ = false, done_ = false;
 };
 
@@ -130,7 +192,7 @@ class DictReader {
         c.off.push_back(0);
         while (c.words() < max_words && c.bytes.size() < max_bytes) {
             if (cancel && cancel->load(std::memory_order_relaxed)) break;
-            if (pos_ >= blk_.data.size()) {
+            if (pos_ >= blk_.size()) {
                 if (blk_.file_end) {  // end of a file: a last line without '\n' is still a word
                     if (!partial_.empty()) emit(c, partial_.data(), partial_.size());
                     partial_.clear();
@@ -142,9 +204,9 @@ class DictReader {
                 pos_ = 0;
                 continue;
             }
-            const char* base = blk_.data.data();
+            const char* base = blk_.data();
             const char* p = base + pos_;
-            const char* end = base + blk_.data.size();
+            const char* end = base + blk_.size();
             while (p < end && c.words() < max_words && c.bytes.size() < max_bytes) {
                 const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
                 if (!nl) {

@@ -108,14 +108,54 @@ struct PinnedArena {
 // ---------------------------------------------------------------------------------------------------------
 // global state
 // ---------------------------------------------------------------------------------------------------------
-// One candidate key of one job in the check path (explicit keys -> slots).
-struct Slot {
-    std::string_view key;     // bytes hashed (after hc_unhex): the caller's buffer or a decoded copy
-    uint32_t job;
-    uint32_t ordinal;         // index among the job's non-null keys
-    const std::string* essid;
-    uint64_t hash;            // hash_bytes(key): computed where the key is first read (dedup never re-reads it)
-    bool pbkdf2;              // false: PMK supplied by the caller
+// The check path's candidate slots (explicit keys) in slot order: ESSID groups in first-seen order, jobs in input
+// order within a group, keys in order within a job.  Flat arrays that keep their capacity (and their pages)
+// between calls; the key bytes ($HEX[] decoded) sit in pinned memory, so they go up with one DMA and the unique
+// keys are never copied on the host (k_prep_keys reads them through uslot).
+constexpr uint32_t SLOT_CALLER = 0x80000000u;  // ord flag: the PMK comes from the caller (common.php:178)
+struct SlotTable {
+    std::vector<uint32_t> job;   // slot -> job
+    std::vector<uint32_t> ord;   // key ordinal among the job's non-null keys (selects its attempt list) | SLOT_CALLER
+    std::vector<uint64_t> hash;  // hash_key of the key, taken while its bytes are in cache
+    PinnedArena mem;             // koff[n], klen[n], key bytes
+    uint64_t* koff = nullptr;
+    uint32_t* klen = nullptr;
+    uint8_t* kbytes = nullptr;
+    size_t n = 0, nbytes = 0;    // slots; capacity of kbytes (upper bound of the decoded bytes)
+    int reserve(size_t slots, size_t bytes) {
+        RCHK(mem.reset(12 * slots + bytes + 16 + 4 * 64));
+        koff = mem.take<uint64_t>(slots);
+        klen = mem.take<uint32_t>(slots);
+        kbytes = mem.take<uint8_t>(bytes + 16);  // + 16: load_key_block reads whole dwords
+        memset(kbytes + bytes, 0, 16);
+        job.resize(slots);
+        ord.resize(slots);
+        hash.resize(slots);
+        n = slots;
+        nbytes = bytes;
+        return 0;
+    }
+    std::string_view key(size_t i) const { return {(const char*)kbytes + koff[i], klen[i]}; }
+};
+
+// Per-run dedup output of one host thread (derive_slots); kept in the call context so its vectors keep capacity.
+struct DedupPart {
+    std::vector<uint32_t> uslot, sref, spool, cpmk, table, sb;  // sref: offsets into this part's spool
+    std::vector<uint64_t> uhash;
+    size_t rb = 0, re = 0, ubase = 0, sbase = 0, cbase = 0;
+};
+
+// Per-job scratch of the check path's host phases (capacity kept between calls).
+struct CheckScratch {
+    std::vector<ParsedLine> parsed;
+    std::vector<uint32_t> nnz;          // non-null keys of a job that can match (0: no slots)
+    std::vector<uint64_t> jbytes;       // their raw bytes (upper bound of the decoded bytes)
+    std::vector<uint32_t> jslot;        // first slot of a job
+    std::vector<uint64_t> jbyte;        // first key byte of a job
+    std::vector<uint32_t> gid, order;   // job -> ESSID group; jobs in slot order (group-major)
+    std::vector<uint32_t> gstart, gslot, gfill;  // per group: first entry of `order`, first slot
+    std::vector<const uint8_t*> job_pmk;
+    std::unordered_map<std::string_view, uint32_t> essid_id;
 };
 
 // Host-mapped pinned buffer that kernels write directly (hit copy-out, k_hits_out).
@@ -158,10 +198,12 @@ struct Device {
     MappedHost hits_host;         // check path: hit count + hits written by k_hits_out
     std::mutex mu;
     Batch batch;
-    DevBuf lines, atts, pool, segs, segs_tail, salt, koff, kbytes, idsup;
+    DevBuf lines, atts, pool, segs, segs_tail, salt, koff, kbytes, idsup, klen, uslot;
     DevBuf keys, keys_tail;        // check path: per-key EapolKey scratch of the attempt-parallel verify
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
-    std::vector<Slot> slots;       // check path: the call's slots (capacity kept between calls)
+    SlotTable slots;               // check path: the call's slots (capacity kept between calls)
+    CheckScratch cs;               // check path: host-phase scratch
+    std::vector<DedupPart> parts;  // check path: dedup output per host thread
 };
 
 static std::mutex g_mu;
@@ -301,18 +343,30 @@ static void pmk_bytes(const uint32_t w[8], uint8_t out[32]) {
 // explicit keys -> slots (server-side check path and dwpa_pbkdf2_pmk)
 // ---------------------------------------------------------------------------------------------------------
 
-// 64-bit hash of a byte string (8-byte multiply-xor rounds) for the (ESSID run, key) dedup table.
-static uint64_t hash_bytes(const char* p, size_t n, uint64_t seed) {
-    uint64_t h = seed ^ (n * 0x9e3779b97f4a7c15ull);
-    for (; n >= 8; p += 8, n -= 8) {
-        uint64_t w;
-        memcpy(&w, p, 8);
-        h = (h ^ w) * 0xff51afd7ed558ccdull;
-        h ^= h >> 32;
+// 64-bit hash of a key (8-byte multiply-xor rounds) for the (ESSID run, key) dedup table.  Reads only the key's
+// own bytes, with overlapping loads for the tail: it runs on the caller's buffers, before the bytes are copied
+// (hashing the fresh copy would stall on store-to-load forwarding).
+static uint64_t hash_key(const uint8_t* p, size_t n) {
+    uint64_t h = n * 0x9e3779b97f4a7c15ull, w;
+    if (n >= 8) {
+        const uint8_t* end = p + n;
+        for (; p + 8 <= end; p += 8) {
+            memcpy(&w, p, 8);
+            h = (h ^ w) * 0xff51afd7ed558ccdull;
+            h ^= h >> 32;
+        }
+        if (p == end) return h ^ (h >> 29);
+        memcpy(&w, end - 8, 8);  // the last 8 bytes (overlapping the previous block)
+    } else if (n >= 4) {
+        uint32_t a, b;
+        memcpy(&a, p, 4);
+        memcpy(&b, p + n - 4, 4);
+        w = (uint64_t)b << 32 | a;
+    } else {
+        w = 0;
+        for (size_t k = 0; k < n; k++) w |= (uint64_t)p[k] << (8 * k);
     }
-    uint64_t t = 0;
-    for (size_t k = 0; k < n; k++) t |= (uint64_t)(uint8_t)p[k] << (8 * k);
-    h = (h ^ t) * 0xc4ceb9fe1a85ec53ull;
+    h = (h ^ w) * 0xc4ceb9fe1a85ec53ull;
     return h ^ (h >> 29);
 }
 
@@ -424,9 +478,8 @@ static int upload_span(DevBuf& b, const Span<T>& v, hipStream_t s) {
 
 // Host staging of one derive step in the device's pinned arena; valid until the stream is synchronised.
 struct DeriveStage {
-    Span<uint64_t> off, ids;
-    Span<uint8_t> bytes;
-    Span<uint32_t> src, sref, spool, cpmk;
+    Span<uint64_t> ids;
+    Span<uint32_t> src, sref, spool, cpmk, uslot;
     uint32_t split = 0;  // slots [0, split) read d.stream's PMKs; [split, n) d.tail's (== n: no tail)
 };
 
@@ -451,15 +504,16 @@ static uint32_t head_pmks(uint32_t nu) {
     return nu / unit * unit;
 }
 
-// Derive the PMKs of slots [b, e) into batch.pmk (slot order) and their key ordinals into batch.ids.  Unique
+// Derive the PMKs of slots [b, e) of T into batch.pmk (slot order) and their key ordinals into batch.ids.  Unique
 // (ESSID, key) pairs are derived once, all ESSIDs in one PBKDF2 launch (server batches fan one key out to every
 // net of an ESSID, common.php:879-902); each slot then gathers its PMK from them or from the caller's $pmk
 // (common.php:178).  Slots arrive grouped by ESSID: `runs` holds the starts of the ESSID runs relative to b plus
-// n = e - b, and keybytes the key bytes of the range.  The uploads are queued ahead of the launches: a pageable
-// upload queued behind a running kernel would block the host until that kernel ends.
-static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, size_t e,
-                        const std::vector<const uint8_t*>& job_pmk, const std::vector<uint32_t>& runs,
-                        size_t keybytes, DeriveStage& st) {
+// n = e - b, run_essid each run's ESSID.  upload_keys: send T's key bytes (every slot of the call) up first.  The
+// uploads are queued ahead of the launches: a pageable upload queued behind a running kernel would block the host
+// until that kernel ends.
+static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const std::vector<const uint8_t*>& job_pmk,
+                        const std::vector<uint32_t>& runs, const std::vector<const std::string*>& run_essid,
+                        bool upload_keys, DeriveStage& st) {
     PhaseTrace tr;
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
@@ -467,44 +521,44 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     size_t saltwords = 0;
     const size_t nruns = runs.size() - 1;
     for (size_t r = 0; r < nruns; r++)  // count word + [2][nblk][16], nblk = SHA-1 blocks of ESSID || INT(i) || pad
-        saltwords += 1 + 32 * ((slots[b + runs[r]].essid->size() + 4 + 9 + 63) / 64);
-    // pinned staging, sized by upper bounds: <= n unique keys, <= keybytes key bytes, <= n caller PMKs
-    RCHK(d.stage.reset(8 * (n + 1) + keybytes + 8 + 4 * (size_t)n + 4 * saltwords + 32 * (size_t)n + 4 * (size_t)n +
-                       8 * (size_t)n + 8 * 64));
+        saltwords += 1 + 32 * ((run_essid[r]->size() + 4 + 9 + 63) / 64);
+    // pinned staging, sized by upper bounds: <= n unique keys, <= n caller PMKs
+    RCHK(d.stage.reset(12 * (size_t)n + 8 * (size_t)n + 4 * saltwords + 32 * (size_t)n + 8 * 64));
     st.src = take<uint32_t>(d.stage, n);
     st.ids = take<uint64_t>(d.stage, n);
     // Runs are deduplicated independently (one small open-addressing table per run keeps it cache-resident), on
-    // up to 8 host threads that each take a contiguous block of runs; the parts are then concatenated.
-    struct Part {
-        std::vector<std::string_view> ukeys;
-        std::vector<uint32_t> sref, spool, cpmk;  // sref: offsets into this part's spool
-        size_t rb = 0, re = 0, ubase = 0, sbase = 0, cbase = 0, bbase = 0;
-    };
-    const size_t T = host_threads(n, 16384);
-    std::vector<Part> parts(std::min(T, nruns));
-    for (size_t t = 0; t < parts.size(); t++) {  // split runs so that parts hold about equal slot counts
-        parts[t].rb = t ? parts[t - 1].re : 0;
-        const uint64_t goal = (uint64_t)n * (t + 1) / parts.size();
-        size_t r = parts[t].rb;
-        while (r < nruns && (runs[r + 1] <= goal || r == parts[t].rb)) r++;
-        parts[t].re = t + 1 == parts.size() ? nruns : r;
+    // up to 16 host threads that each take a contiguous block of runs; the parts are then concatenated.
+    const size_t T_ = host_threads(n, 8192);
+    const size_t np = std::max<size_t>(1, std::min(T_, nruns));
+    if (d.parts.size() < np) d.parts.resize(np);
+    for (size_t t = 0; t < np; t++) {  // split runs so that parts hold about equal slot counts
+        DedupPart& P = d.parts[t];
+        P.rb = t ? d.parts[t - 1].re : 0;
+        const uint64_t goal = (uint64_t)n * (t + 1) / np;
+        size_t r = P.rb;
+        while (r < nruns && (runs[r + 1] <= goal || r == P.rb)) r++;
+        P.re = t + 1 == np ? nruns : r;
     }
-    parallel_for(parts.size(), [&](size_t t) {
-        Part& P = parts[t];
-        std::vector<uint32_t> table;
-        std::vector<uint64_t> uhash;
+    parallel_for(np, [&](size_t t) {
+        DedupPart& P = d.parts[t];
+        P.uslot.clear();
+        P.sref.clear();
+        P.spool.clear();
+        P.cpmk.clear();
         for (size_t r = P.rb; r < P.re; r++) {
             const uint32_t i0 = runs[r], i1 = runs[r + 1];
             size_t tcap = 16;
             while (tcap < 2 * (size_t)(i1 - i0)) tcap <<= 1;
-            table.assign(tcap, UINT32_MAX);
-            const size_t u0 = P.ukeys.size();
+            P.table.assign(tcap, UINT32_MAX);
+            P.uhash.clear();
+            const size_t u0 = P.uslot.size();
             uint32_t cur_ref = UINT32_MAX;
             for (uint32_t i = i0; i < i1; i++) {
-                const Slot& sl = slots[b + i];
-                st.ids[i] = sl.ordinal;  // selects the PHP attempt list of the key
-                if (!sl.pbkdf2) {
-                    const uint8_t* p = job_pmk[sl.job];
+                const size_t si = b + i;
+                const uint32_t ord = T.ord[si];
+                st.ids[i] = ord & ~SLOT_CALLER;  // selects the PHP attempt list of the key
+                if (ord & SLOT_CALLER) {
+                    const uint8_t* p = job_pmk[T.job[si]];
                     st.src[i] = GATHER_CALLER | (uint32_t)(P.cpmk.size() / 8);
                     for (int k = 0; k < 8; k++)
                         P.cpmk.push_back((uint32_t)p[4 * k] << 24 | (uint32_t)p[4 * k + 1] << 16 |
@@ -512,66 +566,54 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
                     continue;
                 }
                 if (cur_ref == UINT32_MAX) {
-                    std::vector<uint32_t> sb;
-                    const uint32_t nb = build_salt_blocks(*sl.essid, sb);
+                    P.sb.clear();
+                    const uint32_t nb = build_salt_blocks(*run_essid[r], P.sb);
                     cur_ref = (uint32_t)P.spool.size();
                     P.spool.push_back(nb);
-                    P.spool.insert(P.spool.end(), sb.begin(), sb.end());
+                    P.spool.insert(P.spool.end(), P.sb.begin(), P.sb.end());
                 }
-                const uint64_t h = sl.hash;
+                const uint64_t h = T.hash[si];
                 size_t pos = h & (tcap - 1);
                 uint32_t u;
-                while ((u = table[pos]) != UINT32_MAX && !(uhash[u - u0] == h && P.ukeys[u] == sl.key))
+                while ((u = P.table[pos]) != UINT32_MAX && !(P.uhash[u - u0] == h && T.key(P.uslot[u]) == T.key(si)))
                     pos = (pos + 1) & (tcap - 1);
                 if (u == UINT32_MAX) {
-                    u = (uint32_t)P.ukeys.size();
-                    table[pos] = u;
-                    P.ukeys.push_back(sl.key);
-                    uhash.push_back(h);
+                    u = (uint32_t)P.uslot.size();
+                    P.table[pos] = u;
+                    P.uslot.push_back((uint32_t)si);
+                    P.uhash.push_back(h);
                     P.sref.push_back(cur_ref);
                 }
                 st.src[i] = u;  // part-local; rebased below
             }
-            uhash.clear();
         }
     });
     tr.mark("  dedup tables");
-    size_t nu_total = 0, nsp = 0, ncp = 0, nbytes = 0;
-    for (Part& P : parts) {
+    size_t nu_total = 0, nsp = 0, ncp = 0;
+    for (size_t t = 0; t < np; t++) {
+        DedupPart& P = d.parts[t];
         P.ubase = nu_total;
         P.sbase = nsp;
         P.cbase = ncp;
-        P.bbase = nbytes;
-        nu_total += P.ukeys.size();
+        nu_total += P.uslot.size();
         nsp += P.spool.size();
         ncp += P.cpmk.size() / 8;
-        for (std::string_view k : P.ukeys) nbytes += k.size();
     }
     const uint32_t nu = (uint32_t)nu_total;
     st.sref = take<uint32_t>(d.stage, nu);
+    st.uslot = take<uint32_t>(d.stage, nu);
     st.spool = take<uint32_t>(d.stage, nsp);
     st.cpmk = take<uint32_t>(d.stage, ncp * 8);
-    st.off = take<uint64_t>(d.stage, nu + 1);
-    st.bytes = take<uint8_t>(d.stage, nbytes + 8);
     if (d.stage.used > d.stage.cap) return DWPA_E_ARG;  // the bounds above are exact upper bounds
-    memset(st.bytes.data() + nbytes, 0, 8);
-    // rebase and concatenate; unique keys -> offsets/bytes (back to back: k_prep_dict derives len from offsets)
-    parallel_for(parts.size(), [&](size_t t) {
-        const Part& P = parts[t];
+    parallel_for(np, [&](size_t t) {  // rebase and concatenate (no key bytes move: k_prep_keys reads them by slot)
+        const DedupPart& P = d.parts[t];
         for (uint32_t i = runs[P.rb]; i < runs[P.re]; i++)
             st.src[i] = (st.src[i] & GATHER_CALLER) ? st.src[i] + (uint32_t)P.cbase : st.src[i] + (uint32_t)P.ubase;
-        for (size_t u = 0; u < P.ukeys.size(); u++) st.sref[P.ubase + u] = P.sref[u] + (uint32_t)P.sbase;
+        for (size_t u = 0; u < P.uslot.size(); u++) st.sref[P.ubase + u] = P.sref[u] + (uint32_t)P.sbase;
+        std::copy(P.uslot.begin(), P.uslot.end(), st.uslot.data() + P.ubase);
         std::copy(P.spool.begin(), P.spool.end(), st.spool.data() + P.sbase);
         std::copy(P.cpmk.begin(), P.cpmk.end(), st.cpmk.data() + 8 * P.cbase);
-        size_t pos = P.bbase;
-        for (size_t u = 0; u < P.ukeys.size(); u++) {
-            if (u + 16 < P.ukeys.size()) __builtin_prefetch(P.ukeys[u + 16].data());
-            st.off[P.ubase + u] = pos;
-            memcpy(st.bytes.data() + pos, P.ukeys[u].data(), P.ukeys[u].size());
-            pos += P.ukeys[u].size();
-        }
     });
-    st.off[nu] = nbytes;
     tr.mark("  concat");
 
     RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
@@ -585,9 +627,13 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
                 st.split = i;
                 break;
             }
+    if (upload_keys) {
+        RCHK(upload_span(d.koff, Span<uint64_t>{T.koff, T.n}, s));
+        RCHK(upload_span(d.klen, Span<uint32_t>{T.klen, T.n}, s));
+        RCHK(upload_span(d.kbytes, Span<uint8_t>{T.kbytes, T.nbytes + 16}, s));
+    }
     if (nu) {
-        RCHK(upload_span(d.koff, st.off, s));
-        RCHK(upload_span(d.kbytes, st.bytes, s));
+        RCHK(upload_span(d.uslot, st.uslot, s));
         RCHK(upload_span(d.salt, st.spool, s));
         RCHK(upload_span(d.sref, st.sref, s));
     }
@@ -602,8 +648,8 @@ static int derive_slots(Device& d, const std::vector<Slot>& slots, size_t b, siz
     const uint32_t* sref = (const uint32_t*)d.sref.p;
     uint32_t* upmk = (uint32_t*)d.upmk.p;
     if (nu) {
-        HIPCHK(launch_prep_dict((const uint64_t*)d.koff.p, (const uint8_t*)d.kbytes.p, 0, nu, 0, 0xffffffffu,
-                                (uint32_t*)d.batch.mid.p, nullptr, nullptr, cap, false, s));
+        HIPCHK(launch_prep_keys((const uint64_t*)d.koff.p, (const uint32_t*)d.klen.p, (const uint8_t*)d.kbytes.p,
+                                (const uint32_t*)d.uslot.p, nu, (uint32_t*)d.batch.mid.p, cap, s));
         HeadFence& f = *g_fence[d.id];
         std::lock_guard<std::mutex> fl(f.mu);
         if (head_fence_knob() && f.last && f.last != d.head_end) HIPCHK(hipStreamWaitEvent(s, f.last, 0));
@@ -644,7 +690,7 @@ static int join_tail(Device& d) {
 // s.  The line tables go up on the side stream (while PBKDF2 may still run) and s waits for them.  EAPOL lines with
 // wide nonce windows use the attempt-parallel kernel (a wave per key, lanes = attempts), the rest the key-parallel
 // one; segments are runs of <= 64 consecutive slots of one job.  Hits are appended on the device (collect_hits).
-static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, size_t b, size_t e,
+static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, size_t e,
                         const std::vector<uint32_t>& job_line, const TableBuilder& tb, bool upload_tables,
                         hipStream_t s, DevBuf& segbuf, DevBuf& keybuf, bool fanout) {
     const uint32_t n = (uint32_t)(e - b), row0 = (uint32_t)(b - base);
@@ -656,8 +702,8 @@ static int queue_verify(Device& d, const std::vector<Slot>& slots, size_t base, 
     auto bucket_vc = [](int k) { return k == 5 ? (uint32_t)(VC_KV1 | VC_KV2) : 1u << (k & 3); };
     for (uint32_t i = 0; i < n;) {
         uint32_t j = i;
-        const uint32_t job = slots[b + i].job;
-        while (j < n && slots[b + j].job == job && j - i < 64) j++;
+        const uint32_t job = T.job[b + i];
+        while (j < n && T.job[b + j] == job && j - i < 64) j++;
         const uint32_t li = job_line[job];
         const LineDev& L = tb.lines[li];
         const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
@@ -789,126 +835,156 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     RCHK(device_stream(d));
 
     PhaseTrace tr;
-    std::vector<ParsedLine> parsed(njobs);
-    std::vector<uint32_t> job_line(njobs, 0);
-    std::vector<const uint8_t*> job_pmk(njobs, nullptr);
-    std::vector<std::vector<std::string_view>> keys(njobs);
-    std::vector<std::vector<uint32_t>> key_index(njobs);
-    std::vector<std::vector<uint64_t>> key_hash(njobs);  // hash_bytes of each key, taken while its bytes are in cache
-    std::vector<size_t> job_bytes(njobs, 0);
+    CheckScratch& cs = d.cs;
+    cs.parsed.resize(njobs);
+    cs.nnz.assign(njobs, 0);
+    cs.jbytes.assign(njobs, 0);
+    cs.jslot.resize(njobs);
+    cs.jbyte.resize(njobs);
+    cs.job_pmk.assign(njobs, nullptr);
+    // phase 1, per job: parse (PHP rules), count the non-null keys and their bytes
     const size_t TP = host_threads(njobs, 64);
-    std::vector<std::deque<std::string>> unhexed(TP);  // decoded $HEX[] keys (stable addresses), per thread
     parallel_for(TP, [&](size_t t) {
-      for (size_t j = njobs * t / TP; j < njobs * (t + 1) / TP; j++) {
-        out[j].key_index = -1;
-        out[j].nc = 0;
-        out[j].endian = 0;
-        out[j].nc_valid = 0;
-        memset(out[j].pmk, 0, 32);
-        parsed[j] = parse_m22000(jobs[j].line, jobs[j].line_len);
-        rcs[j] = parsed[j].status;
-        if (parsed[j].status) continue;
-        rcs[j] = DWPA_MISS;
-        if (!line_can_match(parsed[j])) continue;  // PMKID/MIC shorter than 16 bytes never verifies
-        keys[j].reserve(jobs[j].nkeys);
-        key_index[j].reserve(jobs[j].nkeys);
-        key_hash[j].reserve(jobs[j].nkeys);
-        for (size_t k = 0; k < jobs[j].nkeys; k++) {
-            // caller keys are scattered (one PHP string / Python bytes object each): prefetch ahead
-            if (k + 16 < jobs[j].nkeys && jobs[j].keys[k + 16].ptr) __builtin_prefetch(jobs[j].keys[k + 16].ptr);
-            const dwpa_bytes& kb = jobs[j].keys[k];
-            if (!kb.ptr) continue;  // is_null($key): skipped (common.php:172,240)
-            std::string_view key((const char*)kb.ptr, kb.len);
-            if (starts_hex(kb.ptr, kb.len)) {
-                unhexed[t].push_back(hc_unhex(std::string(key)));
-                key = unhexed[t].back();
-            }
-            keys[j].push_back(key);
-            key_index[j].push_back((uint32_t)k);
-            key_hash[j].push_back(hash_bytes(key.data(), key.size(), 0));
-            job_bytes[j] += key.size();
+        for (size_t j = njobs * t / TP; j < njobs * (t + 1) / TP; j++) {
+            out[j].key_index = -1;
+            out[j].nc = 0;
+            out[j].endian = 0;
+            out[j].nc_valid = 0;
+            memset(out[j].pmk, 0, 32);
+            ParsedLine& pl = cs.parsed[j];
+            parse_m22000_into(jobs[j].line, jobs[j].line_len, pl);
+            rcs[j] = pl.status;
+            if (pl.status) continue;
+            rcs[j] = DWPA_MISS;
+            cs.job_pmk[j] = jobs[j].pmk;
+            if (!line_can_match(pl)) continue;  // PMKID/MIC shorter than 16 bytes never verifies
+            uint32_t c = 0;
+            uint64_t by = 0;
+            for (size_t k = 0; k < jobs[j].nkeys; k++)
+                if (jobs[j].keys[k].ptr) {  // is_null($key): skipped (common.php:172,240)
+                    c++;
+                    by += jobs[j].keys[k].len;
+                }
+            cs.nnz[j] = c;
+            cs.jbytes[j] = by;
         }
-        job_pmk[j] = jobs[j].pmk;
-      }
     });
-    tr.mark("parse+keys");
-    // slots grouped by ESSID (jobs in input order within an ESSID, keys in order within a job)
-    std::unordered_map<std::string_view, uint32_t> essid_id;
-    std::vector<std::vector<uint32_t>> by_essid;
-    size_t nslots = 0;
+    tr.mark("parse");
+    // phase 2: ESSID groups in first-seen order, jobs in input order within a group -> slot and byte bases
+    cs.essid_id.clear();
+    cs.gid.assign(njobs, UINT32_MAX);
+    cs.gstart.clear();
     for (size_t j = 0; j < njobs; j++) {
-        if (rcs[j] != DWPA_MISS || keys[j].empty()) continue;
-        auto ins = essid_id.try_emplace(std::string_view(parsed[j].essid), (uint32_t)by_essid.size());
-        if (ins.second) by_essid.emplace_back();
-        by_essid[ins.first->second].push_back((uint32_t)j);
-        nslots += keys[j].size();
+        if (!cs.nnz[j]) continue;
+        auto ins = cs.essid_id.try_emplace(std::string_view(cs.parsed[j].essid), (uint32_t)cs.gstart.size());
+        if (ins.second) cs.gstart.push_back(0);
+        cs.gid[j] = ins.first->second;
+        cs.gstart[cs.gid[j]]++;  // count for now
     }
+    const size_t G = cs.gstart.size();
+    cs.gstart.push_back(0);
+    for (size_t g = 0, acc = 0; g <= G; g++) {  // counts -> starts
+        const size_t c = cs.gstart[g];
+        cs.gstart[g] = (uint32_t)acc;
+        acc += c;
+    }
+    cs.order.resize(cs.gstart[G]);
+    cs.gfill.assign(cs.gstart.begin(), cs.gstart.end() - 1);
+    for (size_t j = 0; j < njobs; j++)
+        if (cs.gid[j] != UINT32_MAX) cs.order[cs.gfill[cs.gid[j]]++] = (uint32_t)j;
+    cs.gslot.resize(G + 1);
+    size_t nslots = 0, nbytes = 0;
+    for (size_t g = 0; g < G; g++) {
+        cs.gslot[g] = (uint32_t)nslots;
+        for (uint32_t q = cs.gstart[g]; q < cs.gstart[g + 1]; q++) {
+            const uint32_t j = cs.order[q];
+            cs.jslot[j] = (uint32_t)nslots;
+            cs.jbyte[j] = nbytes;
+            nslots += cs.nnz[j];
+            nbytes += cs.jbytes[j];
+        }
+    }
+    cs.gslot[G] = (uint32_t)nslots;
     if (!nslots) return 0;
+    if (nslots >= SLOT_CALLER) return DWPA_E_ARG;
     tr.mark("essid groups");
-    // slot order: ESSID groups in first-seen order, jobs in input order, keys in order; filled per group range on
-    // up to 8 host threads (contiguous group ranges of about equal slot counts)
-    // the device's slot buffer keeps its pages between calls (a fresh 8 MB vector per C5 call page-faults)
-    std::vector<Slot>& slots = d.slots;
-    slots.resize(nslots);
-    std::vector<size_t> gbase(by_essid.size() + 1, 0);
-    for (size_t g = 0; g < by_essid.size(); g++) {
-        gbase[g + 1] = gbase[g];
-        for (uint32_t j : by_essid[g]) gbase[g + 1] += keys[j].size();
-    }
-    const size_t TS = std::min(host_threads(nslots, 16384), by_essid.size());
+    // phase 3, per job: the job's keys ($HEX[] decoded) into its byte range of the pinned key bytes, slot records
+    SlotTable& T = d.slots;
+    RCHK(T.reserve(nslots, nbytes));
+    const size_t TS = host_threads(nslots, 8192);
     parallel_for(TS, [&](size_t t) {
-        const size_t g0 = std::lower_bound(gbase.begin(), gbase.end() - 1, nslots * t / TS) - gbase.begin();
-        const size_t g1 = std::lower_bound(gbase.begin(), gbase.end() - 1, nslots * (t + 1) / TS) - gbase.begin();
-        for (size_t g = g0; g < (t + 1 == TS ? by_essid.size() : g1); g++) {
-            size_t i = gbase[g];
-            for (uint32_t j : by_essid[g])
-                for (uint32_t o = 0; o < keys[j].size(); o++)
-                    slots[i++] = {keys[j][o], j, o, &parsed[j].essid, key_hash[j][o], !(o == 0 && job_pmk[j])};
+        std::string dec;
+        const size_t q0 = std::upper_bound(cs.order.begin(), cs.order.end(), nslots * t / TS,
+                                           [&](size_t v, uint32_t j) { return v < cs.jslot[j]; }) - cs.order.begin();
+        const size_t q1 = std::upper_bound(cs.order.begin(), cs.order.end(), nslots * (t + 1) / TS,
+                                           [&](size_t v, uint32_t j) { return v < cs.jslot[j]; }) - cs.order.begin();
+        // a job belongs to the thread whose slot range holds its first slot
+        for (size_t q = t ? q0 : 0; q < (t + 1 == TS ? cs.order.size() : q1); q++) {
+            const uint32_t j = cs.order[q];
+            const dwpa_job& J = jobs[j];
+            size_t si = cs.jslot[j];
+            uint64_t pos = cs.jbyte[j];
+            uint32_t o = 0;
+            for (size_t k = 0; k < J.nkeys; k++) {
+                // caller keys are scattered (one PHP string / Python bytes object each): prefetch ahead
+                if (k + 16 < J.nkeys && J.keys[k + 16].ptr) __builtin_prefetch(J.keys[k + 16].ptr);
+                const dwpa_bytes& kb = J.keys[k];
+                if (!kb.ptr) continue;
+                const uint8_t* src = kb.ptr;
+                size_t len = kb.len;
+                if (starts_hex(kb.ptr, kb.len)) {
+                    dec = hc_unhex(std::string((const char*)kb.ptr, kb.len));
+                    src = (const uint8_t*)dec.data();
+                    len = dec.size();  // <= kb.len
+                }
+                T.hash[si] = hash_key(src, len);
+                memcpy(T.kbytes + pos, src, len);
+                T.koff[si] = pos;
+                T.klen[si] = (uint32_t)len;
+                T.job[si] = j;
+                T.ord[si] = o | (o == 0 && cs.job_pmk[j] ? SLOT_CALLER : 0u);
+                pos += len;
+                si++;
+                o++;
+            }
         }
     });
     tr.mark("slots");
 
     // The first chunk's PBKDF2 is queued before the line tables exist: the host builds them while the GPU derives.
     TableBuilder tb;
+    std::vector<uint32_t> job_line(njobs, 0);
     std::vector<HitDev> hits;
     const size_t chunk = default_batch();
-    std::vector<size_t> gbytes(by_essid.size(), 0);
-    for (size_t g = 0; g < by_essid.size(); g++)
-        for (uint32_t j : by_essid[g]) gbytes[g] += job_bytes[j];
     for (size_t b = 0; b < nslots; b += chunk) {
         const size_t e = std::min(nslots, b + chunk);
         // the ESSID runs of [b, e) are the groups' slot ranges clipped to it
         std::vector<uint32_t> runs{0};
-        size_t keybytes = 0;
-        for (size_t g = 0; g < by_essid.size(); g++) {
-            if (gbase[g + 1] <= b || gbase[g] >= e) continue;
-            if (gbase[g] > b) runs.push_back((uint32_t)(gbase[g] - b));
-            keybytes += gbase[g] >= b && gbase[g + 1] <= e ? gbytes[g] : 0;
-            if (gbase[g] < b || gbase[g + 1] > e)  // a group cut by the chunk: count its bytes inside
-                for (size_t i = std::max(b, gbase[g]); i < std::min(e, gbase[g + 1]); i++) keybytes += slots[i].key.size();
+        std::vector<const std::string*> run_essid;
+        for (size_t g = 0; g < G; g++) {
+            if (cs.gslot[g + 1] <= b || cs.gslot[g] >= e) continue;
+            if (cs.gslot[g] > b) runs.push_back((uint32_t)(cs.gslot[g] - b));
+            run_essid.push_back(&cs.parsed[cs.order[cs.gstart[g]]].essid);
         }
         runs.push_back((uint32_t)(e - b));
         DeriveStage st;
-        RCHK(derive_slots(d, slots, b, e, job_pmk, runs, keybytes, st));
+        RCHK(derive_slots(d, T, b, e, cs.job_pmk, runs, run_essid, b == 0, st));
         if (b == 0) {
-            for (const auto& js : by_essid)
-                for (uint32_t j : js) job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
+            for (uint32_t j : cs.order) job_line[j] = tb.add_line(cs.parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
             tr.mark("tables (overlapped)");
         }
         // the tail slots' verify first: its segment upload goes up the side stream ahead of the head's keyver-3
         // verify, which that stream then runs (fan-out)
-        RCHK(queue_verify(d, slots, b, b + st.split, e, job_line, tb, b == 0, d.tail, d.segs_tail, d.keys_tail,
-                          false));
-        RCHK(queue_verify(d, slots, b, b, b + st.split, job_line, tb, false, d.stream, d.segs, d.keys, true));
+        RCHK(queue_verify(d, T, b, b + st.split, e, job_line, tb, b == 0, d.tail, d.segs_tail, d.keys_tail, false));
+        RCHK(queue_verify(d, T, b, b, b + st.split, job_line, tb, false, d.stream, d.segs, d.keys, true));
         tr.mark("  verify queued");
         RCHK(collect_hits(d, hits));
     }
     tr.mark("device");
 
     // first key in input order wins, then the first attempt in PHP order (common.php:186,280-289)
-    std::map<uint32_t, size_t> line_job;
-    for (const auto& js : by_essid)
-        for (uint32_t j : js) line_job[job_line[j]] = j;
+    std::unordered_map<uint32_t, uint32_t> line_job;
+    for (uint32_t j : cs.order) line_job[job_line[j]] = j;
     std::vector<int64_t> best(njobs, -1);
     std::vector<uint32_t> best_att(njobs, 0);
     std::vector<const HitDev*> best_hit(njobs, nullptr);
@@ -926,7 +1002,12 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         if (best[j] < 0) continue;
         const LineDev& L = tb.lines[job_line[j]];
         rcs[j] = DWPA_HIT;
-        out[j].key_index = (int32_t)key_index[j][(size_t)best[j]];
+        // the winning ordinal counts non-null keys: back to the caller's index
+        int64_t left = best[j];
+        size_t k = 0;
+        for (; k < jobs[j].nkeys; k++)
+            if (jobs[j].keys[k].ptr && left-- == 0) break;
+        out[j].key_index = (int32_t)k;
         pmk_bytes(best_hit[j]->pmk, out[j].pmk);
         if (L.kind == LINE_PMKID) {
             out[j].nc_valid = 0;
@@ -949,21 +1030,29 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
     Device& d = *dp;
     HIPCHK(hipSetDevice(d.id));
     RCHK(device_stream(d));
-    std::string es((const char*)essid, essid_len);
-    std::vector<Slot> slots(nkeys);
-    for (size_t i = 0; i < nkeys; i++) {
-        const std::string_view k = keys[i].ptr ? std::string_view((const char*)keys[i].ptr, keys[i].len)
-                                               : std::string_view();
-        slots[i] = {k, 0, (uint32_t)i, &es, hash_bytes(k.data(), k.size(), 0), true};
+    if (nkeys >= SLOT_CALLER) return DWPA_E_ARG;
+    const std::string es((const char*)essid, essid_len);
+    SlotTable& T = d.slots;
+    size_t nbytes = 0;
+    for (size_t i = 0; i < nkeys; i++) nbytes += keys[i].ptr ? keys[i].len : 0;
+    RCHK(T.reserve(nkeys, nbytes));
+    uint64_t pos = 0;
+    for (size_t i = 0; i < nkeys; i++) {  // a null key derives as the empty key
+        const size_t len = keys[i].ptr ? keys[i].len : 0;
+        T.hash[i] = hash_key(keys[i].ptr, len);
+        if (len) memcpy(T.kbytes + pos, keys[i].ptr, len);
+        T.koff[i] = pos;
+        T.klen[i] = (uint32_t)len;
+        T.job[i] = 0;
+        T.ord[i] = (uint32_t)i;
+        pos += len;
     }
     const size_t chunk = default_batch();
     std::vector<const uint8_t*> jp(1, nullptr);
     for (size_t b = 0; b < nkeys; b += chunk) {
         const size_t e = std::min(nkeys, b + chunk);
-        size_t keybytes = 0;
-        for (size_t i = b; i < e; i++) keybytes += slots[i].key.size();
         DeriveStage st;
-        RCHK(derive_slots(d, slots, b, e, jp, {0u, (uint32_t)(e - b)}, keybytes, st));
+        RCHK(derive_slots(d, T, b, e, jp, {0u, (uint32_t)(e - b)}, {&es}, b == 0, st));
         RCHK(join_tail(d));
         std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
         HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, d.stream));

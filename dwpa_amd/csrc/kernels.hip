@@ -2,6 +2,7 @@
 //
 //   k_prep_dict     dictionary words in HBM (offsets+bytes)  -> HMAC-SHA1 key midstates (ipad/opad), compacted
 //   k_prep_numeric  in-kernel decimal keyspace (C4)          -> midstates
+//   k_prep_keys     check path: unique keys (slot indices into the call's key bytes) -> midstates
 //   k_pbkdf2        midstates x ESSID salt                    -> PMK (32 B)      [~99 % of all work]
 //   k_verify        PMK x hashline(s) of that ESSID           -> hit records     [PMKID / EAPOL keyver 1,2,3 + NC]
 //
@@ -48,6 +49,19 @@ __global__ __launch_bounds__(256) void k_prep_dict(const uint64_t* __restrict__ 
     key_block_from_bytes(bytes + b0, len, kb);
     store_mid(mid, cap, slot, kb);
     if (ids) ids[slot] = first + i;
+}
+
+// Check path: unique key u -> its midstates at row u.  The key is slot uslot[u]'s bytes; koff/klen index the
+// call's key bytes in slot order, so the host never copies the unique keys into a contiguous list.
+__global__ __launch_bounds__(256) void k_prep_keys(const uint64_t* __restrict__ koff, const uint32_t* __restrict__ klen,
+                                                   const uint8_t* __restrict__ kbytes, const uint32_t* __restrict__ uslot,
+                                                   uint32_t count, uint32_t* __restrict__ mid, uint32_t cap) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= count || u >= cap) return;
+    const uint32_t s = uslot[u];
+    uint32_t kb[16];
+    key_block_from_bytes(kbytes + koff[s], klen[s], kb);
+    store_mid(mid, cap, u, kb);
 }
 
 // Decimal keyspace: candidate v -> its `digits`-wide zero-padded decimal string (C4: 00000000..99999999).
@@ -591,6 +605,13 @@ hipError_t launch_prep_dict(const uint64_t* off, const uint8_t* bytes, uint64_t 
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(k_prep_dict, dim3(cdiv(count, 256)), dim3(256), 0, s, off, bytes, first, count, minlen, maxlen,
                        mid, ids, counter, cap, compact ? 1u : 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_keys(const uint64_t* koff, const uint32_t* klen, const uint8_t* kbytes, const uint32_t* uslot,
+                            uint32_t count, uint32_t* mid, uint32_t cap, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prep_keys, dim3(cdiv(count, 256)), dim3(256), 0, s, koff, klen, kbytes, uslot, count, mid, cap);
     return hipGetLastError();
 }
 

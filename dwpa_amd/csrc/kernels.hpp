@@ -10,6 +10,9 @@ namespace dwpa {
 hipError_t launch_prep_dict(const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t count, uint32_t minlen,
                             uint32_t maxlen, uint32_t* mid, uint64_t* ids, uint32_t* counter, uint32_t cap,
                             bool compact, hipStream_t s);
+// check path: unique key u = slot uslot[u] of the call's key bytes (koff/klen per slot) -> mid row u
+hipError_t launch_prep_keys(const uint64_t* koff, const uint32_t* klen, const uint8_t* kbytes, const uint32_t* uslot,
+                            uint32_t count, uint32_t* mid, uint32_t cap, hipStream_t s);
 hipError_t launch_prep_numeric(uint64_t first, uint32_t count, uint32_t digits, uint32_t* mid, uint64_t* ids,
                                uint32_t cap, hipStream_t s);
 // product launch: issue-pass code object (pbkdf2_module.cpp); DWPA_PBKDF2_PLAIN=1 -> launch_pbkdf2_plain

@@ -29,9 +29,34 @@ static bool valid_hex(const char* s, size_t n) {
         if (!is_xd((uint8_t)s[i])) return false;
     return true;
 }
-static std::string hex2bin(const char* s, size_t n) {
-    std::string o(n / 2, '\0');
+static void hex2bin_into(const char* s, size_t n, std::string& o) {
+    o.resize(n / 2);
     for (size_t i = 0; i < n / 2; i++) o[i] = (char)(hv((uint8_t)s[2 * i]) << 4 | hv((uint8_t)s[2 * i + 1]));
+}
+// valid_hex(s) then hex2bin(s) in one pass over a nibble table (16 = not a hex digit); false leaves o undefined
+struct NibbleTable {
+    uint8_t v[256];
+    constexpr NibbleTable() : v() {
+        for (int c = 0; c < 256; c++)
+            v[c] = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10
+                 : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : 16;
+    }
+};
+static constexpr NibbleTable kNib;
+static bool valid_hex_into(const char* s, size_t n, std::string& o) {
+    if (n == 0 || (n & 1)) return false;
+    o.resize(n / 2);
+    uint32_t bad = 0;
+    for (size_t i = 0; i < n / 2; i++) {
+        const uint32_t hi = kNib.v[(uint8_t)s[2 * i]], lo = kNib.v[(uint8_t)s[2 * i + 1]];
+        bad |= hi | lo;
+        o[i] = (char)(hi << 4 | lo);
+    }
+    return bad < 16;
+}
+static std::string hex2bin(const char* s, size_t n) {
+    std::string o;
+    hex2bin_into(s, n, o);
     return o;
 }
 
@@ -91,37 +116,44 @@ static bool php_eq_type(const char* s, size_t n, int target) {
 // ---------------------------------------------------------------------------------------------------------
 ParsedLine parse_m22000(const char* s, size_t n) {
     ParsedLine p;
+    parse_m22000_into(s, n, p);
+    return p;
+}
+
+// The same into an existing ParsedLine: its strings keep their capacity (the check path re-parses a batch into
+// the same objects on every call instead of allocating ~9 strings per line).
+void parse_m22000_into(const char* s, size_t n, ParsedLine& p) {
+    p.status = 0;
+    p.kind = 0;
+    p.keyver = 0;
+    for (std::string* f : {&p.mac_ap, &p.mac_sta, &p.essid, &p.pmkid, &p.keymic, &p.nonce_ap, &p.eapol, &p.mp,
+                           &p.field2_hex})
+        f->clear();
     const char* f[9];
     size_t fl[9];
     size_t cnt = 0, st = 0;
     for (size_t i = 0; i < n && cnt < 8; i++)
         if (s[i] == '*') { f[cnt] = s + st; fl[cnt] = i - st; cnt++; st = i + 1; }
     f[cnt] = s + st; fl[cnt] = n - st; cnt++;            // explode('*', $hashline, 9)
-    if (cnt != 9 || fl[0] != 3 || memcmp(f[0], "WPA", 3) != 0) { p.status = DWPA_E_FORMAT; return p; }
-    if (!valid_hex(f[3], fl[3]) || !valid_hex(f[4], fl[4]) || !valid_hex(f[5], fl[5])) { p.status = DWPA_E_HEX; return p; }
-    p.mac_ap = hex2bin(f[3], fl[3]);
-    p.mac_sta = hex2bin(f[4], fl[4]);
-    p.essid = hex2bin(f[5], fl[5]);
+    if (cnt != 9 || fl[0] != 3 || memcmp(f[0], "WPA", 3) != 0) { p.status = DWPA_E_FORMAT; return; }
+    // the checks run in common.php's order (:159-164 before the type, :169/:192-195 after it), so the first failing
+    // one sets the status
+    if (!valid_hex_into(f[3], fl[3], p.mac_ap) || !valid_hex_into(f[4], fl[4], p.mac_sta) ||
+        !valid_hex_into(f[5], fl[5], p.essid)) { p.status = DWPA_E_HEX; return; }
     p.field2_hex.assign(f[2], fl[2]);
     if (php_eq_type(f[1], fl[1], 1)) {
         p.kind = LINE_PMKID;
-        if (!valid_hex(f[2], fl[2])) { p.status = DWPA_E_HEX; return p; }
-        p.pmkid = hex2bin(f[2], fl[2]);
+        if (!valid_hex_into(f[2], fl[2], p.pmkid)) { p.status = DWPA_E_HEX; return; }
     } else if (php_eq_type(f[1], fl[1], 2)) {
         p.kind = LINE_EAPOL;
-        for (int k : {2, 6, 7, 8})
-            if (!valid_hex(f[k], fl[k])) { p.status = DWPA_E_HEX; return p; }
-        p.keymic = hex2bin(f[2], fl[2]);
-        p.nonce_ap = hex2bin(f[6], fl[6]);
-        p.eapol = hex2bin(f[7], fl[7]);
-        p.mp = hex2bin(f[8], fl[8]);
+        if (!valid_hex_into(f[2], fl[2], p.keymic) || !valid_hex_into(f[6], fl[6], p.nonce_ap) ||
+            !valid_hex_into(f[7], fl[7], p.eapol) || !valid_hex_into(f[8], fl[8], p.mp)) { p.status = DWPA_E_HEX; return; }
         // unpack('x5/nkey_information/x10/a32nonce_sta', $eapol) needs 49 bytes, else null -> keyver 0
         if (p.eapol.size() >= 49) p.keyver = (((uint8_t)p.eapol[5] << 8) | (uint8_t)p.eapol[6]) & 3;
         if (p.keyver == 0) p.status = DWPA_E_KEYVER;  // common.php:274-276: unknown keyver -> False
     } else {
         p.status = DWPA_E_TYPE;
     }
-    return p;
 }
 
 // ---------------------------------------------------------------------------------------------------------

@@ -19,6 +19,7 @@ struct ParsedLine {
 };
 
 ParsedLine parse_m22000(const char* s, size_t n);
+void parse_m22000_into(const char* s, size_t n, ParsedLine& p);  // reuses p's string capacity
 // False when the line's PMKID / MIC is shorter than 16 bytes: strncmp over 16 bytes never matches
 // (common.php:186,280); TableBuilder marks such lines `never`.
 inline bool line_can_match(const ParsedLine& p) {
