@@ -57,7 +57,8 @@ clean:
 
 .PHONY: all oracle clean asm
 
-tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench
+tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
+       tools/bin/inflate_check
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -77,6 +78,11 @@ tools/bin/valu_peak64: tools/valu_peak64.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
-tools/bin/inflate_bench: tools/inflate_bench.cpp $(SRC)/dict_reader.hpp $(SRC)/m22000_host.cpp $(SRC)/m22000_host.hpp
+tools/bin/inflate_bench: tools/inflate_bench.cpp $(SRC)/dict_reader.hpp $(SRC)/inflate.hpp $(SRC)/m22000_host.cpp \
+                         $(SRC)/m22000_host.hpp
 	@mkdir -p tools/bin
 	g++ -O3 -std=c++17 -Iinclude -I$(SRC) -o $@ tools/inflate_bench.cpp $(SRC)/m22000_host.cpp -lz -lpthread
+
+tools/bin/inflate_check: tools/inflate_check.cpp $(SRC)/inflate.hpp
+	@mkdir -p tools/bin
+	g++ -O3 -std=c++17 -Wall -I$(SRC) -o $@ tools/inflate_check.cpp -lz

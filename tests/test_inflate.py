@@ -1,0 +1,144 @@
+"""CPU: the dictionary reader's gzip decoder (dwpa_amd/csrc/inflate.hpp, GzipDecoder) against zlib.
+
+help_crack hands the cracker gzip wordlists (help_crack.py:520-552).  dwpa_crack_files inflates them with its own
+DEFLATE decoder (about twice zlib 1.2.11's rate on a host core, so one gz stream feeds more GPUs), which must yield
+exactly the bytes zlib's gzread yields and reject what zlib rejects.  tools/bin/inflate_check decodes each file with
+both, in blocks of a given size (so back-references cross block boundaries), and compares.
+"""
+import gzip
+import os
+import random
+import struct
+import subprocess
+import zlib
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "tools", "bin", "inflate_check")
+
+
+@pytest.fixture(scope="module")
+def tool():
+    subprocess.run(["make", "-s", "-C", ROOT, "tools/bin/inflate_check"], check=True)
+    return TOOL
+
+
+def _words(rng, n):
+    out = []
+    for i in range(n):
+        if i % 7 == 0:
+            out.append(bytes(rng.choice(b"abcdefghijklmnopqrstuvwxyz0123456789!@#") for _ in range(rng.randint(8, 63))))
+        else:
+            out.append(b"pass%08d" % rng.randrange(10 ** 8))
+    return b"\n".join(out) + b"\n"
+
+
+def _raw_deflate(data, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, memlevel=8):
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, memlevel, strategy)
+    return c.compress(data) + c.flush()
+
+
+def _member(data, flags=0, extra=b"", name=b"", comment=b"", hcrc=True, **kw):
+    h = b"\x1f\x8b\x08" + bytes([flags]) + b"\0\0\0\0\0\xff"
+    if flags & 4:
+        h += struct.pack("<H", len(extra)) + extra
+    if flags & 8:
+        h += name + b"\0"
+    if flags & 16:
+        h += comment + b"\0"
+    if flags & 2:
+        h += struct.pack("<H", (zlib.crc32(h) & 0xFFFF) ^ (0 if hcrc else 1))
+    return h + _raw_deflate(data, **kw) + struct.pack("<II", zlib.crc32(data), len(data) & 0xFFFFFFFF)
+
+
+def _far_match():
+    """A fixed-Huffman block whose first symbol is a match (length 3, distance 1) before any output."""
+    bits = []
+
+    def put(v, n):  # header fields and extra bits: LSB first
+        bits.extend((v >> i) & 1 for i in range(n))
+
+    def code(c, n):  # Huffman codes: MSB first
+        bits.extend((c >> i) & 1 for i in range(n - 1, -1, -1))
+    put(1, 1)
+    put(1, 2)
+    code(1, 7)  # symbol 257 (length 3)
+    code(0, 5)  # distance code 0 (distance 1)
+    code(0, 7)  # end of block
+    bits += [0] * (-len(bits) % 8)
+    return bytes(sum(b << i for i, b in enumerate(bits[k:k + 8])) for k in range(0, len(bits), 8))
+
+
+def _run(tool, paths, block=None):
+    args = [tool] + (["-b", str(block)] if block else []) + [str(p) for p in paths]
+    r = subprocess.run(args, capture_output=True, text=True)
+    lines = dict(l.split(" ", 1) for l in r.stdout.splitlines()[1:])
+    return r.returncode, lines
+
+
+def test_decoder_matches_zlib(tool, tmp_path):
+    rng = random.Random(3)
+    txt = _words(rng, 300_000)
+    cases = {
+        "l1.gz": gzip.compress(txt, compresslevel=1),
+        "l6.gz": gzip.compress(txt, compresslevel=6),
+        "l9.gz": gzip.compress(txt, compresslevel=9),
+        "fixed.gz": _member(txt[:400_000], strategy=zlib.Z_FIXED),
+        "huffonly.gz": _member(txt[:400_000], strategy=zlib.Z_HUFFMAN_ONLY),
+        "rle.gz": _member(b"a" * 300_000 + b"ab" * 100_000 + b"abc" * 50_000 + bytes(range(256)) * 300,
+                          strategy=zlib.Z_RLE),
+        "stored.gz": _member(txt[:300_000], level=0),
+        "random.gz": gzip.compress(rng.randbytes(2_000_000)),
+        "multi.gz": gzip.compress(txt[:70_000]) + gzip.compress(b"") + gzip.compress(txt[70_000:250_000]),
+        "empty.gz": gzip.compress(b""),
+        "header.gz": _member(txt[:60_000], flags=2 | 4 | 8 | 16, extra=b"xyz12", name=b"words.txt",
+                             comment=b"a comment"),
+        "garbage.gz": gzip.compress(txt[:9_000]) + b"trailing bytes that are not gzip",
+        "memlevel1.gz": _member(txt[:200_000], memlevel=1),
+        "long_distance.gz": gzip.compress(rng.randbytes(40_000) + txt[:10_000] + rng.randbytes(20_000) +
+                                          rng.randbytes(40_000)[:1] + txt[:10_000]),
+    }
+    paths = []
+    for name, blob in cases.items():
+        p = tmp_path / name
+        p.write_bytes(blob)
+        paths.append(p)
+    for block in (None, 4096, 65536 + 17):  # 4 MiB blocks, and blocks far smaller than the 32 KiB window
+        rc, lines = _run(tool, paths, block)
+        for p in paths:
+            assert lines[str(p)].startswith("ok "), (block, p.name, lines[str(p)])
+        assert rc == 0
+
+
+def test_decoder_rejects_what_zlib_rejects(tool, tmp_path):
+    rng = random.Random(4)
+    txt = _words(rng, 40_000)
+    good = gzip.compress(txt)
+    bad_crc = bytearray(good)
+    bad_crc[-6] ^= 1
+    bad_size = bytearray(good)
+    bad_size[-2] ^= 1
+    body = bytearray(good)
+    body[len(body) // 2] ^= 0x55
+    cases = {
+        "crc.gz": bytes(bad_crc),
+        "isize.gz": bytes(bad_size),
+        "truncated.gz": good[: len(good) // 2],
+        "no_trailer.gz": good[:-8],
+        "hcrc.gz": _member(txt, flags=2 | 8, name=b"n", hcrc=False),
+        "corrupt.gz": bytes(body),
+        "blocktype3.gz": b"\x1f\x8b\x08\0\0\0\0\0\0\xff" + bytes([0b111]) + b"\0" * 16,
+        "stored_nlen.gz": b"\x1f\x8b\x08\0\0\0\0\0\0\xff" + b"\x01\x05\x00\x00\x00" + b"hello" + b"\0" * 8,
+        "distance.gz": b"\x1f\x8b\x08\0\0\0\0\0\0\xff" + _far_match() + b"\0" * 8,
+    }
+    paths = []
+    for name, blob in cases.items():
+        p = tmp_path / name
+        p.write_bytes(blob)
+        paths.append(p)
+    rc, lines = _run(tool, paths)
+    for p in paths:
+        res = lines[str(p)]
+        assert res.startswith("error ") and not res.startswith("error none"), (p.name, res)
+    assert rc == 0  # both decoders failed on every file

@@ -7,10 +7,13 @@
 //   inflate_bench --passes K FILE... runs crack_files' ChunkSource K times over the files in one process (the second
 //     pass onwards replays the DictCache) and prints "#pass i cache_hits h" then that pass's words, hex-encoded
 //
-// Prints one JSON line: raw gzread throughput of the first file (inflate only), DictReader words/s on the first
-// file (one stream: an inflate thread feeding the line cutting + $HEX[] decoding thread), and ChunkSource words/s
-// over all files (up to 4 such streams, as crack_files runs them).
+// Prints one JSON line: inflate-only throughput of the first file with zlib's gzread and with the reader's
+// GzipDecoder (inflate.hpp), DictReader words/s on the first file (one stream: an inflate thread feeding the line
+// cutting + $HEX[] decoding thread; DWPA_INFLATE=zlib runs it on gzread), and ChunkSource words/s over all files
+// (up to 4 such streams, as crack_files runs them).
+#include <fcntl.h>
 #include <stdio.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <chrono>
@@ -87,6 +90,20 @@ int main(int argc, char** argv) {
     for (int r; (r = gzread(gz, buf.data(), (unsigned)buf.size())) > 0;) raw += (size_t)r;
     const double t_inflate = since(t);
     gzclose(gz);
+    // 1b. inflate only, GzipDecoder
+    size_t raw_fast = 0;
+    double t_fast = 0;
+    {
+        const int fd = open(paths[0].c_str(), O_RDONLY);
+        if (fd < 0) return 1;
+        dwpa::GzipDecoder dec(fd);
+        std::vector<uint8_t> ob(dwpa::GzipDecoder::WIN + (4u << 20) + dwpa::GzipDecoder::SLACK);
+        t = clk::now();
+        while (!dec.done() && !dec.failed()) raw_fast += dec.read(ob.data(), 4u << 20);
+        t_fast = since(t);
+        close(fd);
+        if (dec.failed() || raw_fast != raw) raw_fast = 0;  // not gzip (plain file) or an error: no figure
+    }
     // 2. one DictReader stream (what one dictionary costs one reader thread)
     size_t words1 = 0;
     {
@@ -109,10 +126,12 @@ int main(int argc, char** argv) {
         if (err) return 1;
     }
     const double t_all = since(t);
-    printf("{\"files\": %zu, \"raw_bytes\": %zu, \"inflate_MBps\": %.1f, \"words\": %zu, "
+    printf("{\"files\": %zu, \"raw_bytes\": %zu, \"inflate_MBps\": %.1f, \"fast_inflate_MBps\": %.1f, "
+           "\"reader_inflater\": \"%s\", \"words\": %zu, "
            "\"reader_words_per_s\": %.0f, \"reader_MBps\": %.1f, \"chunk_source_threads\": %zu, "
            "\"chunk_source_words_per_s\": %.0f}\n",
-           paths.size(), raw, raw / t_inflate / 1e6, words1, words1 / t_reader, raw / t_reader / 1e6,
+           paths.size(), raw, raw / t_inflate / 1e6, raw_fast ? raw_fast / t_fast / 1e6 : 0.0,
+           getenv("DWPA_INFLATE") && !strcmp(getenv("DWPA_INFLATE"), "zlib") ? "zlib" : "GzipDecoder", words1, words1 / t_reader, raw / t_reader / 1e6,
            std::min<size_t>(paths.size(), 4), words_all / t_all);
     return 0;
 }
