@@ -282,10 +282,12 @@ static int env_int(const char* name, int dflt, int lo, int hi) {
 }
 // Check-path scheduling knobs (A/B switches; the defaults are the measured best):
 //   DWPA_CHECK_PRIO    wave priority of the post-derive kernels (0)
+//   DWPA_KV3_PRIO      wave priority of the keyver-3 verify kernels (0)
 //   DWPA_TAIL_PRIO     priority the PBKDF2 tail raises itself to once the head has ended (2; 0 = stays at 0)
 //   DWPA_HEAD_FENCE    concurrent calls on one device launch their heads one after another (1)
 //   DWPA_VERIFY_FANOUT the head slots' keyver-3 verify runs on its own stream beside the other classes (1)
 static int check_prio_knob() { static const int v = env_int("DWPA_CHECK_PRIO", 0, 0, 3); return v; }
+static int kv3_prio_knob() { static const int v = env_int("DWPA_KV3_PRIO", 0, 0, 3); return v; }
 static int tail_prio_knob() { static const int v = env_int("DWPA_TAIL_PRIO", 2, 0, 3); return v; }
 static bool head_fence_knob() { static const bool v = env_int("DWPA_HEAD_FENCE", 1, 0, 1) != 0; return v; }
 static bool verify_fanout_knob() { static const bool v = env_int("DWPA_VERIFY_FANOUT", 1, 0, 1) != 0; return v; }
@@ -294,6 +296,7 @@ static int device_stream(Device& d) {
     if (!d.stream) {
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(set_check_prio((uint32_t)check_prio_knob()));
+        HIPCHK(set_kv3_prio((uint32_t)kv3_prio_knob()));
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&d.side_done, hipEventDisableTiming));

@@ -132,9 +132,13 @@ __global__ void k_set_flag(uint32_t* __restrict__ flag) {
     if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave priority of the check path's post-derive kernels (DWPA_CHECK_PRIO, set per device by set_check_prio).
+// Wave priority of the check path's post-derive kernels (DWPA_CHECK_PRIO, set per device by set_check_prio); the
+// keyver-3 class (latency-bound AES-CMAC, the longest verify) has its own (DWPA_KV3_PRIO, set_kv3_prio).
 __device__ uint32_t g_check_prio = 0;
+__device__ uint32_t g_kv3_prio = 0;
 __device__ __forceinline__ void check_prio() { set_wave_prio(g_check_prio); }
+template <uint32_t VC>
+__device__ __forceinline__ void check_prio_vc() { set_wave_prio(VC == VC_KV3 ? g_kv3_prio : g_check_prio); }
 
 // Slot PMKs from the derived unique (ESSID, key) PMKs or from caller-supplied PMKs:
 // src[i] = u -> upmk[.][u];  src[i] = GATHER_CALLER | c -> cpmk[c][0..7] (check_key_m22000's $pmk, common.php:178).
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                 const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                 uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
-    check_prio();
+    check_prio_vc<VC>();
     __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -512,7 +516,7 @@ __global__ __launch_bounds__(256) void k_eapol_keys(const uint32_t* __restrict__
                                                     const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool, uint32_t* __restrict__ keys,
                                                     uint32_t kstride) {
-    check_prio();
+    check_prio_vc<VC>();
     const uint32_t segi = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t k = threadIdx.x & 63;
     if (segi >= nsegs) return;
@@ -550,7 +554,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                     const uint32_t* __restrict__ pool,
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                     uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
-    check_prio();
+    check_prio_vc<VC>();
     __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
     const uint32_t lane = threadIdx.x & 63;
@@ -668,6 +672,7 @@ hipError_t launch_set_flag(uint32_t* flag, hipStream_t s) {
 }
 
 hipError_t set_check_prio(uint32_t prio) { return hipMemcpyToSymbol(HIP_SYMBOL(g_check_prio), &prio, 4); }
+hipError_t set_kv3_prio(uint32_t prio) { return hipMemcpyToSymbol(HIP_SYMBOL(g_kv3_prio), &prio, 4); }
 
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s) {
     uint4 lo = make_uint4(w[0], w[1], w[2], w[3]), hi = make_uint4(w[4], w[5], w[6], w[7]);
