@@ -198,7 +198,8 @@ struct Device {
     MappedHost hits_host;         // check path: hit count + hits written by k_hits_out
     std::mutex mu;
     Batch batch;
-    DevBuf lines, atts, pool, segs, segs_tail, salt, koff, kbytes, idsup, klen, uslot;
+    DevBuf lines, atts, pool, segs, segs_tail, salt;
+    DevBuf koff, klen, kbytes, uslot;  // check path: the call's key bytes by slot, unique key -> its first slot
     DevBuf keys, keys_tail;        // check path: per-key EapolKey scratch of the attempt-parallel verify
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
     SlotTable slots;               // check path: the call's slots (capacity kept between calls)
@@ -1415,12 +1416,14 @@ void dwpa_shutdown(void) {
         std::lock_guard<std::mutex> dl(d->mu);
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
-        for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->keys, &d->keys_tail, &d->salt, &d->koff, &d->kbytes, &d->idsup,
-                          &d->upmk, &d->sref, &d->src, &d->cpmk,
+        for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->keys, &d->keys_tail, &d->salt,
+                          &d->koff, &d->klen, &d->kbytes, &d->uslot, &d->upmk, &d->sref, &d->src, &d->cpmk,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();
         d->batch.cap = d->batch.hitcap = 0;
         d->stage.release();
+        d->slots.mem.release();
+        d->slots.n = d->slots.nbytes = 0;
         d->hits_host.release();
         if (d->head_end) (void)hipEventDestroy(d->head_end);
         d->head_end = nullptr;
