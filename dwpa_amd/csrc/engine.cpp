@@ -287,11 +287,13 @@ static int env_int(const char* name, int dflt, int lo, int hi) {
 //   DWPA_TAIL_PRIO     priority the PBKDF2 tail raises itself to once the head has ended (2; 0 = stays at 0)
 //   DWPA_HEAD_FENCE    concurrent calls on one device launch their heads one after another (1)
 //   DWPA_VERIFY_FANOUT the head slots' keyver-3 verify runs on its own stream beside the other classes (1)
+//   DWPA_VERIFY_KV3_FIRST the keyver-3 launches are queued before the other classes (0)
 static int check_prio_knob() { static const int v = env_int("DWPA_CHECK_PRIO", 0, 0, 3); return v; }
 static int kv3_prio_knob() { static const int v = env_int("DWPA_KV3_PRIO", 0, 0, 3); return v; }
 static int tail_prio_knob() { static const int v = env_int("DWPA_TAIL_PRIO", 2, 0, 3); return v; }
 static bool head_fence_knob() { static const bool v = env_int("DWPA_HEAD_FENCE", 1, 0, 1) != 0; return v; }
 static bool verify_fanout_knob() { static const bool v = env_int("DWPA_VERIFY_FANOUT", 1, 0, 1) != 0; return v; }
+static bool verify_kv3_first_knob() { static const bool v = env_int("DWPA_VERIFY_KV3_FIRST", 0, 0, 1) != 0; return v; }
 
 static int device_stream(Device& d) {
     if (!d.stream) {
@@ -759,7 +761,8 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
         HIPCHK(hipStreamWaitEvent(d.side, d.vs_go, 0));
     }
     uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
-    for (int k = 0; k < 8; k++) {
+    static const int kOrder[2][8] = {{0, 1, 2, 3, 4, 5, 6, 7}, {3, 7, 0, 1, 2, 4, 5, 6}};
+    for (int k : kOrder[verify_kv3_first_knob() ? 1 : 0]) {
         const uint32_t nb = (uint32_t)(bstart[k + 1] - bstart[k]), vc = bucket_vc(k);
         const SegDev* sg = (const SegDev*)segbuf.p + bstart[k];
         if (!nb) continue;

@@ -135,6 +135,43 @@ def test_batch_fanout_dedup_and_mixed_salt_lengths():
     assert sum(1 for e in exp if e) >= len(jobs) // 2
 
 
+def test_batch_dedup_hex_forms_nulls_and_key_index():
+    """The check path's slot table (engine.cpp SlotTable): keys are deduplicated per ESSID on their decoded bytes, so
+    "$HEX[..]" (either hex case) and the plain form of one key share a PMK, while malformed $HEX[ forms stay literal
+    (hc_unhex, common.php:3-25); null keys are skipped but still count in the returned key index
+    (common.php:172,240), and a caller PMK applies to the first non-null key only (:178).  Every job against the
+    oracle."""
+    import random
+    rng = random.Random(91)
+    essid = b"dedup-net"
+    psk = b"Pa55:w\xc3\xb6rd!"
+    hexl, hexu = b"$HEX[" + psk.hex().encode() + b"]", b"$HEX[" + psk.hex().upper().encode() + b"]"
+    near = [b"$HEX[" + psk.hex().encode()[:-1] + b"]", b"$HEX[" + psk.hex().encode() + b"", b"$HEX[zz]", b"$HEX[]",
+            psk + b" ", b""]
+    pmk = S.pmk(psk, essid)
+    jobs = []
+    for k in range(40):
+        ap, sta = rng.randbytes(6), rng.randbytes(6)
+        if k % 2:
+            line = S.pmkid_line(psk, essid, ap, sta)
+        else:
+            line = S.eapol_line(psk, essid, ap, sta, rng.randbytes(32), rng.randbytes(32), 1 + k % 3,
+                                rng.randint(-3, 3), rng.choice(["LE", "BE"]), rng=rng)
+        keys = [None] * (k % 4) + rng.sample(near, 3) + [None]
+        form = (psk, hexl, hexu)[k % 3]
+        keys.insert(rng.randrange(len(keys) + 1), form)
+        if k % 5 == 0:
+            keys.append(psk)  # a second copy later in the same job
+        caller = pmk if k % 7 == 0 else (b"\x11" * 32 if k % 7 == 1 else False)
+        jobs.append((line, keys, caller, 8))
+    jobs.append((S.pmkid_line(psk, essid, b"\x01" * 6, b"\x02" * 6), [None, None], False, 8))  # only nulls
+    got = dwpa_amd.check_batch(jobs)
+    exp = [O.c_check_key_m22000(*j) for j in jobs]
+    bad = [i for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    assert not bad, [(i, got[i], exp[i]) for i in bad[:3]]
+    assert sum(1 for e in exp if e) >= 30
+
+
 def test_batch_chunked_across_essid_groups():
     """dwpa_init(batch=...) caps the slots per derive, so one call runs in several chunks whose boundaries cut
     through ESSID groups (the per-group dedup and key-byte counts are then clipped to the chunk); the results
