@@ -56,7 +56,7 @@ struct WorkItem {
 
 // Cuts the reader's chunks into work items that every shard worker pulls for itself: a device that finishes its
 // item early takes the next one, so no device waits for the slowest at a chunk boundary.  Items start at `first`
-// words (one batch of candidates, so every device starts after one batch's read) and double up to `most`.
+// words (a sixteenth of a batch of candidates, so every device starts after a short read) and double up to `most`.
 class ItemQueue {
   public:
     ItemQueue(ChunkSource& src, size_t first, size_t most) : src_(src), size_(std::max<size_t>(1, first)),
@@ -301,11 +301,13 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
 
     std::vector<std::string> dpaths;
     for (size_t i = 0; i < ndicts; i++) dpaths.push_back(dicts[i]);
-    // Items: the first is one batch of candidates, later ones up to 16 batches (a partial last batch per item
-    // then costs ~1 % of its wave rounds).  The reader's chunks start at one item per worker and grow to two
-    // full items per worker, so reading stays ahead of the scans without holding much more than that in memory.
+    // Items: the first is 1/16 of a batch of candidates (a device starts after ~1M words have been read, not a
+    // whole 16M-word batch: on a dictionary's first pass that read took ~0.5 s of a 21 s C2 pass), doubling to
+    // 16 batches (a partial last batch per item then costs ~1 % of its wave rounds).  The reader's chunks start at
+    // one item per worker and grow to two full items per worker, so reading stays ahead of the scans without
+    // holding much more than that in memory.
     const size_t nr = rp ? rp->size() : 1;
-    const size_t first_item = std::max<size_t>(1, batch / nr), most_item = std::max<size_t>(1, 16 * (size_t)batch / nr);
+    const size_t first_item = std::max<size_t>(1, batch / nr / 16), most_item = std::max<size_t>(1, 16 * (size_t)batch / nr);
     ChunkSource source(dpaths, first_item * G, 2 * most_item * G);
     ItemQueue items(source, first_item, most_item);
     const auto t0 = std::chrono::steady_clock::now();

@@ -117,6 +117,7 @@ struct SlotTable {
     std::vector<uint32_t> job;   // slot -> job
     std::vector<uint32_t> ord;   // key ordinal among the job's non-null keys (selects its attempt list) | SLOT_CALLER
     std::vector<uint64_t> hash;  // hash_key of the key, taken while its bytes are in cache
+    std::vector<uint32_t> kidx;  // the key's index in the caller's key list (null keys included)
     PinnedArena mem;             // koff[n], klen[n], key bytes
     uint64_t* koff = nullptr;
     uint32_t* klen = nullptr;
@@ -131,6 +132,7 @@ struct SlotTable {
         job.resize(slots);
         ord.resize(slots);
         hash.resize(slots);
+        kidx.resize(slots);
         n = slots;
         nbytes = bytes;
         return 0;
@@ -865,6 +867,10 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
             rcs[j] = DWPA_MISS;
             cs.job_pmk[j] = jobs[j].pmk;
             if (!line_can_match(pl)) continue;  // PMKID/MIC shorter than 16 bytes never verifies
+            if (jobs[j].nkeys > UINT32_MAX) {      // key indices are 32-bit (SlotTable::kidx)
+                rcs[j] = DWPA_E_ARG;
+                continue;
+            }
             uint32_t c = 0;
             uint64_t by = 0;
             for (size_t k = 0; k < jobs[j].nkeys; k++)
@@ -950,6 +956,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
                 T.klen[si] = (uint32_t)len;
                 T.job[si] = j;
                 T.ord[si] = o | (o == 0 && cs.job_pmk[j] ? SLOT_CALLER : 0u);
+                T.kidx[si] = (uint32_t)k;
                 pos += len;
                 si++;
                 o++;
@@ -1009,12 +1016,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         if (best[j] < 0) continue;
         const LineDev& L = tb.lines[job_line[j]];
         rcs[j] = DWPA_HIT;
-        // the winning ordinal counts non-null keys: back to the caller's index
-        int64_t left = best[j];
-        size_t k = 0;
-        for (; k < jobs[j].nkeys; k++)
-            if (jobs[j].keys[k].ptr && left-- == 0) break;
-        out[j].key_index = (int32_t)k;
+        out[j].key_index = (int32_t)T.kidx[cs.jslot[j] + (size_t)best[j]];  // ordinal -> the caller's index
         pmk_bytes(best_hit[j]->pmk, out[j].pmk);
         if (L.kind == LINE_PMKID) {
             out[j].nc_valid = 0;
@@ -1026,6 +1028,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
             out[j].endian = (int8_t)at.endian;
         }
     }
+    tr.mark("results");
     return 0;
 }
 
@@ -1052,6 +1055,7 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
         T.klen[i] = (uint32_t)len;
         T.job[i] = 0;
         T.ord[i] = (uint32_t)i;
+        T.kidx[i] = (uint32_t)i;
         pos += len;
     }
     const size_t chunk = default_batch();

@@ -495,19 +495,14 @@ class GzipDecoder {
             bc -= e & 15;
             if ((e & (K_MASK | K_BAD)) == K_LIT) {
                 *o++ = (uint8_t)(e >> 16);
-                // up to two more literals from the same refill: a primary-table literal is <= 11 bits and >= 41
-                // bits are left; the output may run 2 bytes past lim (SLACK)
-                e = lt[bb & ((1u << LBITS) - 1)];
-                if ((e & (K_MASK | K_BAD)) == K_LIT) {
+#pragma GCC unroll 5
+                for (int r = 0; r < 5; r++) {  // more literals from this refill while >= 11 bits remain (the
+                                               // output may run 5 bytes past lim: SLACK)
+                    e = lt[bb & ((1u << LBITS) - 1)];
+                    if ((e & (K_MASK | K_BAD)) != K_LIT || bc < 11) break;
                     bb >>= e & 15;
                     bc -= e & 15;
                     *o++ = (uint8_t)(e >> 16);
-                    e = lt[bb & ((1u << LBITS) - 1)];
-                    if ((e & (K_MASK | K_BAD)) == K_LIT) {
-                        bb >>= e & 15;
-                        bc -= e & 15;
-                        *o++ = (uint8_t)(e >> 16);
-                    }
                 }
                 continue;
             }
