@@ -477,6 +477,44 @@ __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te4, const ui
     s[3] = aes4_subword(te4, s3 >> 24, (s0 >> 16) & 0xff, (s1 >> 8) & 0xff, s2 & 0xff) ^ k3;
 }
 
+// The same with the round keys expanded once per key into LDS (rk[(r - 1) * stride] = round key r, one 16-byte slot
+// per lane: ds_read_b128 of lane-contiguous slots is bank-conflict free), so a CMAC over n blocks pays the 40
+// key-schedule lookups once instead of n times (build with -DDWPA_KV3_RK_LDS=1; A/B of the keyver-3 verify).
+__device__ __forceinline__ void aes128_expand_lds(const uint32_t* te4, const uint32_t key[4], uint4* rk,
+                                                  uint32_t stride) {
+    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
+#pragma unroll
+    for (int r = 1; r <= 10; r++) {
+        k0 ^= aes4_subword(te4, (k3 >> 16) & 0xff, (k3 >> 8) & 0xff, k3 & 0xff, k3 >> 24) ^ (RCON[r - 1] << 24);
+        k1 ^= k0;
+        k2 ^= k1;
+        k3 ^= k2;
+        rk[(r - 1) * stride] = make_uint4(k0, k1, k2, k3);
+    }
+}
+__device__ __forceinline__ void aes128_encrypt_rk(const uint32_t* te4, const uint32_t key[4], const uint4* rk,
+                                                  uint32_t stride, uint32_t s[4]) {
+    const uint32_t* T0 = te4;
+    const uint32_t* T1 = te4 + 256;
+    const uint32_t* T2 = te4 + 512;
+    const uint32_t* T3 = te4 + 768;
+    uint32_t s0 = s[0] ^ key[0], s1 = s[1] ^ key[1], s2 = s[2] ^ key[2], s3 = s[3] ^ key[3];
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        const uint4 k = rk[(r - 1) * stride];
+        const uint32_t t0 = xor3(xor3(T0[s0 >> 24], T1[(s1 >> 16) & 0xff], T2[(s2 >> 8) & 0xff]), T3[s3 & 0xff], k.x);
+        const uint32_t t1 = xor3(xor3(T0[s1 >> 24], T1[(s2 >> 16) & 0xff], T2[(s3 >> 8) & 0xff]), T3[s0 & 0xff], k.y);
+        const uint32_t t2 = xor3(xor3(T0[s2 >> 24], T1[(s3 >> 16) & 0xff], T2[(s0 >> 8) & 0xff]), T3[s1 & 0xff], k.z);
+        const uint32_t t3 = xor3(xor3(T0[s3 >> 24], T1[(s0 >> 16) & 0xff], T2[(s1 >> 8) & 0xff]), T3[s2 & 0xff], k.w);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint4 k = rk[9 * stride];
+    s[0] = aes4_subword(te4, s0 >> 24, (s1 >> 16) & 0xff, (s2 >> 8) & 0xff, s3 & 0xff) ^ k.x;
+    s[1] = aes4_subword(te4, s1 >> 24, (s2 >> 16) & 0xff, (s3 >> 8) & 0xff, s0 & 0xff) ^ k.y;
+    s[2] = aes4_subword(te4, s2 >> 24, (s3 >> 16) & 0xff, (s0 >> 8) & 0xff, s1 & 0xff) ^ k.z;
+    s[3] = aes4_subword(te4, s3 >> 24, (s0 >> 16) & 0xff, (s1 >> 8) & 0xff, s2 & 0xff) ^ k.w;
+}
 
 // CMAC subkey doubling on a 128-bit big-endian value held in 4 words
 __device__ __forceinline__ void cmac_dbl(const uint32_t in[4], uint32_t out[4]) {

@@ -286,9 +286,16 @@ __device__ __forceinline__ uint32_t att_nblk(const LineDev& L, const AttDev& at)
 // keyver 3: KDF-SHA256) -> KCK -> HMAC-MD5 (1), HMAC-SHA1 (2) or AES-128-CMAC (3) over the EAPOL frame.
 // KP (key-parallel): `at` is the same for every lane, so its PRF blocks come as KW blocks; otherwise (attempt-
 // parallel, lanes hold different attempts) they are patched per lane.  The EAPOL frame's blocks are KW blocks.
+// DWPA_KV3_RK_LDS=1 (with DWPA_KV3_WAVES=3): AES round keys expanded once per key into LDS instead of per CMAC
+// block.  Measured level (profiles/r02/kv3_rk_lds_ab): the compiler already hoists the loop-invariant key schedule
+// out of the CMAC loop into registers, so the LDS reads left are the state's T-table lookups (4.3 bank-conflict
+// cycles per ds_read); kept as a build switch for A/B.
+#ifndef DWPA_KV3_RK_LDS
+#define DWPA_KV3_RK_LDS 0
+#endif
 template <uint32_t VC, bool KP>
 __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __restrict__ pool, const EapolKey& K,
-                                          const AttDev& at, const uint32_t* te, uint32_t mic[4]) {
+                                          const AttDev& at, const uint32_t* te, uint32_t mic[4], uint4* rk = nullptr) {
     constexpr bool has1 = (VC & VC_KV1) != 0, has2 = (VC & VC_KV2) != 0, has3 = (VC & VC_KV3) != 0;
     if ((has1 || has2) && (!has3 || L.keyver != 3)) {
         uint32_t st[5], ptk[5];
@@ -337,7 +344,13 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         sha256_compress(ptk, m);
         // AES-128-CMAC(KCK = PTK[0..15], EAPOL)  (common.php:72-112)
         uint32_t Lb[4] = {0, 0, 0, 0}, K1[4], K2[4];
+#if DWPA_KV3_RK_LDS
+        aes128_expand_lds(te, ptk, rk, blockDim.x);
+        aes128_encrypt_rk(te, ptk, rk, blockDim.x, Lb);
+#else
+        (void)rk;
         aes128_encrypt_te4(te, ptk, Lb);
+#endif
         cmac_dbl(Lb, K1);
         cmac_dbl(K1, K2);
         uint32_t c[4] = {0, 0, 0, 0};
@@ -350,7 +363,11 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
                 if (last) v ^= L.cmac_complete ? K1[k] : K2[k];
                 c[k] ^= v;
             }
+#if DWPA_KV3_RK_LDS
+            aes128_encrypt_rk(te, ptk, rk, blockDim.x, c);
+#else
             aes128_encrypt_te4(te, ptk, c);
+#endif
         }
         mic[0] = c[0]; mic[1] = c[1]; mic[2] = c[2]; mic[3] = c[3];
     }
@@ -424,6 +441,12 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     check_prio_vc<VC>();
     __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
+#if DWPA_KV3_RK_LDS
+    __shared__ uint4 rk_lds[(VC & VC_KV3) ? 10 * vc_block(VC) : 1];
+    uint4* rk = rk_lds + threadIdx.x;
+#else
+    uint4* rk = nullptr;
+#endif
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t segi = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -482,7 +505,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
             const AttDev* al = atts + L.list_off + list * L.natt;
             for (uint32_t a = 0; a < L.natt; a++) {
                 uint32_t mic[4];
-                eapol_mic<VC, true>(L, pool, K, al[a], te, mic);
+                eapol_mic<VC, true>(L, pool, K, al[a], te, mic, rk);
                 if (mine && !found && mic_match(L, mic)) {
                     found = true;
                     found_att = a;
@@ -557,6 +580,12 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     check_prio_vc<VC>();
     __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
+#if DWPA_KV3_RK_LDS
+    __shared__ uint4 rk_lds[(VC & VC_KV3) ? 10 * vc_block(VC) : 1];
+    uint4* rk = rk_lds + threadIdx.x;
+#else
+    uint4* rk = nullptr;
+#endif
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (gw >= nwaves) return;
@@ -593,7 +622,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     }
     const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
     uint32_t mic[4];
-    eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic);
+    eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic, rk);
     const bool found = active && mic_match(L, mic);
     report_hits(found, lane, cand, sg.line, a, pmk + slot, cap, hits, hitcnt, hitcap);
 }
