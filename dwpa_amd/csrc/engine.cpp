@@ -931,7 +931,8 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
                                            [&](size_t v, uint32_t j) { return v < cs.jslot[j]; }) - cs.order.begin();
         const size_t q1 = std::upper_bound(cs.order.begin(), cs.order.end(), nslots * (t + 1) / TS,
                                            [&](size_t v, uint32_t j) { return v < cs.jslot[j]; }) - cs.order.begin();
-        // a job belongs to the thread whose slot range holds its first slot
+        // thread t takes the jobs whose first slot s has lo_t < s <= lo_{t+1} (lo_t = nslots * t / TS; thread 0
+        // also slot 0): contiguous runs of `order` with about nslots / TS slots each
         for (size_t q = t ? q0 : 0; q < (t + 1 == TS ? cs.order.size() : q1); q++) {
             const uint32_t j = cs.order[q];
             const dwpa_job& J = jobs[j];
