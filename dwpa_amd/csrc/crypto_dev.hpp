@@ -441,18 +441,26 @@ __constant__ static const AesTables AES_TABLES = make_aes_tables();
 // lookup), with the key schedule computed round by round (FIPS-197 5.2) instead of held as rk[44] (40 fewer live
 // registers; 40 more lookups per block).  S-box bytes come out of the T-tables already in place: S[x] is byte 3
 // of Te2/Te3, byte 2 of Te0/Te3, byte 1 of Te0/Te1 and byte 0 of Te1/Te2, so a SubWord is 4 lookups + 3 v_perm.
+//
+// Sliced tables (DWPA_KV3_SLICES = S, default 16): every table holds S interleaved copies, entry x of copy c at word
+// S x + c, and lane l reads copy l % S.  ds_read_b32 banks are (address / 4) mod 32 per 32-lane group, so with
+// S = 16 two lanes can only collide when they share a copy (l and l + 16) and their entries have the same parity:
+// 2-way conflicts at most.  The plain tables (S = 1) put 68 % of the keyver-3 verify's LDS cycles into random-index
+// bank conflicts; S = 16 halves the conflict cycles and takes the kernel alone from 2.02 to 1.56 ms per launch
+// (S = 8 barely helps: 4 lanes share a copy), 64 KiB per 512-thread workgroup (profiles/r02/kv3_slices_ab).
+#ifndef DWPA_KV3_SLICES
+#define DWPA_KV3_SLICES 16
+#endif
+constexpr uint32_t AES_SLICES = DWPA_KV3_SLICES;
+#define AES_T(t, x) te4[(t) * 256u * AES_SLICES + (x) * AES_SLICES]
 __device__ __forceinline__ uint32_t aes4_subword(const uint32_t* te4, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     // bytes (S[a], S[b], S[c], S[d]) from most to least significant; a..d are byte values (0..255)
-    const uint32_t hi = __builtin_amdgcn_perm(te4[512 + a], te4[768 + b], 0x07020100u);  // S[a]:b3, S[b]:b2
-    const uint32_t lo = __builtin_amdgcn_perm(te4[c], te4[256 + d], 0x07060500u);        // S[c]:b1, S[d]:b0
+    const uint32_t hi = __builtin_amdgcn_perm(AES_T(2, a), AES_T(3, b), 0x07020100u);  // S[a]:b3, S[b]:b2
+    const uint32_t lo = __builtin_amdgcn_perm(AES_T(0, c), AES_T(1, d), 0x07060500u);  // S[c]:b1, S[d]:b0
     return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
 }
 __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te4, const uint32_t key[4], uint32_t s[4]) {
     constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
-    const uint32_t* T0 = te4;
-    const uint32_t* T1 = te4 + 256;
-    const uint32_t* T2 = te4 + 512;
-    const uint32_t* T3 = te4 + 768;
     uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
     uint32_t s0 = s[0] ^ k0, s1 = s[1] ^ k1, s2 = s[2] ^ k2, s3 = s[3] ^ k3;
 #pragma unroll
@@ -461,10 +469,14 @@ __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te4, const ui
         k1 ^= k0;
         k2 ^= k1;
         k3 ^= k2;
-        const uint32_t t0 = xor3(xor3(T0[s0 >> 24], T1[(s1 >> 16) & 0xff], T2[(s2 >> 8) & 0xff]), T3[s3 & 0xff], k0);
-        const uint32_t t1 = xor3(xor3(T0[s1 >> 24], T1[(s2 >> 16) & 0xff], T2[(s3 >> 8) & 0xff]), T3[s0 & 0xff], k1);
-        const uint32_t t2 = xor3(xor3(T0[s2 >> 24], T1[(s3 >> 16) & 0xff], T2[(s0 >> 8) & 0xff]), T3[s1 & 0xff], k2);
-        const uint32_t t3 = xor3(xor3(T0[s3 >> 24], T1[(s0 >> 16) & 0xff], T2[(s1 >> 8) & 0xff]), T3[s2 & 0xff], k3);
+        const uint32_t t0 = xor3(xor3(AES_T(0, s0 >> 24), AES_T(1, (s1 >> 16) & 0xff), AES_T(2, (s2 >> 8) & 0xff)),
+                                 AES_T(3, s3 & 0xff), k0);
+        const uint32_t t1 = xor3(xor3(AES_T(0, s1 >> 24), AES_T(1, (s2 >> 16) & 0xff), AES_T(2, (s3 >> 8) & 0xff)),
+                                 AES_T(3, s0 & 0xff), k1);
+        const uint32_t t2 = xor3(xor3(AES_T(0, s2 >> 24), AES_T(1, (s3 >> 16) & 0xff), AES_T(2, (s0 >> 8) & 0xff)),
+                                 AES_T(3, s1 & 0xff), k2);
+        const uint32_t t3 = xor3(xor3(AES_T(0, s3 >> 24), AES_T(1, (s0 >> 16) & 0xff), AES_T(2, (s1 >> 8) & 0xff)),
+                                 AES_T(3, s2 & 0xff), k3);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     k0 ^= aes4_subword(te4, (k3 >> 16) & 0xff, (k3 >> 8) & 0xff, k3 & 0xff, k3 >> 24) ^ (RCON[9] << 24);
@@ -495,18 +507,18 @@ __device__ __forceinline__ void aes128_expand_lds(const uint32_t* te4, const uin
 }
 __device__ __forceinline__ void aes128_encrypt_rk(const uint32_t* te4, const uint32_t key[4], const uint4* rk,
                                                   uint32_t stride, uint32_t s[4]) {
-    const uint32_t* T0 = te4;
-    const uint32_t* T1 = te4 + 256;
-    const uint32_t* T2 = te4 + 512;
-    const uint32_t* T3 = te4 + 768;
     uint32_t s0 = s[0] ^ key[0], s1 = s[1] ^ key[1], s2 = s[2] ^ key[2], s3 = s[3] ^ key[3];
 #pragma unroll
     for (int r = 1; r < 10; r++) {
         const uint4 k = rk[(r - 1) * stride];
-        const uint32_t t0 = xor3(xor3(T0[s0 >> 24], T1[(s1 >> 16) & 0xff], T2[(s2 >> 8) & 0xff]), T3[s3 & 0xff], k.x);
-        const uint32_t t1 = xor3(xor3(T0[s1 >> 24], T1[(s2 >> 16) & 0xff], T2[(s3 >> 8) & 0xff]), T3[s0 & 0xff], k.y);
-        const uint32_t t2 = xor3(xor3(T0[s2 >> 24], T1[(s3 >> 16) & 0xff], T2[(s0 >> 8) & 0xff]), T3[s1 & 0xff], k.z);
-        const uint32_t t3 = xor3(xor3(T0[s3 >> 24], T1[(s0 >> 16) & 0xff], T2[(s1 >> 8) & 0xff]), T3[s2 & 0xff], k.w);
+        const uint32_t t0 = xor3(xor3(AES_T(0, s0 >> 24), AES_T(1, (s1 >> 16) & 0xff), AES_T(2, (s2 >> 8) & 0xff)),
+                                 AES_T(3, s3 & 0xff), k.x);
+        const uint32_t t1 = xor3(xor3(AES_T(0, s1 >> 24), AES_T(1, (s2 >> 16) & 0xff), AES_T(2, (s3 >> 8) & 0xff)),
+                                 AES_T(3, s0 & 0xff), k.y);
+        const uint32_t t2 = xor3(xor3(AES_T(0, s2 >> 24), AES_T(1, (s3 >> 16) & 0xff), AES_T(2, (s0 >> 8) & 0xff)),
+                                 AES_T(3, s1 & 0xff), k.z);
+        const uint32_t t3 = xor3(xor3(AES_T(0, s3 >> 24), AES_T(1, (s0 >> 16) & 0xff), AES_T(2, (s1 >> 8) & 0xff)),
+                                 AES_T(3, s2 & 0xff), k.w);
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint4 k = rk[9 * stride];

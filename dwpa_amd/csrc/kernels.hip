@@ -404,18 +404,22 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
 }
 
 // Te0..Te3 (crypto_dev.hpp aes128_encrypt_te4) into the workgroup's LDS, for kernels that verify keyver 3.
-constexpr uint32_t AES_LDS_WORDS = 1024;
+constexpr uint32_t AES_LDS_WORDS = 1024 * AES_SLICES;
 template <uint32_t VC>
 __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     if constexpr ((VC & VC_KV3) != 0) {
-        for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) te[k] = rotr(AES_TABLES.te0[k & 255], 8 * (k >> 8));
+        for (uint32_t k = threadIdx.x; k < AES_LDS_WORDS; k += blockDim.x) {
+            const uint32_t t = k / (256 * AES_SLICES), x = k / AES_SLICES & 255;  // table t, entry x, copy k % S
+            te[k] = rotr(AES_TABLES.te0[x], 8 * t);
+        }
         __syncthreads();
     }
-    return te;
+    return te + threadIdx.x % AES_SLICES;
 }
-// keyver-3 kernels keep 256-thread workgroups: a lane-sliced Te0 (64 KiB, 1024-thread workgroups, no bank
-// conflicts) measured level (profiles/r02/c5_sched/aes_sliced_ab)
-constexpr uint32_t vc_block(uint32_t) { return 256; }
+// keyver-3 kernels with sliced AES tables (64 KiB of LDS at S = 16) run 512-thread workgroups: two per CU, 4 waves
+// per SIMD.  (An earlier single lane-sliced Te0 with 1024-thread workgroups measured level in the C5 schedule of the
+// time, profiles/r02/c5_sched/aes_sliced_ab.)
+constexpr uint32_t vc_block(uint32_t vc) { return (vc & VC_KV3) && AES_SLICES > 1 ? 512 : 256; }
 
 // Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
 // wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
