@@ -442,14 +442,16 @@ __constant__ static const AesTables AES_TABLES = make_aes_tables();
 // registers; 40 more lookups per block).  S-box bytes come out of the T-tables already in place: S[x] is byte 3
 // of Te2/Te3, byte 2 of Te0/Te3, byte 1 of Te0/Te1 and byte 0 of Te1/Te2, so a SubWord is 4 lookups + 3 v_perm.
 //
-// Sliced tables (DWPA_KV3_SLICES = S, default 16): every table holds S interleaved copies, entry x of copy c at word
-// S x + c, and lane l reads copy l % S.  ds_read_b32 banks are (address / 4) mod 32 per 32-lane group, so with
-// S = 16 two lanes can only collide when they share a copy (l and l + 16) and their entries have the same parity:
-// 2-way conflicts at most.  The plain tables (S = 1) put 68 % of the keyver-3 verify's LDS cycles into random-index
-// bank conflicts; S = 16 halves the conflict cycles and takes the kernel alone from 2.02 to 1.56 ms per launch
-// (S = 8 barely helps: 4 lanes share a copy), 64 KiB per 512-thread workgroup (profiles/r02/kv3_slices_ab).
+// Sliced tables (build switch DWPA_KV3_SLICES = S, default 1 = plain): every table holds S interleaved copies,
+// entry x of copy c at word S x + c, and lane l reads copy l % S.  ds_read_b32 banks are (address / 4) mod 32 per
+// 32-lane group, so with S = 16 two lanes can only collide when they share a copy (l and l + 16) and their entries
+// have the same parity: 2-way conflicts at most.  The plain tables put 68 % of the keyver-3 verify's LDS cycles into
+// random-index bank conflicts; S = 16 halves the conflict cycles and takes the kernel alone from 2.02 to 1.56 ms per
+// launch, one C5 call from 51.8 to 51.2 ms -- but its 64 KiB, 512-thread workgroups (2 waves per SIMD at once) no
+// longer fit beside another call's PBKDF2 head, and two concurrent callers fell from 4.06 to 3.26 M PMK/s
+// (profiles/r02/kv3_slices_ab), so the default stays plain.
 #ifndef DWPA_KV3_SLICES
-#define DWPA_KV3_SLICES 16
+#define DWPA_KV3_SLICES 1
 #endif
 constexpr uint32_t AES_SLICES = DWPA_KV3_SLICES;
 #define AES_T(t, x) te4[(t) * 256u * AES_SLICES + (x) * AES_SLICES]

@@ -416,10 +416,14 @@ __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     }
     return te + threadIdx.x % AES_SLICES;
 }
-// keyver-3 kernels with sliced AES tables (64 KiB of LDS at S = 16) run 512-thread workgroups: two per CU, 4 waves
-// per SIMD.  (An earlier single lane-sliced Te0 with 1024-thread workgroups measured level in the C5 schedule of the
-// time, profiles/r02/c5_sched/aes_sliced_ab.)
-constexpr uint32_t vc_block(uint32_t vc) { return (vc & VC_KV3) && AES_SLICES > 1 ? 512 : 256; }
+// keyver-3 kernels with sliced AES tables (64 KiB of LDS at S = 16, an A/B build) run 512-thread workgroups: two per
+// CU, 4 waves per SIMD; the default plain tables keep 256-thread workgroups, which also fit beside a concurrent
+// call's PBKDF2 head.  (An earlier single lane-sliced Te0 with 1024-thread workgroups measured level,
+// profiles/r02/c5_sched/aes_sliced_ab.)
+#ifndef DWPA_KV3_BLOCK
+#define DWPA_KV3_BLOCK (AES_SLICES > 1 ? 512 : 256)
+#endif
+constexpr uint32_t vc_block(uint32_t vc) { return (vc & VC_KV3) ? DWPA_KV3_BLOCK : 256; }
 
 // Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
 // wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
