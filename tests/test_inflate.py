@@ -98,6 +98,10 @@ def test_decoder_matches_zlib(tool, tmp_path):
         "memlevel1.gz": _member(txt[:200_000], memlevel=1),
         "long_distance.gz": gzip.compress(rng.randbytes(40_000) + txt[:10_000] + rng.randbytes(20_000) +
                                           rng.randbytes(40_000)[:1] + txt[:10_000]),
+        # compressed streams longer than the decoder's 4 MiB input buffer: stored and Huffman blocks across refills
+        "big_random.gz": gzip.compress(rng.randbytes(5_000_000)),
+        "big_mixed.gz": gzip.compress(b"".join(rng.randbytes(700_000) if i % 2 else (b"password%07d\n" % i) * 60_000
+                                               for i in range(12)), compresslevel=1),
     }
     paths = []
     for name, blob in cases.items():
