@@ -66,7 +66,20 @@ PEAK_LANE_OPS = 256 * 128 * CLOCK_HZ
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node.  Under a launcher (WORLD_SIZE set) it must equal WORLD_SIZE; "
+                         "without one, N > 1 starts N rank processes of this script itself (one per GPU, "
+                         "LOCAL_RANK = device) and prints rank 0's line.  Default: WORLD_SIZE, else 1")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak (default): every rank scans its own batches, fixed work per GPU per step.  strong "
+                         "(c4 only): a step exhausts the whole 10^8 keyspace once, rank g of G taking the "
+                         "contiguous range [g*10^8/G, (g+1)*10^8/G) (SURVEY.md 8(d) C4); value = node PMK/s")
+    ap.add_argument("--t1-s", type=float, default=None,
+                    help="strong scaling: the one-GPU time to exhaust the keyspace (a previous --gpus 1 run's "
+                         "t_exhaust_s); the line then reports speedup S(G) = T1 / TG")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: every rank builds its shard schedule and runs the control plane only (gloo "
+                         "barrier, max/sum reductions); rank 0 prints the ranks' coverage (tests the N-rank path)")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 24,
@@ -263,8 +276,91 @@ def build_c3(args, local, S, Scan, Dictionary):
     return w
 
 
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK = LOCAL_RANK = r,
+    WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free port for the gloo control plane), one per GPU, as
+    torch.distributed.run would.  This parent never touches a GPU.  It relays rank 0's stdout (the JSON line),
+    stops the other ranks as soon as one fails, and fails unless all N ranks exited 0 and the line reports
+    n_gpus == N.  Returns the exit code."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True))
+    lines = []
+
+    def relay():
+        for raw in procs[0].stdout:
+            lines.append(raw.decode(errors="replace").rstrip("\n"))
+    reader = threading.Thread(target=relay, daemon=True)
+    reader.start()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p, c in zip(procs, codes):
+                if c is None:  # our own child's process group (start_new_session), never a pattern
+                    os.killpg(p.pid, signal.SIGTERM)
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    p.wait()
+            break
+        if all(c == 0 for c in codes):
+            break
+        time.sleep(0.2)
+    reader.join(timeout=30)
+    result = None
+    for ln in lines:
+        try:
+            obj = json.loads(ln)
+        except ValueError:
+            print(ln, flush=True)
+            continue
+        result = obj
+    if rc != 0:
+        print(f"bench.py: a rank failed with exit code {rc}", file=sys.stderr)
+        return rc if rc > 0 else 1
+    if result is None or result.get("n_gpus") != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but rank 0 reported "
+              f"{None if result is None else result.get('n_gpus')} ranks", file=sys.stderr)
+        return 4
+    print(json.dumps(result), flush=True)
+    return 0
+
+
+def check_device(local: int, rank: int) -> None:
+    """Fail loudly when this rank's GPU is not visible (a node with fewer GPUs than --gpus)."""
+    import dwpa_amd
+    n = dwpa_amd.device_count()
+    if local >= n:
+        raise SystemExit(f"bench.py rank {rank}: device {local} not visible ({n} gfx950 devices); "
+                         "DWPA_BENCH_ONE_DEVICE=1 rehearses N ranks on one GPU")
+
+
 def main():
     args = parse()
+    if os.environ.get("WORLD_SIZE") is None and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.scaling == "strong" and args.workload != "c4":
+        sys.exit("bench.py: --scaling strong is defined for --workload c4 (the numeric keyspace)")
     if args.peak_costs:
         global C_MIN_CYCLES, PEAK_COMPRESSIONS
         from tools.cmin import from_costs
@@ -272,15 +368,19 @@ def main():
         PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("DWPA_BENCH_ONE_DEVICE") == "1":
         local = 0  # rehearsal of the N>1 control path with every rank on one GPU (not a scaling measurement)
+    if args.dry_run:
+        return main_dry(args, world, rank)
+    check_device(local, rank)
     if args.workload in ("c1", "c5"):
         return main_ffi(args, world, rank, local)
     if args.workload == "c2files":
         return main_files(args, world, rank, local)
+    if args.scaling == "strong":
+        return main_strong(args, world, rank, local)
     if world > 1:
         # control plane only (barrier, max-over-ranks time, sum of PMKs): the data path shards the keyspace and
         # never exchanges data, so there is no RCCL collective on the GPU.
@@ -428,6 +528,148 @@ def main():
         sys.exit(3)
 
 
+def main_dry(args, world, rank):
+    """--dry-run: the N-rank control path with no GPU.  Every rank builds the shard schedule its workload would
+    scan (weak: dictionary/keyspace batches r, r+N, ... of the timed steps; strong c4: its contiguous keyspace
+    range), then the gloo barrier and the max/sum reductions run as in a measured run; rank 0 prints the coverage
+    of every rank.  tests/test_bench_spawn.py checks N ranks and disjoint coverage through `--gpus N`."""
+    import torch.distributed as dist
+    from dwpa_amd.shard import batch_ids, reduce_timing, strong_batches
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = (args.batch + 63) & ~63
+    if args.scaling == "strong":
+        mine = [list(x) for x in strong_batches(10 ** 8, rank, world, B)]
+        units = sum(c for _, c in mine)
+    else:
+        n = 10 ** 8 if args.workload == "c4" else args.dict_words
+        nb = (n + B - 1) // B
+        mine = batch_ids(rank, world, args.warmup, args.steps, nb)
+        units = len(mine) * B
+    gathered = [mine]
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        dist.barrier()
+        _, total = reduce_timing(dist, 0.0, units)
+    else:
+        total = float(units)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "PMK/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "scaling": args.scaling,
+                          "config": {"workload": args.workload, "batch_per_step": B},
+                          "units_all_ranks": total, "coverage": gathered, "pid": os.getpid()}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main_strong(args, world, rank, local):
+    """C4 strong scaling: a step exhausts the 10^8 keyspace 00000000..99999999 once; rank g
+    of G scans [g*10^8/G, (g+1)*10^8/G) in equal batches (generated in-kernel, PBKDF2 + PMKID verify).  Time per
+    step = max over ranks (gloo), value = node PMK/s; with --t1-s the line carries S(G) = T1 / TG.  The planted
+    PSK 73019412 must be reported by the rank whose range holds it, in every timed pass."""
+    import torch.distributed as dist
+    import dwpa_amd
+    from dwpa_amd import synth as S
+    from dwpa_amd.device import Event, Stream
+    from dwpa_amd.shard import contiguous_shard, reduce_timing, strong_batches
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    w = build_c4(args, local, S, dwpa_amd.Scan, None)
+    sc = w.scans[0]
+    stream = Stream(local)
+    hs = stream.handle
+    n = 10 ** 8
+    sched = strong_batches(n, rank, world, w.B)
+    lo, hi = contiguous_shard(n, rank, world)
+
+    def scan(first, cnt, ev=None):
+        sc.load_numeric(first, cnt, 8, hs)
+        if ev is not None:
+            ev[0].record(stream)
+        sc.pbkdf2(0, hs)
+        if ev is not None:
+            ev[1].record(stream)
+        sc.verify(0, hs)
+
+    for _ in range(args.warmup):
+        scan(*sched[0])
+    stream.synchronize()
+    sc.hits(hs)
+    kev = [[(Event(local), Event(local)) for _ in sched] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    stream.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        for j, (first, cnt) in enumerate(sched):
+            scan(first, cnt, kev[s][j])
+    stream.synchronize()
+    elapsed_local = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    done = float(sum(c for _, c in sched) * args.steps)
+    hits = sc.hits(hs)
+    want = args.steps if lo <= w.plant < hi else 0
+    good = sum(1 for h in hits if h["cand"] == w.plant and h["pmk"] == S.pmk(b"%08d" % w.plant, w.essid))
+    ok_local = good == want and len(hits) == want
+    kms = [a.elapsed_ms(b) for step in kev for a, b in step]
+    kernel_ms = sum(kms) / len(kms)
+    kernel_pmk_s = sum(c for _, c in sched) * args.steps / (sum(kms) * 1e-3)
+    if world > 1:
+        import torch
+        elapsed, total = reduce_timing(dist, elapsed, done)
+        okt = torch.tensor([1.0 if ok_local else 0.0], dtype=torch.float64)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        verified = bool(okt.item() == 1.0)
+        shards = [None] * world
+        dist.all_gather_object(shards, [lo, hi, len(sched), round(elapsed_local, 4)])
+    else:
+        total, verified, shards = done, ok_local, [[lo, hi, len(sched), round(elapsed_local, 4)]]
+    if rank == 0:
+        t_exhaust = elapsed / args.steps
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(w.cpu_line, w.cpu_keys, args.cpu_seconds, w.cpu_what)
+        pmk_per_launch = sum(c for _, c in sched) / len(sched)
+        traffic_pmk = TRAFFIC_BYTES_PER_PMK["c4"]
+        print(json.dumps({
+            "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "C4 strong scaling: the 8-digit keyspace 00000000..99999999 (10^8, generated on "
+                                   "the GPU) exhausted once per step, rank g of G scanning [g*10^8/G, (g+1)*10^8/G); "
+                                   "one ESSID, PMKID line", "keyspace": n, "batch_max": w.B,
+                       "parallelism": f"contiguous keyspace shards x{world}, no collective on the data path"},
+            "t_exhaust_s": round(t_exhaust, 4),
+            "speedup": round(args.t1_s / t_exhaust, 4) if args.t1_s else None,
+            "speedup_basis": f"S(G) = T1 / TG with T1 = {args.t1_s} s (--t1-s)" if args.t1_s else None,
+            "shards": shards,
+            "roofline": {
+                "bound": "valu", "kernel": "k_pbkdf2 (rank 0)",
+                "achieved": round(kernel_pmk_s * COMPRESSIONS_PER_PMK / 1e9, 3),
+                "peak": round(PEAK_COMPRESSIONS / 1e9, 3), "unit": "G SHA-1 compressions/s",
+                "frac": round(kernel_pmk_s * COMPRESSIONS_PER_PMK / PEAK_COMPRESSIONS, 4),
+                "traffic": round(traffic_pmk * pmk_per_launch), "algorithmic_bytes": round(ALGO_BYTES_PER_PMK * pmk_per_launch),
+                "traffic_unit": "HBM bytes per launch (" + TRAFFIC_SOURCE["c4"] + ")",
+                "kernel_ms": round(kernel_ms, 3), "pmk_per_launch": pmk_per_launch,
+                "kernel_pmk_per_s": round(kernel_pmk_s, 1),
+                "frac_guide_valu_peak": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * SURVEY_OPS_PER_COMPRESSION
+                                              / PEAK_LANE_OPS, 4)},
+            "cpu_baseline": cpu, "hits_verified": verified,
+            "hits_checked": "the planted PSK 73019412 with its PMK, once per timed pass, on the rank holding it; "
+                            "no other hit on any rank"}), flush=True)
+    sc.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0 and not verified:
+        sys.exit(3)
+
+
 def main_ffi(args, world, rank, local):
     """C1 / C5 legs: the server-side FFI call (dwpa_check_m22000 / dwpa_check_batch) on host buffers, as PHP
     makes it (common.php:157, :902).  A step = one call over the whole config: C1 = 10k keys x 1 PMKID line,
@@ -449,7 +691,7 @@ def main_ffi(args, world, rank, local):
         jobs = [(line, keys, False, 128)]
         desc = "C1: 10,000 PSKs (1 % $HEX[]) vs one PMKID line, dwpa_check_m22000 per step (FFI, host buffers)"
     else:
-        jobs = S.c5_jobs()
+        jobs, plants = S.c5_plan()
         desc = ("C5: 250 PMKID + 250 x keyver 1/2/3 EAPOL lines (NC offsets 0..+-8, LE/BE) + 10 zero-PMK jobs, "
                 "202 keys per job, nc=128 (261 attempts), dwpa_check_batch per step (FFI, host buffers)")
     import threading
@@ -494,22 +736,23 @@ def main_ffi(args, world, rank, local):
         total = keys_all
     got = batch.results()
     same = all(b.results() == got for b in batches[1:])
+    mismatches = None
     if args.workload == "c1":
         verified = bool(got[0]) and got[0][0] == psk and got[0][3] == S.pmk(psk, bytes.fromhex(line.split(b"*")[5].decode()))
     else:
-        # every hit's exact [PSK, NC, endian, PMK] tuple, re-derived by the oracle from the winning key alone
-        # (the first-key-in-order rule and the misses are checked by tests/test_gpu_configs.py)
+        # every job exactly: the planted key's [PSK, NC, endian, PMK] tuple re-derived by the oracle from that key
+        # alone, or False where no key was planted (tests/test_gpu_configs.py adds the first-key prefix checks)
         from concurrent.futures import ThreadPoolExecutor
         from oracle import oracle as O
 
-        def hit_alone(i):
+        def expected(i):
             line, keys, pmk, nc = jobs[i]
-            k = next(x for x in keys if x is not None and O.hc_unhex(x) == got[i][0])
-            return O.c_check_key_m22000(line, [k], pmk if keys[0] == k else False, nc) == got[i]
-        hit_jobs = [i for i, g in enumerate(got) if g]
+            p = plants[i]
+            return False if p is None else O.c_check_key_m22000(line, [keys[p]], pmk if p == 0 else False, nc)
         with ThreadPoolExecutor(host_cpu()["threads_all"]) as ex:
-            exact = sum(ex.map(hit_alone, hit_jobs))
-        verified = exact == len(hit_jobs) and len(hit_jobs) >= 0.85 * len(jobs)
+            exp = list(ex.map(expected, range(len(jobs))))
+        mismatches = sum(1 for g, e in zip(got, exp) if g != e)
+        verified = mismatches == 0 and sum(1 for e in exp if e) >= 0.85 * len(jobs)
     verified = verified and same
     if rank == 0:
         cpu = None
@@ -523,8 +766,10 @@ def main_ffi(args, world, rank, local):
                        "callers": callers, "parallelism": f"replicas x{world}"},
             "roofline": None, "cpu_baseline": cpu, "hits_verified": verified,
             "hits": sum(1 for g in got if g),
-            "hits_checked": "every hit's [PSK, NC, endian, PMK] re-derived by the CPU oracle" if args.workload == "c5"
-                            else "the planted PSK and its PMK"}), flush=True)
+            "mismatches": mismatches if args.workload == "c5" else None,
+            "hits_checked": "every job's result against its planted key's [PSK, NC, endian, PMK] (re-derived by the "
+                            "CPU oracle) or False" if args.workload == "c5" else "the planted PSK and its PMK"}),
+              flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

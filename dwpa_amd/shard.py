@@ -18,6 +18,18 @@ def contiguous_shard(n: int, k: int, g: int):
     return n * k // g, n * (k + 1) // g
 
 
+def strong_batches(n: int, rank: int, world: int, batch: int):
+    """Strong scaling: rank g's contiguous range [g*n/G, (g+1)*n/G) cut into the fewest
+    batches of at most `batch` candidates, all of (nearly) equal size so no launch runs a thin last wave round.
+    Returns [(first, count)]."""
+    b, e = contiguous_shard(n, rank, world)
+    m = e - b
+    if m <= 0:
+        return []
+    nb = -(-m // max(1, batch))
+    return [(b + m * j // nb, m * (j + 1) // nb - m * j // nb) for j in range(nb)]
+
+
 def reduce_timing(dist, elapsed: float, done: float):
     """max elapsed and summed PMKs over ranks (gloo tensors on the CPU)."""
     import torch

@@ -159,13 +159,20 @@ def c1_workload(seed: int = 0, n: int = 10_000):
 
 def c5_jobs(seed: int = 5, per_kind: int = 250, keys_per_job: int = 202, essids: int = 200, nc: int = 128,
             hit_rate: float = 0.9, zero_pmk: int = 10):
+    """The C5 batch (see c5_plan) without the planted indices."""
+    return c5_plan(seed, per_kind, keys_per_job, essids, nc, hit_rate, zero_pmk)[0]
+
+
+def c5_plan(seed: int = 5, per_kind: int = 250, keys_per_job: int = 202, essids: int = 200, nc: int = 128,
+            hit_rate: float = 0.9, zero_pmk: int = 10):
     """per_kind PMKID + keyver 1/2/3 EAPOL lines (nonce offsets uniform in {0, +-1..+-8} x
     {LE, BE}) plus zero_pmk zero-PMK jobs (common.php:592), keys_per_job candidates per job (the put_work cap,
     common.php:937), the true PSK planted at a random index in hit_rate of the jobs.  ESSIDs are drawn from a
-    pool of `essids` networks so the batch path groups lines.  Returns [(line, keys, pmk, nc)]."""
+    pool of `essids` networks so the batch path groups lines.  Returns ([(line, keys, pmk, nc)], plants) where
+    plants[i] is the index of job i's planted key (None: no key of the job was planted, the job must miss)."""
     rng = random.Random(seed)
     nets = [random_net(rng) for _ in range(essids)]
-    jobs = []
+    jobs, plants = [], []
     for kind in ("pmkid", 1, 2, 3):
         for _ in range(per_kind):
             essid, ap, sta, an, sn = nets[rng.randrange(essids)]
@@ -180,8 +187,10 @@ def c5_jobs(seed: int = 5, per_kind: int = 250, keys_per_job: int = 202, essids:
             keys = [fast_psk(rng) for _ in range(keys_per_job - 1)]
             if rng.random() < hit_rate:
                 keys.insert(rng.randrange(keys_per_job), psk)
+                plants.append(keys.index(psk))
             else:
                 keys.append(fast_psk(rng))
+                plants.append(None)
             jobs.append((line, keys, False, nc))
     zpmk = b"\0" * 32
     for i in range(zero_pmk):
@@ -192,4 +201,5 @@ def c5_jobs(seed: int = 5, per_kind: int = 250, keys_per_job: int = 202, essids:
             line = eapol_line(b"", essid, ap, sta, rng.randbytes(32), rng.randbytes(32), 2 + i % 4 // 2,
                               rng.randint(-8, 8), "BE", the_pmk=zpmk, rng=rng)
         jobs.append((line, [b""], zpmk, nc))
-    return jobs
+        plants.append(0)
+    return jobs, plants

@@ -44,3 +44,8 @@ def mixed():
 @pytest.fixture(scope="session")
 def kat():
     return load_golden("kat.json")
+
+
+@pytest.fixture(scope="session")
+def nc_windows():
+    return load_golden("nc_windows.json")["jobs"]

@@ -255,11 +255,79 @@ def mixed():
     return {"jobs": jobs}
 
 
+def nc_windows():
+    """The nonce windows of check_key_m22000's real call sites (common.php:250-300, halfnc = (nc>>1)+1):
+    put_work's PMK propagation nc = |nc|*2+128 (:919; |nc| = 65 -> 258, halfnc 130, 521 attempts), submission's
+    (|nc|<<1)+1 (:606; 131, halfnc 66), odd and negative windows.  Hits are planted at +-halfnc in both endians
+    (inside) and one past it (outside), at the first (N+0) and last (N-halfnc) attempt of a 521-attempt list, behind
+    hundreds of keys (attempt-parallel verify, items past the first waves), with a caller PMK, and with short
+    ANONCEs whose $n grows (explicit per-key lists at 521 attempts)."""
+    rng = random.Random(258)
+    jobs = []
+
+    def add(line, keys, pmk=False, nc=128, tag=""):
+        r = both(line, keys, pmk, nc)
+        jobs.append({"tag": tag, "line": line.decode("latin-1"),
+                     "keys": [None if k is None else k.hex() for k in keys],
+                     "pmk": pmk.hex() if pmk else None, "nc": nc, "expect": enc(r)})
+        return r
+
+    for nc in (258, 131, 17, 1):
+        half = (nc >> 1) + 1
+        for kv in (1, 2, 3):
+            for off, endian in ((half, "LE"), (-half, "LE"), (half, "BE"), (-half, "BE"), (half + 1, "LE"),
+                                (-half - 1, "BE")):
+                essid, ap, sta, an, sn = S.random_net(rng)
+                psk = S.random_psk(rng)
+                keys = [S.random_psk(rng) for _ in range(rng.randint(0, 2))] + [psk]
+                r = add(S.eapol_line(psk, essid, ap, sta, an, sn, kv, off, endian, rng=rng), keys, nc=nc,
+                        tag=f"nc{nc}-kv{kv}-{endian}{off:+d}")
+                assert bool(r) == (abs(off) <= half), (nc, off, r)
+    # first attempt (N+0) and last attempt (N-130) of a 521-attempt list, the key behind 300 (keyver 1/2) or
+    # 40 (keyver 3: the pure-Python cross-check's AES is slow) other keys
+    for kv, nkeys in ((1, 300), (2, 300), (3, 40)):
+        for off, endian in ((0, "BE"), (-130, "BE"), (130, "LE")):
+            essid, ap, sta, an, sn = S.random_net(rng)
+            psk = S.random_psk(rng)
+            keys = [S.random_psk(rng) for _ in range(nkeys)] + [psk]
+            r = add(S.eapol_line(psk, essid, ap, sta, an, sn, kv, off, endian, rng=rng), keys, nc=258,
+                    tag=f"nc258-last-key-kv{kv}-{endian}{off:+d}")
+            assert r and r[0] == psk
+    # negative windows: only N+0 is tried ((nc>>1)+1 <= 0)
+    for nc in (-1, -3, -258):
+        essid, ap, sta, an, sn = S.random_net(rng)
+        psk = S.random_psk(rng)
+        assert add(S.eapol_line(psk, essid, ap, sta, an, sn, 2, 0, "LE", rng=rng), [psk], nc=nc, tag=f"nc{nc}-0")
+        assert not add(S.eapol_line(psk, essid, ap, sta, an, sn, 2, 1, "BE", rng=rng), [psk], nc=nc,
+                       tag=f"nc{nc}-1-miss")
+    # PMK propagation itself (:919): caller PMK, key '', nc = |-65|*2+128
+    essid, ap, sta, an, sn = S.random_net(rng)
+    psk = S.random_psk(rng)
+    real = S.pmk(psk, essid)
+    for kv in (1, 2, 3):
+        line = S.eapol_line(psk, essid, rng.randbytes(6), sta, rng.randbytes(32), rng.randbytes(32), kv, -65, "BE",
+                            rng=rng)
+        assert add(line, [b""], real, abs(-65) * 2 + 128, tag=f"pmk-propagate-258-kv{kv}")
+        assert not add(line, [b""], real, abs(-32) * 2 + 1, tag=f"pmk-submission-65-kv{kv}-miss")
+    # short ANONCE at 521 attempts: $n grows, explicit lists; winning attempt late in the list, behind a key
+    for (anlen, keys_before, att, kv) in [(20, 1, 520, 2), (29, 0, 259, 1), (20, 2, 300, 2), (10, 1, 0, 1)]:
+        essid, ap, sta, an, sn = S.random_net(rng)
+        sn = bytes([0]) + sn[1:]
+        an = bytes([255]) + an[1:anlen]
+        psk = S.random_psk(rng)
+        line = short_anonce_line(psk, essid, ap, sta, sn, an, kv, keys_before, att, 258)
+        keys = [S.random_psk(rng) for _ in range(keys_before)] + [psk, S.random_psk(rng)]
+        assert add(line, keys, nc=258, tag=f"short-anonce-258-{anlen}-{keys_before}-{att}-kv{kv}")
+    return {"jobs": jobs}
+
+
 def main():
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kat(), f, indent=1)
     with open(os.path.join(HERE, "mixed.json"), "w") as f:
         json.dump(mixed(), f, indent=0)
+    with open(os.path.join(HERE, "nc_windows.json"), "w") as f:
+        json.dump(nc_windows(), f, indent=0)
     print("ok")
 
 

@@ -1,0 +1,75 @@
+"""CPU: `bench.py --gpus N` starts its own N rank processes when no launcher set WORLD_SIZE.
+
+`--dry-run` runs the whole N-rank control path -- the parent's spawn, gloo rendezvous on 127.0.0.1, barrier,
+max/sum reductions -- with no GPU, and rank 0 prints every rank's shard schedule.  Checked: the line reports
+n_gpus == N, the ranks' batches are disjoint (weak scaling) or tile the 10^8 keyspace contiguously (strong
+scaling), a failing rank fails the parent, and a launcher's WORLD_SIZE must match --gpus.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*argv, env_extra=None, timeout=180):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], capture_output=True, text=True,
+                          env=env, timeout=timeout, cwd=ROOT)
+
+
+def _line(r):
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_weak_spawn_n_ranks_disjoint_batches(n):
+    out = _line(_bench("--gpus", str(n), "--dry-run", "--steps", "4", "--warmup", "1", "--dict-words", "200000000"))
+    assert out["n_gpus"] == n and out["dry_run"]
+    cov = out["coverage"]
+    assert len(cov) == n and all(len(c) == 4 for c in cov)
+    for s in range(4):  # within every timed step the ranks scan distinct batches
+        assert len({c[s] for c in cov}) == n
+    assert out["units_all_ranks"] == n * 4 * out["config"]["batch_per_step"]
+
+
+def test_strong_spawn_tiles_keyspace():
+    out = _line(_bench("--gpus", "3", "--dry-run", "--workload", "c4", "--scaling", "strong"))
+    assert out["n_gpus"] == 3 and out["scaling"] == "strong"
+    spans = sorted((f, f + c) for rank in out["coverage"] for f, c in rank)
+    assert spans[0][0] == 0 and spans[-1][1] == 10 ** 8
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    assert out["units_all_ranks"] == 10 ** 8
+    # rank g holds [g*10^8/G, (g+1)*10^8/G)
+    for g, rank in enumerate(out["coverage"]):
+        assert rank[0][0] == g * 10 ** 8 // 3 and rank[-1][0] + rank[-1][1] == (g + 1) * 10 ** 8 // 3
+
+
+def test_single_rank_dry_run_without_spawn():
+    out = _line(_bench("--dry-run", "--steps", "2", "--warmup", "0"))
+    assert out["n_gpus"] == 1 and len(out["coverage"]) == 1
+
+
+def test_failing_rank_fails_the_parent():
+    """Without a GPU every rank's device check fails: the parent must stop the others and exit non-zero."""
+    r = _bench("--gpus", "2", "--workload", "c4", "--scaling", "strong", "--steps", "1", "--warmup", "0")
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_launcher_world_size_must_match_gpus():
+    r = _bench("--gpus", "2", "--dry-run", env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_strong_scaling_only_for_c4():
+    r = _bench("--dry-run", "--scaling", "strong")
+    assert r.returncode != 0

@@ -63,6 +63,18 @@ def test_mixed_golden_batch(mixed):
         assert g == dec(j["expect"]), j["tag"]
 
 
+def test_nc_windows_golden(nc_windows):
+    """The call sites' windows (nc 258 = put_work PMK propagation :919, 131 = submission :606, odd, negative),
+    hits at +-halfnc in both endians and one past, the first/last attempt of 521-attempt lists behind 300 keys
+    (attempt-parallel verify), caller PMKs and growing short-ANONCE lists: one call per job, then one batch."""
+    for j in nc_windows:
+        line, keys, pmk, nc = job_args(j)
+        assert dwpa_amd.check_key_m22000(line, keys, pmk, nc) == dec(j["expect"]), j["tag"]
+    got = dwpa_amd.check_batch([job_args(j) for j in nc_windows])
+    for j, g in zip(nc_windows, got):
+        assert g == dec(j["expect"]), j["tag"]
+
+
 def _oracle_many(jobs):
     with ThreadPoolExecutor(16) as ex:
         return list(ex.map(lambda a: O.c_check_key_m22000(*a), jobs))

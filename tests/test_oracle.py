@@ -49,6 +49,18 @@ def test_mixed_golden_both_oracles(mixed):
         assert O.py_check_key_m22000(line, keys, pmk, nc) == exp, j["tag"]
 
 
+def test_nc_windows_golden(nc_windows):
+    """The call sites' nonce windows (common.php:606,919: nc 131 and 258; odd and negative nc): the C oracle on
+    every fixture job, the pure-Python oracle on the short ones (its AES makes the 300-key jobs take minutes;
+    make_golden.py asserted both on all of them when it wrote the file)."""
+    for j in nc_windows:
+        line, keys, pmk, nc = job_args(j)
+        exp = dec(j["expect"])
+        assert O.c_check_key_m22000(line, keys, pmk, nc) == exp, j["tag"]
+        if len(keys) <= 4 and (nc < 200 or line[4:6] == b"02" and b"kv3" not in j["tag"].encode()):
+            assert O.py_check_key_m22000(line, keys, pmk, nc) == exp, j["tag"]
+
+
 @pytest.mark.parametrize("seed", [11, 12])
 def test_oracles_agree_random(seed):
     rng = random.Random(seed)
