@@ -94,10 +94,11 @@ def parse():
                     help="batches in flight (c2/c3/c4), each on its own scan working set and HIP stream.  Measured "
                          "A/B (profiles/r01/pipeline/): 2 gains 0.2 %% -- the next batch's PBKDF2 waves hold the "
                          "SIMDs, so the verify runs starved beside it -- and blurs the per-kernel events; default 1")
-    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files"], default="c2",
+    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files", "c1lat"], default="c2",
                     help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs; "
                          "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
-                         "dwpa_crack_files from a gz dictionary on disk (the help_crack client path)")
+                         "dwpa_crack_files from a gz dictionary on disk (the help_crack client path); c1lat = "
+                         "server call latency at 1/16/202 keys per call beside one CPU core")
     ap.add_argument("--essids", type=int, default=1000, help="c3: number of ESSIDs (BASELINE: 1000)")
     ap.add_argument("--scan-run", action="store_true",
                     help="c2/c4: derive + verify through dwpa_scan_run (the multi-group kernel C3 uses) instead of "
@@ -379,6 +380,8 @@ def main():
         return main_ffi(args, world, rank, local)
     if args.workload == "c2files":
         return main_files(args, world, rank, local)
+    if args.workload == "c1lat":
+        return main_latency(args, world, rank, local)
     if args.scaling == "strong":
         return main_strong(args, world, rank, local)
     if world > 1:
@@ -777,6 +780,76 @@ def main_ffi(args, world, rank, local):
         sys.exit(3)
 
 
+def main_latency(args, world, rank, local):
+    """Server call latency.  put_work checks each submitted PSK with its own
+    check_key_m22000($struct, [$psk]) call, default nc=128 (common.php:902), for at most ~202 submissions per
+    request (:937).  Measured here per FFI call: 1, 16 and 202 keys against one PMKID line and one EAPOL keyver-2
+    line at nc=128 (dwpa_check_m22000, the true key last), and the whole 202-submission request as one
+    dwpa_check_batch of 202 one-key jobs -- each beside the same call on one CPU core (the OpenSSL restatement,
+    one PHP request).  A call that derives k PMKs cannot finish before one PBKDF2 chain does (8,194 dependent
+    SHA-1 compressions per lane, a lone wave on its SIMD), so below a few keys per call the CPU wins and callers
+    should batch."""
+    import random
+    import statistics
+    import dwpa_amd
+    from dwpa_amd import synth as S
+    from oracle import oracle as O
+    rng = random.Random(7)
+    essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
+    rows = []
+    reps = max(3, args.steps)
+
+    def timed(fn, n):
+        fn()  # warm (first call of a shape: staging buffers)
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            r = fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts) * 1e3, r
+
+    for kind in ("pmkid", "eapol-kv2"):
+        for k in (1, 16, 202):
+            keys = [S.fast_psk(rng) for _ in range(k - 1)]
+            psk = S.fast_psk(rng)
+            keys.append(psk)
+            line = (S.pmkid_line(psk, essid, ap, sta) if kind == "pmkid" else
+                    S.eapol_line(psk, essid, ap, sta, an, sn, 2, -5, "BE", rng=rng))
+            gpu_ms, got = timed(lambda: dwpa_amd.check_key_m22000(line, keys), reps)
+            cpu_ms, exp = timed(lambda: O.c_check_key_m22000(line, keys), max(1, min(reps, 3 if k > 16 else reps)))
+            rows.append({"call": f"check_key_m22000, {kind}, {k} key(s), nc=128", "keys": k,
+                         "gpu_ms_per_call": round(gpu_ms, 3), "cpu_1core_ms_per_call": round(cpu_ms, 3),
+                         "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp})
+    # the whole put_work request: 202 submitted PSKs, each against its net (one key per job), one batch call
+    jobs = []
+    for i in range(202):
+        e2, a2, s2, an2, sn2 = S.random_net(rng)
+        psk = S.fast_psk(rng)
+        line = (S.pmkid_line(psk, e2, a2, s2) if i % 2 else S.eapol_line(psk, e2, a2, s2, an2, sn2, 2, i % 9 - 4, "LE",
+                                                                         rng=rng))
+        jobs.append((line, [psk if i % 3 else S.fast_psk(rng)], False, 128))
+    batch = dwpa_amd.BatchJobs(jobs)
+    gpu_ms, _ = timed(lambda: batch.run(), reps)
+    got = batch.results()
+    t0 = time.perf_counter()
+    exp = [O.c_check_key_m22000(*j) for j in jobs]
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    rows.append({"call": "put_work request: 202 one-key jobs (PMKID + EAPOL keyver 2, nc=128) in one "
+                         "dwpa_check_batch vs 202 check_key_m22000 calls", "keys": 202,
+                 "gpu_ms_per_call": round(gpu_ms, 3), "cpu_1core_ms_per_call": round(cpu_ms, 3),
+                 "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp})
+    ok = all(r["same_result"] for r in rows)
+    if rank == 0:
+        print(json.dumps({"metric": "ms per server check call (latency), m22000", "value": rows[0]["gpu_ms_per_call"],
+                          "unit": "ms", "n_gpus": world, "steps": reps, "warmup": 1, "higher_is_better": False,
+                          "dtype": "u32", "data": "synthetic",
+                          "config": {"workload": "C1 latency: FFI calls of 1/16/202 keys (put_work, common.php:902,"
+                                                 "937) beside one CPU core", "parallelism": "none"},
+                          "rows": rows, "cpu_model": host_cpu()["cpu_model"], "hits_verified": ok}), flush=True)
+    if rank == 0 and not ok:
+        sys.exit(3)
+
+
 def main_files(args, world, rank, local):
     """C2 end to end through the client path (dwpa_crack_files, help_crack.py:765-802): the 100M-word dictionary
     as a gzip file on local disk, streamed, inflated and $HEX[]-decoded on the host, uploaded chunk by chunk and
@@ -874,107 +947,88 @@ def main_files(args, world, rank, local):
 
 
 def cpu_baseline_jobs(jobs, seconds):
-    """The PHP path for the same jobs: check_key_m22000 per job on the OpenSSL restatement (oracle/), jobs in
-    parallel on up to 16 host threads, over a bounded prefix of the job list."""
-    from concurrent.futures import ThreadPoolExecutor
-    from oracle import oracle as O
+    """The PHP path for the same jobs: check_key_m22000 per job on the OpenSSL restatement (oracle/), as PHP-FPM
+    runs requests: one job per worker process at a time, min(16, affinity) single-threaded processes (oracle/
+    php_pool.py), over a bounded prefix of the job list; plus one process alone (one PHP request after another)."""
+    from oracle.php_pool import PhpPool, _job_pmks
     hc = host_cpu()
-    threads = hc["threads_all"]
+    P = hc["threads_all"]
     if len(jobs) == 1:
         line, keys, pmk, nc = jobs[0]
-        probe = keys[-threads * 32:]
-        t0 = time.perf_counter()
-        O.c_check_many(line, probe, nc, threads)
-        rate = len(probe) / (time.perf_counter() - t0)
-        sample = keys[-int(max(len(probe), min(len(keys), rate * seconds))):]
-        t0 = time.perf_counter()
-        idx, _ = O.c_check_many(line, sample, nc, threads)
-        dt = time.perf_counter() - t0
-        one = keys[-max(8, int(rate / threads * seconds / 4)):]
-        t1 = time.perf_counter()
-        O.c_check_many(line, one, nc, 1)
-        dt1 = time.perf_counter() - t1
-        return dict({"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
-                     "sample": f"last {len(sample)} keys (ending at the true PSK), one check per key, {dt:.1f} s",
-                     "found_planted": idx == len(sample) - 1,
-                     "one_thread": {"value": round(len(one) / dt1, 1), "unit": "PMK/s", "cores": 1,
-                                    "sample": f"last {len(one)} keys on one thread (one PHP request), {dt1:.1f} s"}},
-                    **hc)
-    def derived(job):
-        """check_key_m22000 on one job; returns the PMKs it derived (it stops at the first matching key)."""
-        line, keys, pmk, nc = job
-        r = O.c_check_key_m22000(line, keys, pmk, nc)
-        if r is False:
-            return sum(1 for k in keys if k is not None)
-        k = next(i for i, x in enumerate(keys) if x is not None and O.hc_unhex(x) == r[0])
-        return sum(1 for x in keys[:k + 1] if x is not None)
-
-    done, nkeys = 0, 0
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(threads) as ex:
-        while done < len(jobs) and time.perf_counter() - t0 < seconds:
-            chunk = jobs[done:done + threads]
-            nkeys += sum(ex.map(derived, chunk))
-            done += len(chunk)
-    dt = time.perf_counter() - t0
-    # one PHP request: the jobs one after another on one thread
+        return cpu_baseline(line, lambda m: keys[-m:], seconds, "keys (ending at the true PSK)", nc=nc)
+    pool = PhpPool(P)
+    try:
+        done, nkeys, dt = pool.job_pmks(jobs, seconds)
+    finally:
+        pool.close()
     done1, nkeys1 = 0, 0
     t1 = time.perf_counter()
     while done1 < len(jobs) and time.perf_counter() - t1 < seconds / 3:
-        nkeys1 += derived(jobs[done1])
+        nkeys1 += _job_pmks(jobs[done1])
         done1 += 1
     dt1 = time.perf_counter() - t1
-    return dict({"value": round(nkeys / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+    return dict({"value": round(nkeys / dt, 1), "unit": "PMK/s", "cores": P, "kind": "port",
+                 "workers": f"{P} single-threaded worker processes (PHP-FPM model, oracle/php_pool.py)",
                  "sample": f"first {done} jobs ({nkeys} PMKs derived: a job stops at its first matching key), "
-                           f"check_key_m22000 per job on {threads} threads, {dt:.1f} s",
+                           f"check_key_m22000 per job, {dt:.1f} s",
+                 "scaling_vs_one_process": round(nkeys / dt / (nkeys1 / dt1), 2),
                  "one_thread": {"value": round(nkeys1 / dt1, 1), "unit": "PMK/s", "cores": 1,
-                                "sample": f"first {done1} jobs ({nkeys1} PMKs derived) on 1 thread (one PHP request), "
-                                          f"{dt1:.1f} s"}},
+                                "sample": f"first {done1} jobs ({nkeys1} PMKs derived) in one process (one PHP "
+                                          f"request after another), {dt1:.1f} s"}},
                 **hc)
 
 
 def host_cpu():
     """CPU model and counts of the host the baseline runs on.  threads_all = min(16, affinity): a GPU box gives one
-    GPU a 16-core share, and its nproc reports the whole machine."""
+    GPU a 16-core share, and its nproc reports the whole machine.  physical_cores_affinity counts distinct cores of
+    the affinity set (SMT siblings once)."""
+    from oracle.php_pool import physical_cores
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), model)
     except OSError:
         pass
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "threads_all": max(1, min(16, aff))}
+    cpus = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else set(range(os.cpu_count() or 1))
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(cpus),
+            "physical_cores_affinity": physical_cores(cpus), "threads_all": max(1, min(16, len(cpus)))}
 
 
-def cpu_baseline(line, keys_fn, seconds, what):
+def cpu_baseline(line, keys_fn, seconds, what, nc=NC):
     """The PHP CPU path: check_key_m22000(line, [key]) once per key (one PHP request per key, as put_work does,
     common.php:902), restated in C on OpenSSL (oracle/; PKCS5_PBKDF2_HMAC is the call openssl_pbkdf2 makes,
-    common.php:178-180,246-248).  Timed on the box's CPU share (threads_all) and on 1 thread (one PHP request),
-    over bounded samples of the workload's own candidates that end at the planted PSK, which both runs must find.
-    PHP nonce window nc=8 (21 attempts per EAPOL key)."""
+    common.php:178-180,246-248).  Timed as PHP-FPM serves requests -- min(16, affinity) single-threaded worker
+    processes (oracle/php_pool.py) -- and in one process (one PHP request), over bounded samples of the workload's
+    own candidates that end at the planted PSK, which both runs must find.  PHP nonce window nc=8 (21 attempts
+    per EAPOL key) unless the leg's jobs carry their own."""
     from oracle import oracle as O
+    from oracle.php_pool import PhpPool
     hc = host_cpu()
-    threads = hc["threads_all"]
-    probe = keys_fn(96 * threads)
-    O.c_check_many(line, probe[:threads], NC, threads)  # loads the oracle library and starts its threads
-    t0 = time.perf_counter()
-    O.c_check_many(line, probe, NC, threads)
-    rate = len(probe) / (time.perf_counter() - t0)
-    m = int(max(len(probe), min(400_000, rate * seconds)))
-    sample = keys_fn(m)
-    t0 = time.perf_counter()
-    idx, _ = O.c_check_many(line, sample, NC, threads)
-    dt = time.perf_counter() - t0
-    one = keys_fn(int(max(16, min(m, rate / threads * seconds / 3))))
+    P = hc["threads_all"]
+    pool = PhpPool(P)
+    try:
+        probe = keys_fn(64 * P)
+        pool.check_keys(line, probe, nc)  # first checks in each worker (OpenSSL's method caches, clocks)
+        _, dtp = pool.check_keys(line, probe, nc)
+        rate = len(probe) / dtp
+        m = int(max(len(probe), min(400_000, rate * seconds)))
+        sample = keys_fn(m)
+        idx, dt = pool.check_keys(line, sample, nc)
+    finally:
+        pool.close()
+    one = keys_fn(int(max(16, min(m, rate / P * seconds / 3))))
     t1 = time.perf_counter()
-    idx1, _ = O.c_check_many(line, one, NC, 1)
+    idx1, _ = O.c_check_many(line, one, nc, 1)
     dt1 = time.perf_counter() - t1
-    return dict({"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": threads, "kind": "port",
+    return dict({"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": P, "kind": "port",
+                 "workers": f"{P} single-threaded worker processes (PHP-FPM model, oracle/php_pool.py)",
                  "sample": f"{len(sample)} {what} ending at the planted PSK, check_key_m22000(line, [key], False, "
-                           f"{NC}) per key on {threads} threads, {dt:.1f} s",
+                           f"{nc}) per key, {dt:.1f} s",
                  "found_planted": idx == len(sample) - 1 and idx1 == len(one) - 1,
+                 "scaling_vs_one_process": round(len(sample) / dt / (len(one) / dt1), 2),
                  "one_thread": {"value": round(len(one) / dt1, 1), "unit": "PMK/s", "cores": 1,
-                                "sample": f"the last {len(one)} of them on 1 thread (one PHP request), {dt1:.1f} s"}},
+                                "sample": f"the last {len(one)} of them in one process (one PHP request), "
+                                          f"{dt1:.1f} s"}},
                 **hc)
 
 

@@ -17,6 +17,7 @@ DWPA_E_FORMAT, DWPA_E_HEX, DWPA_E_TYPE, DWPA_E_KEYVER = -1, -2, -3, -4
 DWPA_E_NODEV, DWPA_E_HIP, DWPA_E_ARG, DWPA_E_NOMEM, DWPA_E_IO, DWPA_E_OVERFLOW, DWPA_E_RULE = -10, -11, -12, -13, -14, -15, -16
 DWPA_RC_CRACKED, DWPA_RC_EXHAUSTED, DWPA_RC_ERROR = 0, 1, -1
 DWPA_NC_PHP, DWPA_NC_HASHCAT = 0, 1
+DWPA_DICT_OK, DWPA_DICT_DAMAGED = 0, 1  # dwpa_crack_files_ex per-dictionary status (or DWPA_E_IO)
 
 
 class DwpaError(RuntimeError):
@@ -74,6 +75,9 @@ SIGNATURES = {
     "dwpa_parse_m22000": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "dwpa_crack_files": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
                           ctypes.c_char_p, ctypes.POINTER(Config)], ctypes.c_int),
+    "dwpa_crack_files_ex": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p,
+                             ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_int32)],
+                            ctypes.c_int),
     "dwpa_rules_expand": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Bytes), ctypes.c_size_t, _P, _P,
                            ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "dwpa_scan_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,

@@ -8,6 +8,7 @@
 // hit of each hashline is written to the outfile and the line is retired on every device (hashcat reports each
 // hash once).  Rules (hashcat -r, help_crack.py:445-447,931-933) are applied on the GPU (rules.cpp).
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <string.h>
 #include <zlib.h>
@@ -226,15 +227,36 @@ static bool trace_on() {
     return e && *e == '1';
 }
 
+// A field of the caller's dwpa_config counts only if its struct_size covers it (an older, shorter struct leaves the
+// later fields at their documented defaults).  struct_size 0 = the full current struct.
+#define DWPA_CFG_HAS(cfg, field) \
+    ((cfg) && (!(cfg)->struct_size || (cfg)->struct_size >= offsetof(dwpa_config, field) + sizeof((cfg)->field)))
+
 static int crack_impl(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file, int nec,
-                      const char* out_file, const dwpa_config* cfg) {
+                      const char* out_file, const dwpa_config* cfg, int32_t* dict_status) {
+    if (dict_status)
+        for (size_t i = 0; i < ndicts; i++) dict_status[i] = DWPA_DICT_OK;
     if (!hash_file || !out_file || (!dicts && ndicts)) return DWPA_RC_ERROR;
-    if (cfg && cfg->struct_size && cfg->struct_size < sizeof(uint32_t) * 3) return DWPA_RC_ERROR;
+    if (cfg && cfg->struct_size && cfg->struct_size < offsetof(dwpa_config, batch)) return DWPA_RC_ERROR;
+    // hashcat refuses to start when a wordlist cannot be opened; so does this call, before touching a device, and it
+    // names the file (DWPA_E_IO in dict_status): a deterministic input error, which help_crack's drop-in does not retry
+    bool unreadable = false;
+    for (size_t i = 0; i < ndicts; i++) {
+        FILE* f = dicts[i] ? fopen(dicts[i], "rb") : nullptr;
+        if (!f) {
+            unreadable = true;
+            if (dict_status) dict_status[i] = DWPA_E_IO;
+            fprintf(stderr, "[dwpa] dictionary %s: cannot be opened\n", dicts[i] ? dicts[i] : "(null)");
+        } else {
+            fclose(f);
+        }
+    }
+    if (unreadable) return DWPA_RC_ERROR;
     // the config applies to this call only (dwpa_init's process-wide selection stays as it is)
     if (engine_init() < 0) return DWPA_RC_ERROR;
-    std::vector<int> devs = engine_devices(cfg ? cfg->device_mask : 0);
+    std::vector<int> devs = engine_devices(DWPA_CFG_HAS(cfg, device_mask) ? cfg->device_mask : 0);
     if (devs.empty()) return DWPA_RC_ERROR;
-    const int nc_mode = cfg ? cfg->nc_mode : DWPA_NC_HASHCAT;
+    const int nc_mode = DWPA_CFG_HAS(cfg, nc_mode) ? cfg->nc_mode : DWPA_NC_HASHCAT;
 
     // hash file
     std::vector<std::string> lines;
@@ -279,7 +301,7 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     std::vector<const char*> lp(lines.size());
     std::vector<size_t> ll(lines.size());
     for (size_t i = 0; i < lines.size(); i++) { lp[i] = lines[i].data(); ll[i] = lines[i].size(); }
-    const uint32_t batch = cfg && cfg->batch ? cfg->batch : engine_batch();
+    const uint32_t batch = DWPA_CFG_HAS(cfg, batch) && cfg->batch ? cfg->batch : engine_batch();
     const size_t spd = shards_per_device();
     std::vector<std::unique_ptr<DevWork>> work;
     int rc = 0;
@@ -388,8 +410,19 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
             });
         }
     for (auto& t : th) t.join();
-    source.cancel();
+    source.finish();
     const bool ioerr = items.io_error();
+    const std::vector<int> fst = source.file_status();
+    for (size_t i = 0; i < ndicts; i++) {
+        if (fst[i] == ChunkSource::FILE_DAMAGED)
+            fprintf(stderr, "[dwpa] dictionary %s: damaged gzip stream (truncated or corrupt); scanned up to the damage, "
+                            "as hashcat's gzread does\n", dicts[i]);
+        else if (fst[i] == ChunkSource::FILE_UNREADABLE)
+            fprintf(stderr, "[dwpa] dictionary %s: read error\n", dicts[i]);
+        if (dict_status)
+            dict_status[i] = fst[i] == ChunkSource::FILE_DAMAGED ? DWPA_DICT_DAMAGED
+                             : fst[i] == ChunkSource::FILE_UNREADABLE ? DWPA_E_IO : DWPA_DICT_OK;
+    }
     if (trace_on()) {
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         fprintf(stderr, "[dwpa] crack dictionary cache: %zu files replayed from memory so far\n", DictCache::get().hits());
@@ -421,7 +454,13 @@ extern "C" {
 
 int dwpa_crack_files(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,
                      int nonce_error_corrections, const char* out_file, const dwpa_config* cfg) {
-    return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg);
+    return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg, nullptr);
+}
+
+int dwpa_crack_files_ex(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,
+                        int nonce_error_corrections, const char* out_file, const dwpa_config* cfg,
+                        int32_t* dict_status) {
+    return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg, dict_status);
 }
 
 // md5 over fields 1..7 of the hashline (web/common.php:310-315); a tiny host MD5 keeps this dependency-free.

@@ -44,7 +44,8 @@ class BlockInflater {
         std::vector<uint8_t> buf;  // [0, WIN): history for back-references; text at [begin, end)
         size_t begin = 0, end = 0;
         bool file_end = false;
-        bool err = false;
+        bool err = false;      // the file could not be read (I/O error): the call fails
+        bool damaged = false;  // on the file's last block: corrupt or truncated gzip, delivered up to the damage
         const char* data() const { return (const char*)buf.data() + begin; }
         size_t size() const { return end - begin; }
     };
@@ -72,6 +73,11 @@ class BlockInflater {
         q_.pop_front();
         cv_.notify_all();
         return true;
+    }
+    // Every file was delivered to its end (no cancel, no I/O error); valid once next() has returned false.
+    bool complete() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return done_ && complete_ && q_.empty();
     }
 
   private:
@@ -115,13 +121,22 @@ class BlockInflater {
             ok = file_zlib(fd);
         } else if (gz) {
             GzipDecoder dec(fd);
+            uint64_t delivered = 0;
             for (bool end = false; ok && !end && !cancelled();) {
                 Block b = fresh();
                 b.end = b.begin + dec.read(b.buf.data(), BLOCK);
-                b.err = dec.failed();
-                end = dec.done() || b.err;
+                if (dec.failed()) {
+                    // A damaged stream (truncated download, CRC error, bad code): deliver exactly what gzread
+                    // would -- zlib decodes the file again from the start, the bytes this decoder already delivered
+                    // are skipped, and what zlib yields up to the damage follows.  hashcat reads wordlists
+                    // through gzread, scans that prefix and finishes normally (rc 0/1).
+                    ok = file_zlib(fd, delivered, dec.error());
+                    break;
+                }
+                delivered += b.size();
+                end = dec.done();
                 b.file_end = end;
-                ok = push(std::move(b)) && !dec.failed();
+                ok = push(std::move(b));
             }
         } else {
             for (bool end = false; ok && !end && !cancelled();) {
@@ -140,30 +155,56 @@ class BlockInflater {
         close(fd);
         return ok;
     }
-    bool file_zlib(int fd) {
+    // gzread over the whole file (DWPA_INFLATE=zlib), or over its rest after GzipDecoder failed (`skip` bytes
+    // already delivered, `why` = the decoder's error).  gzread returns the data before a cut and then 0 (error
+    // Z_BUF_ERROR), or -1 at a data error; either way the file's last block is marked damaged.
+    bool file_zlib(int fd, uint64_t skip = 0, const char* why = nullptr) {
+        if (lseek(fd, 0, SEEK_SET) != 0) return error_block();
         gzFile gz = gzdopen(dup(fd), "rb");
         if (!gz) return error_block();
         gzbuffer(gz, 1 << 20);
-        bool ok = true, eof = false;
-        while (ok && !eof && !cancelled()) {
+        bool ok = true, eof = false, damaged = false;
+        std::vector<uint8_t> scratch;
+        while (skip && !damaged) {  // the prefix GzipDecoder delivered (byte-identical to zlib's output)
+            scratch.resize((size_t)std::min<uint64_t>(skip, 1u << 20));
+            const int r = gzread(gz, scratch.data(), (unsigned)scratch.size());
+            if (r <= 0) damaged = true;
+            else skip -= (uint64_t)r;
+        }
+        if (damaged) {  // zlib failed inside the prefix already: close the file
+            Block b = fresh();
+            b.file_end = b.damaged = true;
+            ok = push(std::move(b));
+        }
+        while (ok && !eof && !damaged && !cancelled()) {
             Block b = fresh();
             while (b.end < b.begin + BLOCK) {
                 const int r = gzread(gz, b.buf.data() + b.end, (unsigned)(b.begin + BLOCK - b.end));
-                if (r < 0) { b.err = true; break; }
+                if (r < 0) { damaged = true; break; }
                 if (r == 0) { eof = true; break; }
                 b.end += (size_t)r;
             }
-            b.file_end = eof || b.err;
-            const bool err = b.err;
-            ok = push(std::move(b)) && !err;
+            if (eof) {
+                int zerr = Z_OK;
+                gzerror(gz, &zerr);
+                damaged = zerr == Z_BUF_ERROR || why != nullptr;  // truncated: gzread delivered what it could
+            }
+            b.file_end = eof || damaged;
+            b.damaged = damaged;
+            ok = push(std::move(b));
         }
         gzclose(gz);
         return ok;
     }
     void run() {
+        bool all = true;
         for (const std::string& path : paths_)
-            if (!file(path) || cancelled()) break;
+            if (!file(path) || cancelled()) {
+                all = false;
+                break;
+            }
         std::lock_guard<std::mutex> lk(mu_);
+        complete_ = all && !cancelled();
         done_ = true;
         cv_.notify_all();
     }
@@ -175,7 +216,7 @@ class BlockInflater {
     std::condition_variable cv_;
     std::deque<Block> q_;
     std::vector<std::vector<uint8_t>> free_;
-    bool stop_ = false, done_ = false;
+    bool stop_ = false, done_ = false, complete_ = false;
 };
 
 // Dictionary reader: plain or gzip (zlib reads both), one word per line, "\n" or "\r\n", $HEX[] decoded.  Lines
@@ -197,9 +238,13 @@ class DictReader {
                     if (!partial_.empty()) emit(c, partial_.data(), partial_.size());
                     partial_.clear();
                     blk_.file_end = false;
+                    damaged_ = damaged_ || blk_.damaged;
                     continue;
                 }
-                if (!src_.next(blk_)) break;
+                if (!src_.next(blk_)) {
+                    finished_ = true;
+                    break;
+                }
                 if (blk_.err) { err = true; return false; }
                 pos_ = 0;
                 continue;
@@ -227,6 +272,10 @@ class DictReader {
         }
         return c.words() > 0;
     }
+    // A file of this reader was damaged (delivered up to the damage, as gzread does).
+    bool damaged() const { return damaged_; }
+    // The reader reached the end of every file: nothing was cut short by a cancel or an error.
+    bool complete() { return finished_ && src_.complete(); }
 
   private:
     static void emit(Chunk& c, const char* p, size_t k) {
@@ -239,6 +288,7 @@ class DictReader {
     BlockInflater::Block blk_;
     size_t pos_ = 0;
     std::string partial_;
+    bool damaged_ = false, finished_ = false;
 };
 
 // Decoded dictionaries kept in host memory between dwpa_crack_files calls of one process.  help_crack downloads a
@@ -261,9 +311,22 @@ class DictCache {
         return path + '\0' + std::to_string((long long)st.st_size) + ':' + std::to_string((long long)st.st_mtim.tv_sec) +
                '.' + std::to_string((long long)st.st_mtim.tv_nsec) + ':' + std::to_string((unsigned long long)st.st_ino);
     }
-    std::shared_ptr<const Chunks> find(const std::string& k) {
+    // The cached decode of `path` under its current key k.  Entries of the same path under another key (the file
+    // was downloaded again: new size, mtime or inode) are dropped here, so a re-fetched cracked.txt.gz does not
+    // leave its old decode behind until LRU eviction.
+    std::shared_ptr<const Chunks> find(const std::string& path, const std::string& k) {
         if (k.empty()) return nullptr;
         std::lock_guard<std::mutex> lk(mu_);
+        const std::string prefix = path + '\0';
+        for (auto it = map_.lower_bound(prefix); it != map_.end() && it->first.compare(0, prefix.size(), prefix) == 0;) {
+            if (it->first == k) {
+                ++it;
+                continue;
+            }
+            total_ -= it->second.bytes;
+            lru_.erase(it->second.pos);
+            it = map_.erase(it);
+        }
         auto it = map_.find(k);
         if (it == map_.end()) return nullptr;
         lru_.splice(lru_.begin(), lru_, it->second.pos);
@@ -286,13 +349,22 @@ class DictCache {
         map_[k] = Entry{std::move(chunks), bytes, lru_.begin()};
         total_ += bytes;
     }
+    size_t budget() const { return budget_; }
     bool can_hold(size_t bytes) const { return bytes <= budget_; }
     size_t hits() const { return hits_.load(); }
 
   private:
+    // Budget: DWPA_DICT_CACHE_MB, else min(4 GiB, a quarter of the memory available when the library first reads
+    // a dictionary) -- a volunteer's help_crack process keeps this much host RAM between work units at most.
     DictCache() {
         const char* e = getenv("DWPA_DICT_CACHE_MB");
-        budget_ = (size_t)(e && *e ? atoll(e) : 4096) << 20;
+        if (e && *e) {
+            budget_ = (size_t)atoll(e) << 20;
+        } else {
+            const long pages = sysconf(_SC_AVPHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+            const size_t avail = pages > 0 && psz > 0 ? (size_t)pages * (size_t)psz : 0;
+            budget_ = std::min<size_t>((size_t)4096 << 20, avail / 4);
+        }
     }
     struct Entry {
         std::shared_ptr<const Chunks> chunks;
@@ -313,28 +385,42 @@ class DictCache {
 // outfile is the same as hashcat's.
 class ChunkSource {
   public:
-    ChunkSource(const std::vector<std::string>& paths, size_t first_words, size_t max_words) {
+    ChunkSource(const std::vector<std::string>& paths, size_t first_words, size_t max_words)
+        : status_(paths.size(), FILE_OK) {
         const size_t T = std::max<size_t>(1, std::min<size_t>(paths.size(), 4));
         cap_ = T + 1;
         live_ = T;
         for (size_t t = 0; t < T; t++) {
-            std::vector<std::string> mine;
-            for (size_t i = t; i < paths.size(); i += T) mine.push_back(paths[i]);
-            workers_.emplace_back([this, mine, first_words, max_words, T] { work(mine, first_words, std::max<size_t>(first_words, max_words / T)); });
+            std::vector<size_t> mine;
+            for (size_t i = t; i < paths.size(); i += T) mine.push_back(i);
+            workers_.emplace_back([this, paths, mine, first_words, max_words, T] {
+                work(paths, mine, first_words, std::max<size_t>(first_words, max_words / T));
+            });
         }
     }
-    ~ChunkSource() {
-        cancel();
-        for (auto& w : workers_) w.join();
-    }
-    // Stops the readers (within one 64 KiB read) and makes next() return false.
+    ~ChunkSource() { finish(); }
+    // Stops the readers (within one 64 KiB read) and makes next() return false.  cancel_ is raised before stop_:
+    // a reader whose push() sees stop_ then also sees cancel_, so it never takes a cut-short file as complete.
     void cancel() {
+        cancel_ = true;
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
         }
-        cancel_ = true;
         cv_.notify_all();
+    }
+    // cancel() and wait for the reader threads; file_status() is final afterwards.
+    void finish() {
+        cancel();
+        for (auto& w : workers_)
+            if (w.joinable()) w.join();
+    }
+    enum { FILE_OK = 0, FILE_DAMAGED = 1, FILE_UNREADABLE = 2 };
+    // Per input path: FILE_OK (read, or never reached), FILE_DAMAGED (corrupt or truncated gzip, delivered up to the
+    // damage as gzread does) or FILE_UNREADABLE (open/read error: the call fails).
+    std::vector<int> file_status() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return status_;
     }
     // Blocks until a chunk is ready; false once every file is read (or on an I/O error: err is set).
     bool next(std::shared_ptr<const Chunk>& c, bool& err) {
@@ -363,13 +449,15 @@ class ChunkSource {
         cv_.notify_all();
         return true;
     }
-    void work(const std::vector<std::string>& paths, size_t words, size_t max_words) {
+    void work(const std::vector<std::string>& paths, const std::vector<size_t>& mine, size_t words,
+              size_t max_words) {
         DictCache& cache = DictCache::get();
         bool err = false;
-        for (const std::string& path : paths) {
+        for (const size_t fi : mine) {
+            const std::string& path = paths[fi];
             if (cancel_.load() || err) break;
             const std::string key = cache.key(path);
-            if (auto hit = cache.find(key)) {  // decoded before: replay from memory
+            if (auto hit = cache.find(path, key)) {  // decoded before: replay from memory
                 for (const auto& c : *hit)
                     if (!push(c)) break;
                 continue;
@@ -391,7 +479,14 @@ class ChunkSource {
                 }
                 if (!push(std::move(c))) break;
             }
-            if (whole && !err && !cancel_.load()) cache.put(key, std::move(keep));  // read to its end
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (err) status_[fi] = FILE_UNREADABLE;
+                else if (reader.damaged()) status_[fi] = FILE_DAMAGED;
+            }
+            // cached only when read to its very end, undamaged (a replay must be the whole dictionary)
+            if (whole && !err && !reader.damaged() && reader.complete() && !cancel_.load())
+                cache.put(key, std::move(keep));
         }
         std::lock_guard<std::mutex> lk(mu_);
         err_ = err_ || err;
@@ -403,6 +498,7 @@ class ChunkSource {
     std::deque<std::shared_ptr<const Chunk>> q_;
     size_t cap_ = 2, live_ = 0;
     bool stop_ = false, err_ = false;
+    std::vector<int> status_;
     std::atomic<bool> cancel_{false};
     std::vector<std::thread> workers_;
 };

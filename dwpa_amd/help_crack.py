@@ -7,8 +7,9 @@ expansions (:508, :575) with the same inputs, outputs and return codes:
               ``conf["rules"]`` ("" or "-S -r <file>", :445-447 / :931-933), ``conf["key_file"]``, the dictionary
               list (plain or .gz), ``conf["coptions"]`` (``-d 1,2`` selects devices like hashcat's ``-d``);
 * output   -- the ``-o`` key file in hashcat's m22000 outfile format, parsed unchanged by ``get_key`` (:804-879);
-* rc       -- hashcat semantics: 0 all cracked, 1 exhausted (drives the second pass at :930); errors are
-              retried after ``sleepy()`` as the reference's loop does (:776-786), never returned.
+* rc       -- hashcat semantics: 0 all cracked, 1 exhausted (drives the second pass at :930); device errors are
+              retried after ``sleepy()`` as the reference's loop does (:776-786), never returned; dictionary
+              errors are not retried (see run_cracker).
 
 Usage from help_crack.py (the one-line change INTEGRATION.md shows)::
 
@@ -57,27 +58,65 @@ def _sleepy(sec: int = 123) -> None:
     time.sleep(sec)
 
 
+def _truncate(path: str, size) -> None:
+    """Undo what a failed attempt appended to the key file (size None: the file did not exist)."""
+    if size is None:
+        if os.path.exists(path):
+            os.unlink(path)
+    elif os.path.exists(path) and os.path.getsize(path) > size:
+        with open(path, "r+b") as f:
+            f.truncate(size)
+
+
 def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR_CORRECTIONS, sleepy=None,
                 pprint=None, max_tries: int | None = None) -> int:
     """In-process equivalent of the hashcat command line at help_crack.py:773 with the reference's retry loop
-    (:776-786): a failed attempt (library, GPU or I/O error -- hashcat's -1 / >= 2) is logged, followed by
-    ``sleepy()`` and retried, so only 0 (all cracked) or 1 (exhausted) ever reaches run(): returning -1 there
-    would skip the rules pass (:930) and let put_work report an unsearched work unit as searched.
+    (:776-786): a failed attempt (library or GPU error -- hashcat's -1 / >= 2) is logged, followed by ``sleepy()``
+    and retried, so only 0 (all cracked) or 1 (exhausted) ever reaches run(): returning -1 there would skip the
+    rules pass (:930) and let put_work report an unsearched work unit as searched.  What a failed attempt appended
+    to the key file is removed before the retry, so no hit is written twice.
+
+    Dictionary errors are deterministic and are not retried:
+
+    * a damaged gzip dictionary (truncated download, corrupt stream) is scanned up to the damage, exactly as
+      hashcat's gzread reads it, and the call returns 0/1 like hashcat; the file is then deleted so that the next
+      prepare_dicts (:520-552, which downloads only missing files and merely warns on an MD5 mismatch) fetches it
+      again -- except the user's own ``conf["additional"]`` dictionary (-ad, :661-663), which is only reported;
+    * a dictionary that cannot be opened makes the library fail before any device work; that raises DwpaError
+      (DWPA_E_IO) at once instead of looping forever on the same work unit.
 
     ``sleepy``/``pprint`` are the HelpCrack methods when bound from help_crack.py.  ``max_tries`` (None = retry
-    forever, as the reference does) ends the loop with a DwpaError instead of a return value.  A missing hash
-    file raises FileNotFoundError (the reference would fail on an unbound ``rc``)."""
+    forever, as the reference does) ends the device-error loop with a DwpaError instead of a return value.  A
+    missing hash file raises FileNotFoundError (the reference would fail on an unbound ``rc``)."""
     if not os.path.exists(conf["hash_file"]):
         raise FileNotFoundError(conf["hash_file"])
     sleepy = sleepy or _sleepy
     pprint = pprint or (lambda mess, code="HEADER": print(mess, file=sys.stderr))
     rules_file, mask = _parse_options(conf.get("rules", ""), conf.get("coptions", ""))
+    key_file = conf["key_file"]
+    dictlist = list(dictlist)
     tries = 0
     while True:
-        rc = M.crack_files(conf["hash_file"], list(dictlist), rules_file, nonce_error_corrections,
-                           conf["key_file"], device_mask=mask)
+        size0 = os.path.getsize(key_file) if os.path.exists(key_file) else None
+        rc, status = M.crack_files_ex(conf["hash_file"], dictlist, rules_file, nonce_error_corrections, key_file,
+                                      device_mask=mask)
+        for d, st in zip(dictlist, status):
+            if st != L.DWPA_DICT_DAMAGED:
+                continue
+            if d == conf.get("additional"):
+                pprint(f"Dictionary {d} is damaged (truncated or corrupt gzip); scanned up to the damage", "WARNING")
+            else:
+                pprint(f"Dictionary {d} is damaged (truncated or corrupt gzip); scanned up to the damage, "
+                       "removed so that it is downloaded again", "WARNING")
+                if os.path.exists(d):
+                    os.unlink(d)
         if rc in (L.DWPA_RC_CRACKED, L.DWPA_RC_EXHAUSTED):
             return rc
+        _truncate(key_file, size0)
+        unreadable = [d for d, st in zip(dictlist, status) if st == L.DWPA_E_IO]
+        if unreadable:
+            pprint(f"Dictionary cannot be read: {', '.join(unreadable)}", "FAIL")
+            raise L.DwpaError(L.DWPA_E_IO, f"dictionary cannot be read: {', '.join(unreadable)}")
         tries += 1
         pprint(f"libdwpa22000 crack_files failed with code {rc}", "FAIL")
         if max_tries is not None and tries >= max_tries:

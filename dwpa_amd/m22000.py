@@ -181,11 +181,20 @@ def rules_expand(rules_text, words, device: int = 0):
 def crack_files(hash_file, dicts, rules_file=None, nonce_error_corrections: int = 8, out_file="help_crack.key",
                 device_mask: int = 0, batch: int = 0, nc_mode: int = L.DWPA_NC_HASHCAT) -> int:
     """In-process hashcat -m22000 replacement; returns a hashcat exit code (0 cracked, 1 exhausted, -1 error)."""
+    return crack_files_ex(hash_file, dicts, rules_file, nonce_error_corrections, out_file, device_mask, batch,
+                          nc_mode)[0]
+
+
+def crack_files_ex(hash_file, dicts, rules_file=None, nonce_error_corrections: int = 8, out_file="help_crack.key",
+                   device_mask: int = 0, batch: int = 0, nc_mode: int = L.DWPA_NC_HASHCAT):
+    """crack_files plus one status per dictionary: (rc, [DWPA_DICT_OK | DWPA_DICT_DAMAGED | DWPA_E_IO])."""
     cfg = L.Config(ctypes.sizeof(L.Config), device_mask, batch, nc_mode)
     dl = [_b(d) for d in dicts]
     darr = (ctypes.c_char_p * max(1, len(dl)))(*dl)
-    return L.load().dwpa_crack_files(_b(hash_file), darr, len(dl), _b(rules_file) if rules_file else None,
-                                     int(nonce_error_corrections), _b(out_file), ctypes.byref(cfg))
+    st = (ctypes.c_int32 * max(1, len(dl)))()
+    rc = L.load().dwpa_crack_files_ex(_b(hash_file), darr, len(dl), _b(rules_file) if rules_file else None,
+                                      int(nonce_error_corrections), _b(out_file), ctypes.byref(cfg), st)
+    return rc, [int(st[i]) for i in range(len(dl))]
 
 
 class Scan:

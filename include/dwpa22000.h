@@ -148,11 +148,24 @@ int dwpa_hash_m22000(const char *line, size_t line_len, uint8_t out[16]);
  * decoded), applies rules_file (hashcat rule syntax, may be NULL) and writes one outfile record per cracked line:
  *   <PMKID|MIC hex>:<MAC_AP hex>:<MAC_STA hex>:<ESSID>:<PSK>   (ESSID/PSK as $HEX[..] when not printable)
  * Returns a hashcat exit code (DWPA_RC_*).  nonce_error_corrections as --nonce-error-corrections.  cfg (nullable):
- * device_mask / batch / nc_mode for this call only (device_mask 0 = the dwpa_init selection, default all devices).
+ * device_mask / batch / nc_mode for this call only (device_mask 0 = the dwpa_init selection, default all devices);
+ * a field beyond cfg->struct_size keeps its default (0 = the whole current struct).
  * Lines that can never match (PMKID or MIC shorter than 16 bytes, which hashcat does not load) do not count
  * towards "every hashline cracked".  DWPA_CRACK_SHARDS_PER_DEVICE=k runs k shard workers per device. */
 int dwpa_crack_files(const char *hash_file, const char *const *dicts, size_t ndicts, const char *rules_file,
                      int nonce_error_corrections, const char *out_file, const dwpa_config *cfg);
+/* dwpa_crack_files plus one outcome per dictionary (dict_status[ndicts], nullable):
+ *   DWPA_DICT_OK       read to its end (or not needed: every line cracked first)
+ *   DWPA_DICT_DAMAGED  corrupt or truncated gzip stream: scanned up to the damage, exactly the bytes zlib's gzread
+ *                      delivers (hashcat reads wordlists through gzread), and the call still returns 0/1; the file
+ *                      should be fetched again (help_crack.py:530-534 only downloads a missing file)
+ *   DWPA_E_IO          cannot be opened or read: the call returns DWPA_RC_ERROR (before any device work when the
+ *                      file cannot be opened, as hashcat refuses to start) */
+#define DWPA_DICT_OK 0
+#define DWPA_DICT_DAMAGED 1
+int dwpa_crack_files_ex(const char *hash_file, const char *const *dicts, size_t ndicts, const char *rules_file,
+                        int nonce_error_corrections, const char *out_file, const dwpa_config *cfg,
+                        int32_t *dict_status);
 
 /* GPU rule application (replaces `hashcat --stdout -r rules words`, help_crack.py:508,575): out holds
  * nwords*nrules candidates of 256 bytes (word-major), out_len their lengths (0xFFFFFFFF = input rejected).

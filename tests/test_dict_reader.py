@@ -55,6 +55,20 @@ def test_reader_words_match(tmp_path):
     assert got == exp
 
 
+def _parse_passes(stdout):
+    """inflate_bench --passes output -> ([[cache_hits, words]] per pass, [file statuses] per pass)."""
+    out, status, cur = [], [], None
+    for line in stdout.decode().split("\n")[:-1]:
+        if line.startswith("#pass"):
+            cur = [int(line.split()[3]), []]
+            out.append(cur)
+        elif line.startswith("#status"):
+            status.append([int(x) for x in line.split()[1:]])
+        else:
+            cur[1].append(bytes.fromhex(line))
+    return out, status
+
+
 def test_reader_cache_replays_same_words(tmp_path):
     """crack_files' ChunkSource keeps each dictionary it read to the end in the process-wide DictCache
     (dict_reader.hpp) and replays it on the next work unit: the second and third passes over the same files yield
@@ -74,14 +88,7 @@ def test_reader_cache_replays_same_words(tmp_path):
     def passes(k, env=None):
         r = subprocess.run([TOOL, "--passes", str(k)] + [p for p, _ in files], capture_output=True, check=True,
                            env=env)
-        out, cur = [], None
-        for line in r.stdout.decode().split("\n")[:-1]:
-            if line.startswith("#pass"):
-                cur = [int(line.split()[3]), []]
-                out.append(cur)
-            else:
-                cur[1].append(bytes.fromhex(line))
-        return out
+        return _parse_passes(r.stdout)[0]
 
     exp = sorted(_expected([d for _, d in files]))
     got = passes(3)
@@ -90,3 +97,43 @@ def test_reader_cache_replays_same_words(tmp_path):
         assert sorted(words) == exp
     off = passes(2, env=dict(os.environ, DWPA_DICT_CACHE_MB="0"))
     assert [h for h, _ in off] == [0, 0] and all(sorted(w) == exp for _, w in off)
+
+
+def test_damaged_gzip_scanned_to_the_damage_like_gzread(tmp_path):
+    """a cut download must not fail the work unit forever.  hashcat reads wordlists through
+    zlib's gzread, which delivers every byte decodable before the cut and then reports end of file; the crack
+    path's reader (ChunkSource, the same code dwpa_crack_files runs) now yields exactly those words, flags the file
+    as damaged (status 1) and keeps going with the next file; a damaged file is never cached, and an intact file
+    next to it still is.  A CRC-corrupted trailer (a data error): gzread drops the read the error lands in, so the
+    words are a prefix of the file's, and the file is damaged.  A cut inside the first 4 MiB block and one
+    far past it (the reader's own decoder hands over to zlib at the failing block)."""
+    import zlib
+    subprocess.run(["make", "-s", "-C", ROOT, "tools/bin/inflate_bench"], check=True)
+    rng = random.Random(63)
+    words = [bytes(rng.choice(b"abcdefghijklmnopqrstuvwxyz0123456789") for _ in range(rng.randint(4, 24)))
+             for _ in range(900_000)]
+    data = b"\n".join(words) + b"\n"
+    full = gzip.compress(data, compresslevel=6)
+    good_words = [b"intact-%d" % i for i in range(1000)]
+    good = tmp_path / "good.txt.gz"
+    good.write_bytes(gzip.compress(b"\n".join(good_words) + b"\n"))
+    cases = {"cut_early": full[:len(full) // 7], "cut_late": full[:len(full) - 5000],
+             "bad_crc": full[:-8] + bytes([full[-8] ^ 0xFF]) + full[-7:]}
+    for name, blob in cases.items():
+        bad = tmp_path / (name + ".txt.gz")
+        bad.write_bytes(blob)
+        r = subprocess.run([TOOL, "--passes", "2", str(bad), str(good)], capture_output=True, check=True)
+        passes, status = _parse_passes(r.stdout)
+        assert status == [[1, 0], [1, 0]], name
+        assert [h for h, _ in passes] == [0, 1], name  # only the intact file is replayed from the cache
+        for _, got in passes:
+            mine = [w for w in got if not w.startswith(b"intact-")]
+            assert sorted(w for w in got if w.startswith(b"intact-")) == sorted(good_words)
+            if name == "bad_crc":
+                # a data error loses gzread's failing read: a prefix of the words (the last one may be cut)
+                assert 0 < len(mine) < len(words), name
+                assert mine[:-1] == words[:len(mine) - 1] and words[len(mine) - 1].startswith(mine[-1])
+            else:
+                exp_text = zlib.decompressobj(31).decompress(blob)  # everything inflate yields before the cut
+                assert 0 < len(exp_text) < len(data)
+                assert mine == _expected([exp_text]), name

@@ -355,6 +355,35 @@ def test_help_crack_two_pass_flow(tmp_path):
         run_cracker(conf, [str(d)])
 
 
+def test_help_crack_truncated_dictionary_no_livelock(tmp_path):
+    """a cut .gz download.  run_cracker with max_tries=None (the reference's forever loop) and
+    a sleepy() that fails the test: one attempt scans the words before the cut (a PSK there is found and written
+    once), returns 1 like hashcat over gzread, and deletes the damaged file so prepare_dicts downloads it again.
+    A PSK after the cut is not found."""
+    from dwpa_amd.help_crack import run_cracker
+    rng = random.Random(41)
+    alnum = b"abcdefghijklmnopqrstuvwxyz0123456789"
+    words = [bytes(rng.choice(alnum) for _ in range(rng.randint(8, 14))) for _ in range(300_000)]
+    nets = [S.random_net(rng) for _ in range(3)]
+    before, after = words[5000], words[290_000]
+    lines = [S.pmkid_line(before, nets[0][0], nets[0][1], nets[0][2]),
+             S.eapol_line(after, nets[1][0], nets[1][1], nets[1][2], nets[1][3], nets[1][4], 2, 2, "BE", rng=rng),
+             S.pmkid_line(b"never-in-the-dictionary", nets[2][0], nets[2][1], nets[2][2])]
+    conf = {"hash_file": str(tmp_path / "help_crack.hash"), "key_file": str(tmp_path / "help_crack.key"),
+            "rules": "", "coptions": ""}
+    (tmp_path / "help_crack.hash").write_bytes(b"\n".join(lines) + b"\n")
+    blob = gzip.compress(b"\n".join(words) + b"\n", compresslevel=6)
+    d = tmp_path / "cut.txt.gz"
+    d.write_bytes(blob[:len(blob) * 2 // 3])
+
+    def no_sleep():
+        raise AssertionError("run_cracker retried a deterministic dictionary error")
+    assert run_cracker(conf, [str(d)], sleepy=no_sleep, pprint=lambda *a: None, max_tries=None) == 1
+    assert not d.exists()
+    assert _get_key(conf["key_file"]) == {nets[0][1].hex(): before.hex()}
+    assert open(conf["key_file"], "rb").read().count(b"\n") == 1
+
+
 def test_help_crack_expand_rules_file(tmp_path):
     """`hashcat --stdout -r bestWPA.rule source.txt` (help_crack.py:508) via the GPU rule engine: the gz output
     equals the rule oracle's expansion with rejected candidates skipped (parity with hashcat itself unpinned)."""

@@ -4,6 +4,8 @@
 //
 //   inflate_bench FILE.gz [FILE2.gz ...]
 //   inflate_bench --dump FILE... prints every word the reader yields, hex-encoded, one per line (tests/test_dict_reader.py)
+//   inflate_bench --passes K FILE... reads the files K times through ChunkSource (the crack path, DictCache included):
+//   per pass "#pass k cache_hits n", "#status s0 s1 ..." (per file: 0 ok, 1 damaged gzip, 2 unreadable), the words
 //   inflate_bench --passes K FILE... runs crack_files' ChunkSource K times over the files in one process (the second
 //     pass onwards replays the DictCache) and prints "#pass i cache_hits h" then that pass's words, hex-encoded
 //
@@ -50,8 +52,11 @@ int main(int argc, char** argv) {
             bool err = false;
             std::vector<std::shared_ptr<const dwpa::Chunk>> got;
             while (src.next(c, err)) got.push_back(c);
+            src.finish();
             if (err) return 1;
-            printf("#pass %d cache_hits %zu\n", pass, dwpa::DictCache::get().hits());
+            printf("#pass %d cache_hits %zu\n#status", pass, dwpa::DictCache::get().hits());
+            for (int st : src.file_status()) printf(" %d", st);  // ChunkSource::FILE_OK / _DAMAGED / _UNREADABLE
+            printf("\n");
             for (const auto& ch : got)
                 for (size_t i = 0; i < ch->words(); i++) {
                     hex_line(*ch, i, line);
