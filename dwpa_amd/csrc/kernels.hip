@@ -403,25 +403,21 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
     }
 }
 
-// Te0..Te3 (crypto_dev.hpp aes128_encrypt_te4) into the workgroup's LDS, for kernels that verify keyver 3.
-constexpr uint32_t AES_LDS_WORDS = 1024 * AES_SLICES;
+// The AES table image (crypto_dev.hpp: lane-sliced Te0, or Te0..Te3) into the workgroup's LDS, for kernels that
+// verify keyver 3; returns this lane's copy.
 template <uint32_t VC>
 __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     if constexpr ((VC & VC_KV3) != 0) {
-        for (uint32_t k = threadIdx.x; k < AES_LDS_WORDS; k += blockDim.x) {
-            const uint32_t t = k / (256 * AES_SLICES), x = k / AES_SLICES & 255;  // table t, entry x, copy k % S
-            te[k] = rotr(AES_TABLES.te0[x], 8 * t);
-        }
+        for (uint32_t k = threadIdx.x; k < AES_LDS_WORDS; k += blockDim.x) te[k] = aes_lds_word(k);
         __syncthreads();
     }
     return te + threadIdx.x % AES_SLICES;
 }
-// keyver-3 kernels with sliced AES tables (64 KiB of LDS at S = 16, an A/B build) run 512-thread workgroups: two per
-// CU, 4 waves per SIMD; the default plain tables keep 256-thread workgroups, which also fit beside a concurrent
-// call's PBKDF2 head.  (An earlier single lane-sliced Te0 with 1024-thread workgroups measured level,
-// profiles/r02/c5_sched/aes_sliced_ab.)
+// keyver-3 kernels with the four-table layout sliced (DWPA_KV3_AES=0, DWPA_KV3_SLICES > 1: 64 KiB of LDS at S = 16,
+// an A/B build) run 512-thread workgroups: two per CU, 4 waves per SIMD; the lane-sliced Te0 (32 KiB) and the plain
+// tables keep 256-thread workgroups, which also fit beside a concurrent call's PBKDF2 head.
 #ifndef DWPA_KV3_BLOCK
-#define DWPA_KV3_BLOCK (AES_SLICES > 1 ? 512 : 256)
+#define DWPA_KV3_BLOCK (DWPA_KV3_AES == 0 && AES_SLICES > 1 ? 512 : 256)
 #endif
 constexpr uint32_t vc_block(uint32_t vc) { return (vc & VC_KV3) ? DWPA_KV3_BLOCK : 256; }
 
