@@ -80,14 +80,23 @@ class PhpPool:
         return first, dt
 
     def job_pmks(self, jobs, budget_s: float):
-        """check_key_m22000 per job until `budget_s` elapses (whole rounds of `workers` jobs); returns
-        (jobs done, PMKs derived, seconds)."""
-        done = nk = 0
+        """check_key_m22000 per job, one job per free worker as PHP-FPM hands requests out, until `budget_s`
+        elapses (then the jobs in flight finish); returns (jobs done, PMKs derived, seconds).  Two jobs per worker
+        stay queued so no worker idles between jobs of different lengths."""
+        from concurrent.futures import FIRST_COMPLETED, wait
+        done = nk = nxt = 0
+        pending = set()
         t0 = time.perf_counter()
-        while done < len(jobs) and time.perf_counter() - t0 < budget_s:
-            chunk = jobs[done:done + 4 * self.workers]
-            nk += sum(self.ex.map(_job_pmks, chunk))
-            done += len(chunk)
+        while True:
+            while nxt < len(jobs) and len(pending) < 2 * self.workers and time.perf_counter() - t0 < budget_s:
+                pending.add(self.ex.submit(_job_pmks, jobs[nxt]))
+                nxt += 1
+            if not pending:
+                break
+            fin, pending = wait(pending, return_when=FIRST_COMPLETED)
+            for f in fin:
+                nk += f.result()
+                done += 1
         return done, nk, time.perf_counter() - t0
 
     def close(self):
