@@ -408,7 +408,15 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
 template <uint32_t VC>
 __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     if constexpr ((VC & VC_KV3) != 0) {
+#if DWPA_KV3_AES == 1
+        // four copies of one entry per 16-byte store (words 4j..4j+3 all hold Te0[4j >> 5])
+        for (uint32_t j = threadIdx.x; j < AES_LDS_WORDS / 4; j += blockDim.x) {
+            const uint32_t v = aes_lds_word(4 * j);
+            reinterpret_cast<uint4*>(te)[j] = make_uint4(v, v, v, v);
+        }
+#else
         for (uint32_t k = threadIdx.x; k < AES_LDS_WORDS; k += blockDim.x) te[k] = aes_lds_word(k);
+#endif
         __syncthreads();
     }
     return te + threadIdx.x % AES_SLICES;
@@ -443,7 +451,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                 uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
     check_prio_vc<VC>();
-    __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 4];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
 #if DWPA_KV3_RK_LDS
     __shared__ uint4 rk_lds[(VC & VC_KV3) ? 10 * vc_block(VC) : 1];
@@ -582,7 +590,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                     uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
     check_prio_vc<VC>();
-    __shared__ uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 4];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
 #if DWPA_KV3_RK_LDS
     __shared__ uint4 rk_lds[(VC & VC_KV3) ? 10 * vc_block(VC) : 1];
