@@ -78,11 +78,11 @@ tools/bin/valu_peak64: tools/valu_peak64.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
-tools/bin/inflate_bench: tools/inflate_bench.cpp $(SRC)/dict_reader.hpp $(SRC)/inflate.hpp $(SRC)/m22000_host.cpp \
+tools/bin/inflate_bench: tools/inflate_bench.cpp $(SRC)/dict_reader.hpp $(SRC)/inflate.hpp $(SRC)/pinflate.hpp $(SRC)/m22000_host.cpp \
                          $(SRC)/m22000_host.hpp
 	@mkdir -p tools/bin
 	g++ -O3 -std=c++17 -Iinclude -I$(SRC) -o $@ tools/inflate_bench.cpp $(SRC)/m22000_host.cpp -lz -lpthread
 
-tools/bin/inflate_check: tools/inflate_check.cpp $(SRC)/inflate.hpp
+tools/bin/inflate_check: tools/inflate_check.cpp $(SRC)/inflate.hpp $(SRC)/pinflate.hpp
 	@mkdir -p tools/bin
-	g++ -O3 -std=c++17 -Wall -I$(SRC) -o $@ tools/inflate_check.cpp -lz
+	g++ -O3 -std=c++17 -Wall -I$(SRC) -o $@ tools/inflate_check.cpp -lz -lpthread

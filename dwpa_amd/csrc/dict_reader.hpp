@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
@@ -23,6 +24,7 @@
 
 #include "inflate.hpp"
 #include "m22000_host.hpp"
+#include "pinflate.hpp"
 
 namespace dwpa {
 
@@ -119,6 +121,8 @@ class BlockInflater {
         bool ok = true;
         if (gz && zlib_) {
             ok = file_zlib(fd);
+        } else if (gz && parallel_threads(fd) > 1) {
+            ok = file_parallel(fd);
         } else if (gz) {
             GzipDecoder dec(fd);
             uint64_t delivered = 0;
@@ -154,6 +158,59 @@ class BlockInflater {
         }
         close(fd);
         return ok;
+    }
+    // Worker threads for one large gzip file (ParallelGunzip, pinflate.hpp): DWPA_INFLATE_THREADS, default
+    // min(8, half the CPUs this process may use); files under 4 chunks (DWPA_INFLATE_CHUNK_MB, default 4) and
+    // DWPA_INFLATE_THREADS=1 take the single-stream decoder.
+    static size_t chunk_bytes() {
+        const char* e = getenv("DWPA_INFLATE_CHUNK_MB");
+        const long mb = e && *e ? atol(e) : 4;
+        return (size_t)std::max<long>(1, mb) << 20;
+    }
+    static unsigned parallel_threads(int fd) {
+        struct stat st;
+        if (fstat(fd, &st) != 0 || (size_t)st.st_size < 4 * chunk_bytes()) return 1;
+        const char* e = getenv("DWPA_INFLATE_THREADS");
+        if (e && *e) return (unsigned)std::max(1, atoi(e));
+        cpu_set_t cs;
+        const unsigned cpus = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? (unsigned)CPU_COUNT(&cs)
+                                                                          : std::thread::hardware_concurrency();
+        return std::max(1u, std::min(8u, cpus / 2));
+    }
+    // One gzip file through ParallelGunzip into BLOCK-sized blocks.  If the parallel decode stops short (damage, or a
+    // false block boundary), zlib's gzread continues from the bytes delivered and decides what the rest yields.
+    bool file_parallel(int fd) {
+        struct stat st;
+        if (fstat(fd, &st) != 0) return error_block();
+        Block b = fresh();
+        bool ok = true;
+        uint64_t pushed = 0;
+        const char* perr = nullptr;
+        ParallelGunzip::run(fd, (size_t)st.st_size, parallel_threads(fd), chunk_bytes(),
+                            [&](const uint8_t* p, size_t k) {
+                                while (k && ok) {
+                                    const size_t t = std::min(b.begin + BLOCK - b.end, k);
+                                    memcpy(b.buf.data() + b.end, p, t);
+                                    b.end += t;
+                                    p += t;
+                                    k -= t;
+                                    if (b.end == b.begin + BLOCK) {
+                                        pushed += b.size();
+                                        ok = push(std::move(b)) && !cancelled();
+                                        b = fresh();
+                                    }
+                                }
+                                return ok;
+                            },
+                            &perr);
+        if (!ok || cancelled()) return false;
+        if (perr) {  // damage (or a false boundary): gzread continues after the bytes delivered
+            pushed += b.size();
+            if (b.size() && !push(std::move(b))) return false;
+            return file_zlib(fd, pushed, ParallelGunzip::false_boundary(perr) ? nullptr : perr);
+        }
+        b.file_end = true;
+        return push(std::move(b));
     }
     // gzread over the whole file (DWPA_INFLATE=zlib), or over its rest after GzipDecoder failed (`skip` bytes
     // already delivered, `why` = the decoder's error).  gzread returns the data before a cut and then 0 (error

@@ -111,25 +111,172 @@ class GzipDecoder {
     static constexpr size_t WIN = 32768;  // history kept in front of every output block
     static constexpr size_t SLACK = 320;  // output room past the limit: one match (258) + an 8-byte word copy
 
+    static constexpr size_t PAD = 64;     // zero bytes the input must carry past its end
+    static constexpr uint16_t MARK = 0x8000;  // read16: MARK + w = byte w of the unknown window (0 = oldest)
+
     explicit GzipDecoder(int fd) : fd_(fd), in_(INCAP + PAD, 0) {
-        in_ptr_ = in_end_ = in_.data();
+        base_ = in_ptr_ = in_end_ = in_.data();
+        build_fixed();
+    }
+    // In-memory input data[0, n), followed by at least PAD readable zero bytes (parallel chunks, pinflate.hpp).  With
+    // `chunk` set the decoder checks no CRC-32/ISIZE itself (its output is part of a stream decoded in pieces): member
+    // trailers are recorded in trailers() for the caller, who checks them over the joined output.
+    GzipDecoder(const uint8_t* data, size_t n, bool chunk) : fd_(-1), mem_(true), chunk_(chunk) {
+        base_ = in_ptr_ = const_cast<uint8_t*>(data);  // never written: fill() does nothing in memory mode
+        in_end_ = base_ + n;
+        eof_ = true;
         build_fixed();
     }
     bool failed() const { return st_ == ERR; }
     bool done() const { return st_ == DONE; }
+    bool stopped() const { return st_ == STOPPED; }
     const char* error() const { return err_; }
+
+    struct Trailer {
+        uint64_t end;  // output offset just past the member's last byte
+        uint32_t crc, isize;
+    };
+    const std::vector<Trailer>& trailers() const { return trailers_; }
+    uint64_t out_total() const { return out_total_; }
+    // input bits consumed (memory mode)
+    uint64_t bit_pos() const { return (uint64_t)(in_ptr_ - base_) * 8 - bc_; }
+    // Memory mode: start at the deflate block header at bit `pos`, with `hlen` bytes of history (0: unknown window,
+    // decode with read16 first).
+    void start_block(uint64_t pos, const uint8_t* hist, size_t hlen) {
+        in_ptr_ = base_ + pos / 8;
+        bb_ = 0;
+        bc_ = 0;
+        refill();
+        bb_ >>= pos & 7;
+        bc_ -= (uint32_t)(pos & 7);
+        hist_.assign(hist, hist + hlen);
+        st_ = BLOCK;
+        members_ = 1;
+        err_ = nullptr;
+    }
+    // Stop (stopped()) at the block boundary at bit `pos`; running past it without landing on it is an error (the
+    // next chunk's boundary was a false find).
+    void stop_at(uint64_t pos) { stop_ = pos; }
+    void set_history(const uint8_t* h, size_t n) { hist_.assign(h, h + n); }
+
+    // Boundary probe (memory mode, right after start_block): the block there is a dynamic-Huffman block whose code
+    // tables are valid and which decodes to its end-of-block (back-references into the unknown window allowed),
+    // followed by a valid next block type or the member's end.
+    bool probe_block(std::vector<uint16_t>& scratch) {
+        scratch.clear();
+        uint8_t* d = nullptr;
+        step(d, d);
+        if (st_ != HUFF || lt_ != dyn_l_.data()) return false;
+        huff16(scratch);
+        if (st_ == TRAILER) return !scratch.empty();
+        if (st_ != BLOCK || scratch.empty()) return false;
+        refill();
+        return ((bb_ >> 1) & 3) != 3;
+    }
+    // Cheap pre-test of a dynamic block header at bit p of d (d padded): block type 2, HLIT/HDIST in range and a
+    // complete code-length code (what build() demands) -- rejects all but a few per cent of bit positions.
+    static bool maybe_dynamic(const uint8_t* d, uint64_t p) {
+        uint64_t w0, w1;
+        memcpy(&w0, d + p / 8, 8);
+        memcpy(&w1, d + p / 8 + 8, 8);
+        const uint32_t sh = (uint32_t)(p & 7);
+        const uint64_t lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;  // 64 bits from p
+        const uint64_t hi = w1 >> sh;                                     // bits 64.. (>= 56 of them)
+        if (((lo >> 1) & 3) != 2) return false;
+        if (((lo >> 3) & 31) > 29 || ((lo >> 8) & 31) > 29) return false;
+        const uint32_t hclen = (uint32_t)((lo >> 13) & 15) + 4;
+        uint32_t kraft = 0, nz = 0;
+        for (uint32_t i = 0; i < hclen; i++) {
+            const uint32_t b = 17 + 3 * i;
+            const uint32_t l = b + 3 <= 64 ? (uint32_t)((lo >> b) & 7)
+                               : b >= 64 ? (uint32_t)((hi >> (b - 64)) & 7)
+                                         : (uint32_t)(((lo >> b) | (hi << (64 - b))) & 7);
+            if (l) {
+                kraft += 128u >> l;
+                nz++;
+            }
+        }
+        return kraft == 128 && nz >= 2;
+    }
+
+    // Marker phase of a chunk whose preceding 32 KiB are not known yet: appends 16-bit symbols to out, a byte value
+    // (< 256) or MARK + w for byte w of that window.  Returns at a block boundary: R16_SWITCH once out holds >= WIN
+    // symbols of which the last WIN are bytes (the caller continues with read() after set_history), R16_STOP at
+    // stop_at's boundary, R16_END at the end of the stream, R16_ERR on an error.
+    enum { R16_SWITCH, R16_STOP, R16_END, R16_ERR };
+    int read16(std::vector<uint16_t>& out) {
+        const size_t out0 = out.size();
+        int r = R16_ERR;
+        for (;;) {
+            if (st_ == ERR) break;
+            if (st_ == DONE) {
+                if (stop_ != NO_STOP) fail("stream ended before the chunk boundary");
+                else r = R16_END;
+                break;
+            }
+            if (st_ == HEADER) {
+                if (!read_header() && st_ != DONE) break;
+                continue;
+            }
+            if (st_ == TRAILER) {
+                cur_out_ = out_total_ + (out.size() - out0);
+                finish_member();
+                continue;
+            }
+            if (st_ == BLOCK) {
+                if (stop_ != NO_STOP && bit_pos() >= stop_) {
+                    if (bit_pos() == stop_) {
+                        st_ = STOPPED;
+                        r = R16_STOP;
+                    } else {
+                        fail("deflate block boundary mismatch");
+                    }
+                    break;
+                }
+                if (out.size() >= WIN && no_marker(out.data() + out.size() - WIN, WIN)) {
+                    r = R16_SWITCH;
+                    break;
+                }
+                uint8_t* d = nullptr;
+                step(d, d);  // block header
+                continue;
+            }
+            if (st_ == STORED) {
+                while (stored_left_) {
+                    const size_t k = (size_t)(in_end_ - in_ptr_) < stored_left_ ? (size_t)(in_end_ - in_ptr_) : stored_left_;
+                    if (!k) break;
+                    for (size_t i = 0; i < k; i++) out.push_back(in_ptr_[i]);
+                    in_ptr_ += k;
+                    stored_left_ -= (uint32_t)k;
+                }
+                if (stored_left_) {
+                    fail("truncated stored block");
+                    break;
+                }
+                end_block(nullptr);
+                continue;
+            }
+            if (st_ == HUFF) {
+                huff16(out);
+                continue;
+            }
+            break;
+        }
+        out_total_ += out.size() - out0;
+        return st_ == ERR ? R16_ERR : r;
+    }
 
     // Decodes up to `want` new bytes into buf[WIN, WIN + want); buf must hold WIN + want + SLACK bytes.  The stream's
     // last <= 32 KiB of output is copied into buf[WIN - h, WIN) first.  Returns the new bytes (0: end of stream or
     // error -- see failed()).
     size_t read(uint8_t* buf, size_t want) {
-        if (st_ == DONE || st_ == ERR) return 0;
+        if (st_ == DONE || st_ == ERR || st_ == STOPPED) return 0;
         memcpy(buf + WIN - hist_.size(), hist_.data(), hist_.size());
         hist_start_ = buf + WIN - hist_.size();
         uint8_t* o = buf + WIN;
         uint8_t* const lim = o + want;
         uint8_t* seg = o;  // first byte of the current member in this call (CRC-32 / ISIZE)
-        while (o < lim && st_ != DONE && st_ != ERR) {
+        while (o < lim && st_ != DONE && st_ != ERR && st_ != STOPPED) {
             if (st_ == HEADER) {
                 if (!read_header()) break;
                 seg = o;
@@ -137,25 +284,31 @@ class GzipDecoder {
             }
             o = step(o, lim);
             if (st_ == TRAILER) {  // the member's last block ended: check its trailer, then look for another member
-                crc_ = Crc32::get()(crc_, seg, (size_t)(o - seg));
-                isize_ += (uint32_t)(o - seg);
+                if (!chunk_) {
+                    crc_ = Crc32::get()(crc_, seg, (size_t)(o - seg));
+                    isize_ += (uint32_t)(o - seg);
+                }
                 seg = o;
+                cur_out_ = out_total_ + (uint64_t)(o - (buf + WIN));
                 finish_member();
             }
         }
-        if (st_ != ERR) {
+        if (st_ != ERR && !chunk_) {
             crc_ = Crc32::get()(crc_, seg, (size_t)(o - seg));
             isize_ += (uint32_t)(o - seg);
         }
+        if (st_ == DONE && stop_ != NO_STOP) fail("stream ended before the chunk boundary");
         // keep the last 32 KiB as the next block's history
         const size_t have = (size_t)(o - hist_start_), keep = have < WIN ? have : WIN;
         hist_.assign(o - keep, o);
+        out_total_ += (uint64_t)(o - (buf + WIN));
         return st_ == ERR ? 0 : (size_t)(o - (buf + WIN));
     }
 
   private:
-    static constexpr size_t INCAP = 4u << 20, PAD = 64;
-    enum St { HEADER, BLOCK, STORED, HUFF, TRAILER, DONE, ERR };
+    static constexpr size_t INCAP = 4u << 20;
+    static constexpr uint64_t NO_STOP = ~0ull;
+    enum St { HEADER, BLOCK, STORED, HUFF, TRAILER, DONE, ERR, STOPPED };
     // table entry: bits 0-3 code length, 4-7 extra bits (SUB: index bits), 8-9 kind, 10 invalid, 16-31 value
     enum : uint32_t { K_LIT = 0, K_LEN = 1u << 8, K_EOB = 2u << 8, K_SUB = 3u << 8, K_MASK = 3u << 8, K_BAD = 1u << 10 };
     static constexpr int LBITS = 11, DBITS = 8, CBITS = 7;
@@ -167,7 +320,7 @@ class GzipDecoder {
     // Keeps the bytes from in_ptr_ - 8 on (a stored block or the trailer may step back over whole bytes that are
     // still in the bit buffer), reads more, zero-pads.
     void fill() {
-        if (eof_) return;
+        if (eof_ || mem_) return;
         uint8_t* keep = in_ptr_ - 8 > in_.data() ? in_ptr_ - 8 : in_.data();
         const size_t back = (size_t)(in_ptr_ - keep), tail = (size_t)(in_end_ - keep);
         memmove(in_.data(), keep, tail);
@@ -405,8 +558,12 @@ class GzipDecoder {
         memcpy(&c, in_ptr_, 4);
         memcpy(&s, in_ptr_ + 4, 4);
         in_ptr_ += 8;
-        if (c != crc_) { fail("gzip CRC-32 mismatch"); return; }
-        if (s != isize_) { fail("gzip ISIZE mismatch"); return; }
+        if (chunk_) {
+            trailers_.push_back(Trailer{cur_out_, c, s});
+        } else {
+            if (c != crc_) { fail("gzip CRC-32 mismatch"); return; }
+            if (s != isize_) { fail("gzip ISIZE mismatch"); return; }
+        }
         st_ = HEADER;
     }
 
@@ -414,6 +571,11 @@ class GzipDecoder {
     uint8_t* step(uint8_t* o, uint8_t* lim) {
         switch (st_) {
             case BLOCK: {
+                if (stop_ != NO_STOP && bit_pos() >= stop_) {
+                    if (bit_pos() == stop_) st_ = STOPPED;
+                    else fail("deflate block boundary mismatch");
+                    return o;
+                }
                 need(64);
                 final_ = bits(1);
                 const uint32_t type = bits(2);
@@ -561,7 +723,60 @@ class GzipDecoder {
         return o;
     }
 
+    static bool no_marker(const uint16_t* p, size_t n) {
+        uint16_t acc = 0;
+        for (size_t i = 0; i < n; i++) acc |= p[i];
+        return !(acc & MARK);
+    }
+    // huff() for the marker phase: 16-bit output, references before the chunk's first symbol become markers.
+    void huff16(std::vector<uint16_t>& out) {
+        const uint32_t* lt = lt_;
+        const uint32_t* dt = dt_;
+        const uint8_t* const in_stop = in_end_ + 16;
+        for (;;) {
+            if (in_ptr_ > in_stop) { fail("truncated deflate stream"); return; }
+            refill();
+            uint32_t e = lt[bb_ & ((1u << LBITS) - 1)];
+            if ((e & K_MASK) == K_SUB) e = lt[(e >> 16) + ((bb_ >> LBITS) & ((1u << ((e >> 4) & 15)) - 1))];
+            if (e & K_BAD) { fail("invalid literal/length code"); return; }
+            bb_ >>= e & 15;
+            bc_ -= e & 15;
+            if ((e & K_MASK) == K_LIT) {
+                out.push_back((uint16_t)(e >> 16));
+                continue;
+            }
+            if ((e & K_MASK) == K_EOB) {
+                end_block(nullptr);
+                if (overrun()) fail("truncated deflate stream");
+                return;
+            }
+            const uint32_t lx = (e >> 4) & 15;
+            const uint32_t len = (e >> 16) + (uint32_t)(bb_ & ((1u << lx) - 1));
+            bb_ >>= lx;
+            bc_ -= lx;
+            uint32_t d = dt[bb_ & ((1u << DBITS) - 1)];
+            if ((d & K_MASK) == K_SUB) d = dt[(d >> 16) + ((bb_ >> DBITS) & ((1u << ((d >> 4) & 15)) - 1))];
+            if (d & K_BAD) { fail("invalid distance code"); return; }
+            bb_ >>= d & 15;
+            bc_ -= d & 15;
+            const uint32_t dx = (d >> 4) & 15;
+            const size_t dist = (d >> 16) + (uint32_t)(bb_ & ((1u << dx) - 1));
+            bb_ >>= dx;
+            bc_ -= dx;
+            const size_t have = out.size();  // symbols of the chunk so far
+            if (dist > have + WIN) { fail("distance too far back"); return; }
+            for (uint32_t i = 0; i < len; i++) {
+                const size_t at = out.size();
+                out.push_back(at >= dist ? out[at - dist] : (uint16_t)(MARK + (WIN + at - dist)));
+            }
+        }
+    }
+
     int fd_;
+    bool mem_ = false, chunk_ = false;
+    uint8_t* base_ = nullptr;  // start of the input (bit_pos)
+    uint64_t stop_ = NO_STOP, out_total_ = 0, cur_out_ = 0;
+    std::vector<Trailer> trailers_;
     std::vector<uint8_t> in_;
     uint8_t* in_ptr_;
     uint8_t* in_end_;

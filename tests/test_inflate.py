@@ -146,3 +146,74 @@ def test_decoder_rejects_what_zlib_rejects(tool, tmp_path):
         res = lines[str(p)]
         assert res.startswith("error ") and not res.startswith("error none"), (p.name, res)
     assert rc == 0  # both decoders failed on every file
+
+
+def _prun(tool, paths, threads=4, chunk=65536):
+    r = subprocess.run([tool, "-p", str(threads), "-c", str(chunk)] + [str(p) for p in paths], capture_output=True,
+                       text=True)
+    return r.returncode, dict(l.split(" ", 1) for l in r.stdout.splitlines())
+
+
+def test_parallel_inflate_matches_zlib(tool, tmp_path):
+    """one gzip stream inflated in parallel chunks (dwpa_amd/csrc/pinflate.hpp, ParallelGunzip:
+    block-boundary search, 16-bit marker phase for the unknown window, in-order marker resolution and per-member
+    CRC-32/ISIZE), continued by gzread when it stops -- exactly what the dictionary reader runs.  64 KiB chunks make
+    every file here dozens of chunks.  Output must equal zlib's byte for byte; the chunks must really run in parallel
+    where the stream has dynamic blocks; fixed-Huffman and stored streams (no boundary to find) still decode, in one
+    piece."""
+    rng = random.Random(13)
+    txt = _words(rng, 200_000)
+    rnd_words = b"\n".join(bytes(rng.randint(0x21, 0x7E) for _ in range(rng.randint(8, 20)))
+                           for _ in range(150_000)) + b"\n"
+    cases = {
+        "rand_l1.gz": gzip.compress(rnd_words, compresslevel=1),
+        "text_l6.gz": gzip.compress(txt, compresslevel=6),
+        "text_l9.gz": gzip.compress(txt, compresslevel=9),
+        "huffonly.gz": _member(txt, strategy=zlib.Z_HUFFMAN_ONLY),
+        "rle.gz": _member(b"a" * 300_000 + txt[:600_000] + b"ab" * 100_000, strategy=zlib.Z_RLE),
+        "fixed.gz": _member(txt[:600_000], strategy=zlib.Z_FIXED),
+        "stored.gz": _member(txt[:600_000], level=0),
+        "mixed.gz": gzip.compress(txt[:300_000] + rng.randbytes(400_000) + txt[300_000:700_000], compresslevel=1),
+        "multi.gz": gzip.compress(txt[:500_000]) + gzip.compress(b"") + gzip.compress(rnd_words[:700_000], 1) +
+                    gzip.compress(txt[500_000:]),
+        "garbage.gz": gzip.compress(txt, compresslevel=1) + b"trailing bytes that are not gzip" * 50,
+    }
+    paths = []
+    for name, blob in cases.items():
+        p = tmp_path / name
+        p.write_bytes(blob)
+        paths.append(p)
+    for threads in (1, 3, 8):
+        rc, lines = _prun(tool, paths, threads)
+        for p in paths:
+            assert lines[str(p)].startswith("ok "), (threads, p.name, lines[str(p)])
+        assert rc == 0
+    info = {p.name: lines[str(p)].split() for p in paths}
+    par = {k: int(v[v.index("parallel") + 1]) for k, v in info.items()}
+    chunks = {k: int(v[v.index("chunks") + 1]) for k, v in info.items()}
+    for k in ("rand_l1.gz", "text_l6.gz", "text_l9.gz", "huffonly.gz", "multi.gz"):
+        assert par[k] >= chunks[k] // 2 and par[k] >= 4, (k, par[k], chunks[k])
+    assert par["fixed.gz"] == 1 and par["stored.gz"] == 1
+    assert all(v[v.index("stop") + 1] == "none" for k, v in info.items()), info
+
+
+def test_parallel_inflate_damaged_like_gzread(tool, tmp_path):
+    """Damage inside a parallel decode: a cut stream yields exactly gzread's bytes (the reader hands over to gzread
+    after what was delivered); a corrupt trailer or body yields at least gzread's bytes and fails."""
+    rng = random.Random(14)
+    good = gzip.compress(_words(rng, 200_000), compresslevel=6)
+    body = bytearray(good)
+    body[len(body) * 3 // 4] ^= 0x55
+    crc = bytearray(good)
+    crc[-6] ^= 1
+    cases = {"cut_mid.gz": good[: len(good) // 2], "cut_end.gz": good[:-3], "cut_trailer.gz": good[:-8],
+             "crc.gz": bytes(crc), "corrupt.gz": bytes(body)}
+    paths = []
+    for name, blob in cases.items():
+        p = tmp_path / name
+        p.write_bytes(blob)
+        paths.append(p)
+    rc, lines = _prun(tool, paths, 4)
+    for p in paths:
+        assert lines[str(p)].startswith("error both"), (p.name, lines[str(p)])
+    assert rc == 0
