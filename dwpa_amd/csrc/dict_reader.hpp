@@ -65,6 +65,8 @@ class BlockInflater {
         cv_.notify_all();
         th_.join();
     }
+    // ParallelGunzip workers this reader gives the gzip file `fd` (1: the single-stream GzipDecoder).
+    static unsigned parallel_threads(int fd) { return parallel_threads_for(fd); }
     // Blocks until the next block (b's previous buffer goes back to the pool); false once every file is delivered.
     bool next(Block& b) {
         std::unique_lock<std::mutex> lk(mu_);
@@ -121,7 +123,7 @@ class BlockInflater {
         bool ok = true;
         if (gz && zlib_) {
             ok = file_zlib(fd);
-        } else if (gz && parallel_threads(fd) > 1) {
+        } else if (gz && parallel_threads_for(fd) > 1) {
             ok = file_parallel(fd);
         } else if (gz) {
             GzipDecoder dec(fd);
@@ -167,7 +169,7 @@ class BlockInflater {
         const long mb = e && *e ? atol(e) : 4;
         return (size_t)std::max<long>(1, mb) << 20;
     }
-    static unsigned parallel_threads(int fd) {
+    static unsigned parallel_threads_for(int fd) {
         struct stat st;
         if (fstat(fd, &st) != 0 || (size_t)st.st_size < 4 * chunk_bytes()) return 1;
         const char* e = getenv("DWPA_INFLATE_THREADS");
@@ -186,7 +188,7 @@ class BlockInflater {
         bool ok = true;
         uint64_t pushed = 0;
         const char* perr = nullptr;
-        ParallelGunzip::run(fd, (size_t)st.st_size, parallel_threads(fd), chunk_bytes(),
+        ParallelGunzip::run(fd, (size_t)st.st_size, parallel_threads_for(fd), chunk_bytes(),
                             [&](const uint8_t* p, size_t k) {
                                 while (k && ok) {
                                     const size_t t = std::min(b.begin + BLOCK - b.end, k);

@@ -131,12 +131,21 @@ int main(int argc, char** argv) {
         if (err) return 1;
     }
     const double t_all = since(t);
+    std::string inflater = "GzipDecoder";
+    {
+        const int fd = open(paths[0].c_str(), O_RDONLY);
+        const char* z = getenv("DWPA_INFLATE");
+        if (z && !strcmp(z, "zlib")) inflater = "zlib";
+        else if (fd >= 0 && dwpa::BlockInflater::parallel_threads(fd) > 1)
+            inflater = "ParallelGunzip x" + std::to_string(dwpa::BlockInflater::parallel_threads(fd));
+        if (fd >= 0) close(fd);
+    }
     printf("{\"files\": %zu, \"raw_bytes\": %zu, \"inflate_MBps\": %.1f, \"fast_inflate_MBps\": %.1f, "
            "\"reader_inflater\": \"%s\", \"words\": %zu, "
            "\"reader_words_per_s\": %.0f, \"reader_MBps\": %.1f, \"chunk_source_threads\": %zu, "
            "\"chunk_source_words_per_s\": %.0f}\n",
            paths.size(), raw, raw / t_inflate / 1e6, raw_fast ? raw_fast / t_fast / 1e6 : 0.0,
-           getenv("DWPA_INFLATE") && !strcmp(getenv("DWPA_INFLATE"), "zlib") ? "zlib" : "GzipDecoder", words1, words1 / t_reader, raw / t_reader / 1e6,
+           inflater.c_str(), words1, words1 / t_reader, raw / t_reader / 1e6,
            std::min<size_t>(paths.size(), 4), words_all / t_all);
     return 0;
 }

@@ -27,8 +27,13 @@ with gzip.open(f"{tmp}/list.txt.gz", "wb", compresslevel=6) as f:
     f.write(b"\n".join(words) + b"\n")
 PY
 for f in c2 list; do
-  timeout -k 10 120 tools/bin/inflate_bench $TMP/$f.txt.gz > $OUT/$f.json
+  for t in ${THREADS:-1 4 8 12}; do
+    DWPA_INFLATE_THREADS=$t timeout -k 10 120 tools/bin/inflate_bench $TMP/$f.txt.gz > $OUT/${f}_t$t.json
+  done
   DWPA_INFLATE=zlib timeout -k 10 120 tools/bin/inflate_bench $TMP/$f.txt.gz > $OUT/${f}_zlib.json
   timeout -k 10 120 tools/bin/inflate_check -r 2 $TMP/$f.txt.gz > $OUT/${f}_check.txt
+  for t in 4 8 12; do
+    timeout -k 10 120 tools/bin/inflate_check -r 2 -p $t $TMP/$f.txt.gz > $OUT/${f}_pcheck_t$t.txt
+  done
 done
 cat $OUT/*.json
