@@ -467,11 +467,25 @@ __constant__ static const AesTables AES_TABLES = make_aes_tables();
 #if DWPA_KV3_AES == 1
 constexpr uint32_t AES_SLICES = 32;                     // copies of Te0
 constexpr uint32_t AES_LDS_WORDS = 256 * AES_SLICES;    // 32 KiB
-#define AES_T(t, x) rotr(te4[(x) << 5], 8u * (t))        // te4 = the lane's copy (base + lane % 32)
-__device__ __forceinline__ uint32_t aes4_subword(const uint32_t* te4, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    // (S[a], S[b], S[c], S[d]) from most to least significant; S[x] = byte 2 (and byte 1) of Te0[x]
-    const uint32_t hi = __builtin_amdgcn_perm(te4[a << 5], te4[b << 5], 0x06020000u);  // S[a]:b3, S[b]:b2
-    const uint32_t lo = __builtin_amdgcn_perm(te4[c << 5], te4[d << 5], 0x00000501u);  // S[c]:b1, S[d]:b0
+// Byte offset of Te0[byte K of s] in the lane's copy: (x << 7) | cw, cw = 4 (lane % 32).  Two full-rate ops for
+// K = 1..3 (a right shift that lands the byte on bits 7..14, then one v_bitop3_b32 (t & 0x7f80) | cw, truth table
+// 0xEA); LLVM's own choice was v_bfe + v_lshl_or, two half-rate ops.  The key schedule's lookups stay hoisted out of
+// the CMAC loop (the builtin, unlike inline asm, is a pure value to LLVM).
+template <int K>
+__device__ __forceinline__ uint32_t aes_v1_off(uint32_t s, uint32_t cw) {
+    const uint32_t t = K == 3 ? s >> 17 : K == 2 ? s >> 9 : K == 1 ? s >> 1 : s << 7;
+    return __builtin_amdgcn_bitop3_b32(t, 0x7f80u, cw, 0xea);  // the builtin (not asm) so LLVM can still hoist
+}
+template <int K>
+__device__ __forceinline__ uint32_t aes_v1_ld(const uint32_t* te, uint32_t s, uint32_t cw) {
+    return *(const uint32_t*)((const char*)te + aes_v1_off<K>(s, cw));
+}
+// (S[a], S[b], S[c], S[d]) with a = byte KA of wa, ...; S[x] = byte 2 (and byte 1) of Te0[x]
+template <int KA, int KB, int KC, int KD>
+__device__ __forceinline__ uint32_t aes4_subword_v1(const uint32_t* te, uint32_t cw, uint32_t wa, uint32_t wb,
+                                                    uint32_t wc, uint32_t wd) {
+    const uint32_t hi = __builtin_amdgcn_perm(aes_v1_ld<KA>(te, wa, cw), aes_v1_ld<KB>(te, wb, cw), 0x06020000u);
+    const uint32_t lo = __builtin_amdgcn_perm(aes_v1_ld<KC>(te, wc, cw), aes_v1_ld<KD>(te, wd, cw), 0x00000501u);
     return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
 }
 #elif DWPA_KV3_AES == 2
@@ -514,7 +528,37 @@ __device__ __forceinline__ uint32_t aes_lds_word(uint32_t k) {
     return rotr(AES_TABLES.te0[x], 8 * t);
 #endif
 }
-#if DWPA_KV3_AES == 2
+#if DWPA_KV3_AES == 1
+// te = the table base (every lane's copy is picked by cw inside the lookups)
+__device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uint32_t key[4], uint32_t s[4]) {
+    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+    const uint32_t cw = (threadIdx.x & 31u) << 2;
+    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
+    uint32_t s0 = s[0] ^ k0, s1 = s[1] ^ k1, s2 = s[2] ^ k2, s3 = s[3] ^ k3;
+#define T(w, k) aes_v1_ld<k>(te, w, cw)
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        k0 ^= aes4_subword_v1<2, 1, 0, 3>(te, cw, k3, k3, k3, k3) ^ (RCON[r - 1] << 24);
+        k1 ^= k0;
+        k2 ^= k1;
+        k3 ^= k2;
+        const uint32_t t0 = xor3(xor3(T(s0, 3), rotr(T(s1, 2), 8), rotr(T(s2, 1), 16)), rotr(T(s3, 0), 24), k0);
+        const uint32_t t1 = xor3(xor3(T(s1, 3), rotr(T(s2, 2), 8), rotr(T(s3, 1), 16)), rotr(T(s0, 0), 24), k1);
+        const uint32_t t2 = xor3(xor3(T(s2, 3), rotr(T(s3, 2), 8), rotr(T(s0, 1), 16)), rotr(T(s1, 0), 24), k2);
+        const uint32_t t3 = xor3(xor3(T(s3, 3), rotr(T(s0, 2), 8), rotr(T(s1, 1), 16)), rotr(T(s2, 0), 24), k3);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+#undef T
+    k0 ^= aes4_subword_v1<2, 1, 0, 3>(te, cw, k3, k3, k3, k3) ^ (RCON[9] << 24);
+    k1 ^= k0;
+    k2 ^= k1;
+    k3 ^= k2;
+    s[0] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s0, s1, s2, s3) ^ k0;
+    s[1] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s1, s2, s3, s0) ^ k1;
+    s[2] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s2, s3, s0, s1) ^ k2;
+    s[3] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s3, s0, s1, s2) ^ k3;
+}
+#elif DWPA_KV3_AES == 2
 __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uint32_t key[4], uint32_t s[4]) {
     constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
     const uint32_t cw = (threadIdx.x & 31u) << 2;

@@ -419,7 +419,7 @@ __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
 #endif
         __syncthreads();
     }
-    return te + threadIdx.x % AES_SLICES;
+    return te + (DWPA_KV3_AES == 0 ? threadIdx.x % AES_SLICES : 0u);  // layouts 1/2 pick the lane's copy per lookup
 }
 // keyver-3 kernels with the four-table layout sliced (DWPA_KV3_AES=0, DWPA_KV3_SLICES > 1: 64 KiB of LDS at S = 16,
 // an A/B build) run 512-thread workgroups: two per CU, 4 waves per SIMD; the lane-sliced Te0 (32 KiB) and the plain
