@@ -196,7 +196,6 @@ struct Device {
     hipEvent_t vs_go = nullptr, vs_done = nullptr;  // check path: fan-out of the keyver-3 verify onto `side`
     hipEvent_t head_done = nullptr, tail_done = nullptr, prep_done = nullptr;
     hipEvent_t head_end = nullptr;  // check path: this context's last PBKDF2 head (the device's head fence)
-    hipEvent_t done_ev = nullptr;   // check path: end of a call's last kernel (polled, wait_done)
     PinnedArena stage;            // check path: host staging of the derive uploads
     MappedHost hits_host;         // check path: hit count + hits written by k_hits_out
     std::mutex mu;
@@ -313,34 +312,7 @@ static int device_stream(Device& d) {
         HIPCHK(hipEventCreateWithFlags(&d.head_end, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.vs_go, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.vs_done, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&d.done_ev, hipEventDisableTiming));
     }
-    return 0;
-}
-
-// The end of a call's kernels on stream s.  DWPA_SYNC=poll (default): query an event every ~20 us, so the host
-// sees the end within tens of microseconds while sleeping through the ~50 ms of GPU work; DWPA_SYNC=sync:
-// hipStreamSynchronize (the runtime's own wait, A/B).
-static bool sync_poll_knob() {
-    static const bool v = [] {
-        const char* e = getenv("DWPA_SYNC");
-        return !(e && !strcmp(e, "sync"));
-    }();
-    return v;
-}
-static int wait_done(Device& d, hipStream_t s) {
-    if (!sync_poll_knob()) {
-        HIPCHK(hipStreamSynchronize(s));
-        return 0;
-    }
-    HIPCHK(hipEventRecord(d.done_ev, s));
-    for (;;) {
-        const hipError_t q = hipEventQuery(d.done_ev);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) return DWPA_E_HIP;
-        std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-    HIPCHK(hipStreamSynchronize(s));  // returns at once; keeps the runtime's own bookkeeping of the stream
     return 0;
 }
 
@@ -822,7 +794,7 @@ static int collect_hits(Device& d, std::vector<HitDev>& hits_out) {
     const uint32_t* hitcnt = (const uint32_t*)d.batch.counters.p + 1;
     RCHK(d.hits_host.ensure(16 + (size_t)d.batch.hitcap * sizeof(HitDev)));
     HIPCHK(launch_hits_out(hitcnt, (const HitDev*)d.batch.hits.p, d.batch.hitcap, (uint32_t*)d.hits_host.dev, s));
-    RCHK(wait_done(d, s));
+    HIPCHK(hipStreamSynchronize(s));
     tr.mark("  device wait");
     const uint32_t nh = *(volatile const uint32_t*)d.hits_host.p;
     if (nh > d.batch.hitcap) return DWPA_E_OVERFLOW;
