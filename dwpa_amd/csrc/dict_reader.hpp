@@ -409,6 +409,10 @@ class DictCache {
         total_ += bytes;
     }
     size_t budget() const { return budget_; }
+    size_t entries() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return map_.size();
+    }
     bool can_hold(size_t bytes) const { return bytes <= budget_; }
     size_t hits() const { return hits_.load(); }
 
@@ -525,9 +529,14 @@ class ChunkSource {
             size_t kept = 0;
             bool whole = !key.empty();
             DictReader reader({path}, &cancel_);
+            size_t per_word = 16;  // decoded bytes per word, from the previous chunk (capacity reserved up front:
+                                   // growing fresh 10-100 MB vectors cost the crack path half its line-cutting rate)
             for (;;) {
                 auto c = std::make_shared<Chunk>();
+                c->off.reserve(words + 1);
+                c->bytes.reserve(words * (per_word + per_word / 8) + 64);
                 const bool have = reader.next(*c, words, (size_t)1 << 31, err, &cancel_);
+                if (c->words()) per_word = c->bytes.size() / c->words() + 1;
                 words = std::min(max_words, 2 * words);
                 if (!have || err) break;
                 if (whole) {

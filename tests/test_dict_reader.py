@@ -58,12 +58,15 @@ def test_reader_words_match(tmp_path):
 
 
 def _parse_passes(stdout):
-    """inflate_bench --passes output -> ([[cache_hits, words]] per pass, [file statuses] per pass)."""
+    """inflate_bench --passes output -> ([[cache_hits, words]] per pass, [file statuses] per pass); the cache's entry
+    count per pass is in _parse_passes.entries."""
     out, status, cur = [], [], None
+    entries = _parse_passes.entries = []
     for line in stdout.decode().split("\n")[:-1]:
         if line.startswith("#pass"):
             cur = [int(line.split()[3]), []]
             out.append(cur)
+            entries.append(int(line.split()[5]))
         elif line.startswith("#status"):
             status.append([int(x) for x in line.split()[1:]])
         else:
@@ -144,3 +147,20 @@ def test_damaged_gzip_scanned_to_the_damage_like_gzread(tmp_path, env):
                 exp_text = zlib.decompressobj(31).decompress(blob)  # everything inflate yields before the cut
                 assert 0 < len(exp_text) < len(data)
                 assert mine == _expected([exp_text]), name
+
+
+def test_cache_drops_stale_entry_of_a_changed_file(tmp_path):
+    """a dictionary re-downloaded under the same path (new size/mtime/inode) must not leave its old decode
+    in the DictCache until LRU eviction: the next read drops the stale entry and caches the new file, so the cache
+    keeps one entry per path and every pass yields the file's current words."""
+    subprocess.run(["make", "-s", "-C", ROOT, "tools/bin/inflate_bench"], check=True)
+    p = tmp_path / "cracked.txt"
+    p.write_bytes(b"".join(b"word%05d\n" % i for i in range(5000)))
+    r = subprocess.run([TOOL, "--passes", "3", str(p)], capture_output=True, check=True,
+                       env=dict(os.environ, DWPA_TEST_REWRITE=str(p)))
+    passes, status = _parse_passes(r.stdout)
+    assert [h for h, _ in passes] == [0, 0, 0]  # every pass sees a changed file: no stale replay
+    assert _parse_passes.entries == [1, 1, 1]
+    for k, (_, words) in enumerate(passes):
+        assert words[-1] == (b"word04999" if k == 0 else b"added-after-pass-%d" % (k - 1))
+        assert len(words) == 5000 + k

@@ -45,6 +45,9 @@ int main(int argc, char** argv) {
     if (std::string(argv[1]) == "--passes" && argc > 3) {
         const int K = atoi(argv[2]);
         std::vector<std::string> paths(argv + 3, argv + argc);
+        // DWPA_TEST_REWRITE=path: append one word to that (plain) file after every pass, as a re-download would
+        // change it (the cache must drop the stale decode and read the new file)
+        const char* rewrite = getenv("DWPA_TEST_REWRITE");
         std::string line;
         for (int pass = 0; pass < K; pass++) {
             dwpa::ChunkSource src(paths, 1000, 1 << 16);
@@ -54,7 +57,8 @@ int main(int argc, char** argv) {
             while (src.next(c, err)) got.push_back(c);
             src.finish();
             if (err) return 1;
-            printf("#pass %d cache_hits %zu\n#status", pass, dwpa::DictCache::get().hits());
+            printf("#pass %d cache_hits %zu cache_entries %zu\n#status", pass, dwpa::DictCache::get().hits(),
+                   dwpa::DictCache::get().entries());
             for (int st : src.file_status()) printf(" %d", st);  // ChunkSource::FILE_OK / _DAMAGED / _UNREADABLE
             printf("\n");
             for (const auto& ch : got)
@@ -62,6 +66,12 @@ int main(int argc, char** argv) {
                     hex_line(*ch, i, line);
                     fwrite(line.data(), 1, line.size(), stdout);
                 }
+            if (rewrite) {
+                FILE* f = fopen(rewrite, "ab");
+                if (!f) return 1;
+                fprintf(f, "added-after-pass-%d\n", pass);
+                fclose(f);
+            }
         }
         return 0;
     }
