@@ -198,6 +198,7 @@ struct Device {
     hipEvent_t head_end = nullptr;  // check path: this context's last PBKDF2 head (the device's head fence)
     PinnedArena stage;            // check path: host staging of the derive uploads
     MappedHost hits_host;         // check path: hit count + hits written by k_hits_out
+    TableBuilder tb;              // check path: line and attempt tables of the current call (capacity kept)
     std::mutex mu;
     Batch batch;
     DevBuf lines, atts, pool, segs, segs_tail, salt;
@@ -967,7 +968,14 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     tr.mark("slots");
 
     // The first chunk's PBKDF2 is queued before the line tables exist: the host builds them while the GPU derives.
-    TableBuilder tb;
+    // The builder is the context's (cleared, capacity kept): a fresh one per call mapped and zero-faulted its
+    // ~7 MB of attempt records every call and unmapped them on return.
+    TableBuilder& tb = d.tb;
+    tb.lines.clear();
+    tb.atts.clear();
+    tb.pool.clear();
+    tb.never.clear();
+    tb.att_kw_all = false;
     std::vector<uint32_t> job_line(njobs, 0);
     std::vector<HitDev> hits;
     const size_t chunk = default_batch();
