@@ -197,6 +197,38 @@ def test_parallel_inflate_matches_zlib(tool, tmp_path):
     assert all(v[v.index("stop") + 1] == "none" for k, v in info.items()), info
 
 
+def test_parallel_inflate_false_boundary_falls_back(tool, tmp_path):
+    """A boundary search can find a position that starts a perfectly valid dynamic block which is not a block of this
+    stream: here stored blocks carry the raw bytes of another deflate stream, so the search in later chunks finds
+    that nested stream's blocks.  The chunk before it must then fail to land on the find, the parallel decode stop
+    at that point, and gzread continue: the output is still exactly zlib's and the stop reason is a boundary
+    mismatch, not damage."""
+    rng = random.Random(15)
+    txt = _words(rng, 120_000)
+    nested = _raw_deflate(txt, level=6)
+    plain = gzip.compress(txt[:200_000], compresslevel=6)
+    cases = {
+        # stored blocks only: every find is false, chunk 0 runs into the first one
+        "stored_nested.gz": _member(txt[:100_000] + nested + txt[:50_000], level=0),
+        # a real dynamic stream, then a stored member whose payload is another stream's deflate bytes
+        "mixed_nested.gz": plain + _member(nested + txt[:30_000], level=0),
+    }
+    paths = []
+    for name, blob in cases.items():
+        p = tmp_path / name
+        p.write_bytes(blob)
+        paths.append(p)
+    for threads in (1, 4):
+        rc, lines = _prun(tool, paths, threads)
+        for p in paths:
+            assert lines[str(p)].startswith("ok "), (threads, p.name, lines[str(p)])
+        assert rc == 0
+        stops = {p.name: lines[str(p)].split(" stop ", 1)[1] for p in paths}
+        assert stops["stored_nested.gz"] != "none", stops  # the nested blocks were found and rejected
+        for reason in stops.values():
+            assert reason == "none" or "boundary" in reason or "chunk" in reason, stops
+
+
 def test_parallel_inflate_damaged_like_gzread(tool, tmp_path):
     """Damage inside a parallel decode: a cut stream yields exactly gzread's bytes (the reader hands over to gzread
     after what was delivered); a corrupt trailer or body yields at least gzread's bytes and fails."""
