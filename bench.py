@@ -4,8 +4,9 @@ Workload (per GPU): one ESSID, one EAPOL keyver-2 hashline (message_pair 0x80, p
 hashcat nonce mode --nonce-error-corrections=8 -> 33 attempts, as help_crack.py:773 runs it), a 100M-word
 synthetic dictionary resident in HBM (uint64 offsets + bytes, lengths geometric around 10 clipped to [8, 63];
 the true PSK is word 99,999,000).  A step = one batch
-of the dictionary through the hot path: candidates -> HMAC midstates -> PBKDF2 -> verify.  Rank r of N scans
-batches r, r+N, ... (static keyspace shards, no collective on the data path): weak scaling.
+of the dictionary through the hot path: candidates -> HMAC midstates -> PBKDF2 -> verify.  Rank r of N scans its
+own 100M-word shard of an N x 100M-word node dictionary (rank 0's is the one above; no two ranks derive the same
+PMK, no collective on the data path): weak scaling.
 
 The JSON line carries the PBKDF2 kernel's roofline (integer VALU bound) from HIP events recorded around each
 launch on the stream it runs on, and the CPU baseline (the OpenSSL restatement of check_key_m22000 from
@@ -113,8 +114,32 @@ def parse():
     return ap.parse_args()
 
 
+_JSON_FD = None
+
+
+def quiet_stdout() -> None:
+    """Keep stdout for the one JSON line: fd 1 goes to stderr from here on (gloo prints its connection banner and
+    runtimes may print notices there) and emit() writes the line to the original stdout."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj) -> None:
+    data = (json.dumps(obj) + "\n").encode()
+    if _JSON_FD is None:
+        sys.stdout.write(data.decode())
+        sys.stdout.flush()
+        return
+    while data:
+        data = data[os.write(_JSON_FD, data):]
+
+
 def make_dictionary(n, seed=2):
-    """Host-side synthetic dictionary in the HBM layout (uint64 offsets + bytes), lengths geometric(0.3)+7 -> [8, 63]."""
+    """Host-side synthetic dictionary in the HBM layout (uint64 offsets + bytes), lengths geometric(0.3)+7 -> [8, 63].
+    Weak scaling gives rank r the seed 2 + r: its own shard of the node dictionary."""
     import numpy as np
     rng = np.random.default_rng(seed)
     lens = np.clip(rng.geometric(0.3, n) + 7, 8, 63).astype(np.uint64)
@@ -130,13 +155,15 @@ class Workload:
     description = ""
 
 
-def build_c2(args, local, S, Scan, Dictionary):
-    """configs[1]: one ESSID, one EAPOL keyver-2 line, 100M-word dictionary."""
+def build_c2(args, local, S, Scan, Dictionary, shard=0):
+    """configs[1]: one ESSID, one EAPOL keyver-2 line, 100M-word dictionary.  Shard r (weak scaling, rank r) is its
+    own 100M-word dictionary (seed 2 + r) with its own planted PSK at the same index, so the ranks' (ESSID, word)
+    units are disjoint."""
     import random
     w = Workload()
     n = args.dict_words
     w.plant = min(PLANT_INDEX, n - 1)
-    w.off, w.data = make_dictionary(n)
+    w.off, w.data = make_dictionary(n, seed=2 + shard)
     w.psk = w.data[int(w.off[w.plant]):int(w.off[w.plant + 1])].tobytes()
     rng = random.Random(1)
     w.essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
@@ -149,7 +176,8 @@ def build_c2(args, local, S, Scan, Dictionary):
     w.name = "C2"
     w.description = ("C2: one ESSID, one EAPOL keyver-2 line (mp 0x80, planted NC +3 LE), 100M-word synthetic "
                      "dictionary resident in HBM, hashcat nonce mode --nonce-error-corrections=8 (33 attempts)")
-    w.extra = {"dict_words": n}
+    w.extra = {"dict_words": n, "shards": "weak: rank r scans its own dict_words-word shard (seed 2 + r) of the node "
+                                         "dictionary, one batch per step"}
 
     def load(i, hs, sc):
         first = (i % w.nbatches) * w.B
@@ -172,13 +200,14 @@ def build_c2(args, local, S, Scan, Dictionary):
     return w
 
 
-def build_c4(args, local, S, Scan, Dictionary):
-    """configs[3]: 8-digit numeric keyspace 00000000..99999999 generated in-kernel, one ESSID (PMKID line)."""
+def build_c4(args, local, S, Scan, Dictionary, shard=0):
+    """configs[3]: 8-digit numeric keyspace 00000000..99999999 generated in-kernel, one ESSID (PMKID line).  Weak
+    scaling gives rank r its own ESSID (shard r), strong scaling splits shard 0's keyspace."""
     import random
     w = Workload()
     n = 10 ** 8
     w.plant = 73019412
-    rng = random.Random(3)
+    rng = random.Random(3 if shard == 0 else 3000 + shard)
     w.essid, ap, sta, an, sn = S.random_net(rng, essid_len=8)
     w.line = S.pmkid_line(b"%08d" % w.plant, w.essid, ap, sta)
     w.B = (args.batch + 63) & ~63
@@ -187,7 +216,7 @@ def build_c4(args, local, S, Scan, Dictionary):
     w.groups = 1
     w.name = "C4"
     w.description = "C4: 8-digit numeric keyspace (10^8) generated on the GPU, one ESSID, PMKID line"
-    w.extra = {"keyspace": n}
+    w.extra = {"keyspace": n, "shards": "weak: rank r scans the keyspace of its own ESSID, one batch per step"}
 
     def load(i, hs, sc):
         first = (i % w.nbatches) * w.B
@@ -204,15 +233,17 @@ def build_c4(args, local, S, Scan, Dictionary):
     return w
 
 
-def build_c3(args, local, S, Scan, Dictionary):
+def build_c3(args, local, S, Scan, Dictionary, shard=0):
     """configs[2]: 10k-word dictionary x WPA rule set amplified on the GPU, across E ESSIDs with 1-4 lines each;
-    each PMK is derived once per ESSID x candidate and tested against every line of that ESSID."""
+    each PMK is derived once per ESSID x candidate and tested against every line of that ESSID.  Weak scaling gives
+    rank r its own E ESSIDs (shard r; same words, rules and planted PSKs)."""
     import random
     from dwpa_amd.rulesets import wpa_rules
     from dwpa_amd.device import dictionary_arrays
     import dwpa_amd
     w = Workload()
     rng = random.Random(4)
+    net_rng = rng if shard == 0 else random.Random(4000 + shard)
     base = [S.random_psk(rng, 6, 12) for _ in range(10000)]
     rules = wpa_rules()
     picks = [(rng.randrange(len(base)), rng.randrange(len(rules))) for _ in range(4 * args.essids)]
@@ -221,7 +252,7 @@ def build_c3(args, local, S, Scan, Dictionary):
     w.dict = Dictionary(w.off, w.data, device=local)
     lines, w.plants = [], []
     for e in range(args.essids):
-        essid, ap, sta, an, sn = S.random_net(rng)
+        essid, ap, sta, an, sn = S.random_net(net_rng)
         for k in range(rng.randint(1, 4)):
             wi, ri = picks[4 * e + k]
             psk = expanded[4 * e + k][ri]
@@ -245,7 +276,8 @@ def build_c3(args, local, S, Scan, Dictionary):
     w.name = "C3"
     w.description = (f"C3: 10k-word dictionary x {w.nrules} WPA rules amplified on the GPU (8..63 filter), "
                      f"{w.groups} ESSIDs x 1-4 lines, one PMK per ESSID x candidate")
-    w.extra = {"essids": w.groups, "lines": len(lines), "rules": w.nrules}
+    w.extra = {"essids": w.groups, "lines": len(lines), "rules": w.nrules,
+               "shards": "weak: rank r scans the candidates against its own ESSIDs, one batch per step"}
 
     def load(i, hs, sc):
         first = (i % w.nbatches) * w.words_per_step
@@ -330,7 +362,7 @@ def spawn_ranks(args) -> int:
         try:
             obj = json.loads(ln)
         except ValueError:
-            print(ln, flush=True)
+            print(ln, file=sys.stderr, flush=True)
             continue
         result = obj
     if rc != 0:
@@ -340,7 +372,7 @@ def spawn_ranks(args) -> int:
         print(f"bench.py: --gpus {args.gpus} but rank 0 reported "
               f"{None if result is None else result.get('n_gpus')} ranks", file=sys.stderr)
         return 4
-    print(json.dumps(result), flush=True)
+    emit(result)
     return 0
 
 
@@ -357,6 +389,7 @@ def main():
     args = parse()
     if os.environ.get("WORLD_SIZE") is None and (args.gpus or 1) > 1:
         sys.exit(spawn_ranks(args))
+    quiet_stdout()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus is not None and args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -392,10 +425,10 @@ def main():
     import dwpa_amd
     from dwpa_amd import synth as S
     from dwpa_amd.device import Dictionary, Event, Stream
-    from dwpa_amd.shard import batch_ids, reduce_timing
+    from dwpa_amd.shard import reduce_timing, weak_units
 
     build = {"c2": build_c2, "c3": build_c3, "c4": build_c4}[args.workload]
-    w = build(args, local, S, dwpa_amd.Scan, Dictionary)
+    w = build(args, local, S, dwpa_amd.Scan, Dictionary, shard=rank)
     # pipeline slot k: its own scan working set (batch buffers, hit buffer) and stream; batch s goes to slot
     # s % P, so batch s+1's PBKDF2 is queued while batch s's verify still runs
     P = len(w.scans)
@@ -425,7 +458,7 @@ def main():
         sc.verify(0, hs)
         return cnt
 
-    for s, b in enumerate(batch_ids(rank, world, 0, args.warmup, w.nbatches)):
+    for s, (_, b) in enumerate(weak_units(rank, 0, args.warmup, w.nbatches)):
         step(b, s % P)
     sync_all()
     for k in range(P):
@@ -438,7 +471,7 @@ def main():
     t0 = time.perf_counter()
     done = 0
     counts = []
-    for s, b in enumerate(batch_ids(rank, world, args.warmup, args.steps, w.nbatches)):
+    for s, (_, b) in enumerate(weak_units(rank, args.warmup, args.steps, w.nbatches)):
         counts.append(step(b, s % P, kev[s]))
         done += counts[-1]
     sync_all()
@@ -521,7 +554,7 @@ def main():
             "rank0_local_s": round(elapsed_local, 4),
             "pipeline": P,
         }
-        print(json.dumps(result), flush=True)
+        emit(result)
     for sc in w.scans:
         sc.close()
     if world > 1:
@@ -533,11 +566,11 @@ def main():
 
 def main_dry(args, world, rank):
     """--dry-run: the N-rank control path with no GPU.  Every rank builds the shard schedule its workload would
-    scan (weak: dictionary/keyspace batches r, r+N, ... of the timed steps; strong c4: its contiguous keyspace
+    scan (weak: (its own shard r, batch) of every timed step; strong c4: its contiguous keyspace
     range), then the gloo barrier and the max/sum reductions run as in a measured run; rank 0 prints the coverage
     of every rank.  tests/test_bench_spawn.py checks N ranks and disjoint coverage through `--gpus N`."""
     import torch.distributed as dist
-    from dwpa_amd.shard import batch_ids, reduce_timing, strong_batches
+    from dwpa_amd.shard import reduce_timing, strong_batches, weak_units
     if world > 1:
         dist.init_process_group("gloo")
     B = (args.batch + 63) & ~63
@@ -547,7 +580,7 @@ def main_dry(args, world, rank):
     else:
         n = 10 ** 8 if args.workload == "c4" else args.dict_words
         nb = (n + B - 1) // B
-        mine = batch_ids(rank, world, args.warmup, args.steps, nb)
+        mine = [list(u) for u in weak_units(rank, args.warmup, args.steps, nb)]
         units = len(mine) * B
     gathered = [mine]
     if world > 1:
@@ -558,10 +591,10 @@ def main_dry(args, world, rank):
     else:
         total = float(units)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "PMK/s", "n_gpus": world, "steps": args.steps,
+        emit({"metric": METRIC, "value": None, "unit": "PMK/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "dry_run": True, "scaling": args.scaling,
                           "config": {"workload": args.workload, "batch_per_step": B},
-                          "units_all_ranks": total, "coverage": gathered, "pid": os.getpid()}), flush=True)
+                          "units_all_ranks": total, "coverage": gathered, "pid": os.getpid()})
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -639,7 +672,7 @@ def main_strong(args, world, rank, local):
             cpu = cpu_baseline(w.cpu_line, w.cpu_keys, args.cpu_seconds, w.cpu_what)
         pmk_per_launch = sum(c for _, c in sched) / len(sched)
         traffic_pmk = TRAFFIC_BYTES_PER_PMK["c4"]
-        print(json.dumps({
+        emit({
             "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
@@ -664,7 +697,7 @@ def main_strong(args, world, rank, local):
                                               / PEAK_LANE_OPS, 4)},
             "cpu_baseline": cpu, "hits_verified": verified,
             "hits_checked": "the planted PSK 73019412 with its PMK, once per timed pass, on the rank holding it; "
-                            "no other hit on any rank"}), flush=True)
+                            "no other hit on any rank"})
     sc.close()
     if world > 1:
         dist.barrier()
@@ -761,7 +794,7 @@ def main_ffi(args, world, rank, local):
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline_jobs(jobs, args.cpu_seconds)
-        print(json.dumps({
+        emit({
             "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
@@ -771,8 +804,7 @@ def main_ffi(args, world, rank, local):
             "hits": sum(1 for g in got if g),
             "mismatches": mismatches if args.workload == "c5" else None,
             "hits_checked": "every job's result against its planted key's [PSK, NC, endian, PMK] (re-derived by the "
-                            "CPU oracle) or False" if args.workload == "c5" else "the planted PSK and its PMK"}),
-              flush=True)
+                            "CPU oracle) or False" if args.workload == "c5" else "the planted PSK and its PMK"})
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -840,12 +872,12 @@ def main_latency(args, world, rank, local):
                  "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp})
     ok = all(r["same_result"] for r in rows)
     if rank == 0:
-        print(json.dumps({"metric": "ms per server check call (latency), m22000", "value": rows[0]["gpu_ms_per_call"],
+        emit({"metric": "ms per server check call (latency), m22000", "value": rows[0]["gpu_ms_per_call"],
                           "unit": "ms", "n_gpus": world, "steps": reps, "warmup": 1, "higher_is_better": False,
                           "dtype": "u32", "data": "synthetic",
                           "config": {"workload": "C1 latency: FFI calls of 1/16/202 keys (put_work, common.php:902,"
                                                  "937) beside one CPU core", "parallelism": "none"},
-                          "rows": rows, "cpu_model": host_cpu()["cpu_model"], "hits_verified": ok}), flush=True)
+                          "rows": rows, "cpu_model": host_cpu()["cpu_model"], "hits_verified": ok})
     if rank == 0 and not ok:
         sys.exit(3)
 
@@ -920,7 +952,7 @@ def main_files(args, world, rank, local):
     else:
         total = float(words)
     if rank == 0:
-        print(json.dumps({
+        emit({
             "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
@@ -934,7 +966,7 @@ def main_files(args, world, rank, local):
                                      "DictCache (no inflate)" if os.environ.get("DWPA_DICT_CACHE_MB", "") != "0"
                                      else "off"},
             "pass_s": all_passes,
-            "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked), "reader": reader}), flush=True)
+            "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked), "reader": reader})
     for x in (dpath, hpath, opath):
         if os.path.exists(x):
             os.remove(x)

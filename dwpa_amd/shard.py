@@ -1,16 +1,18 @@
 """Static keyspace sharding shared by bench.py and the multi-rank tests.
 
-Every (ESSID, candidate) PMK is independent, so shards never exchange data: rank r of N scans batches
-r, r+N, r+2N, ... of the dictionary (weak scaling: fixed work per GPU per step), and crack_files splits every
-dictionary chunk into N contiguous equal ranges (dwpa_amd/csrc/crack.cpp).  The only cross-rank traffic is the
-bench's control plane: a barrier around the timed region, the max elapsed time and the total PMK count.
+Every (ESSID, candidate) PMK is independent, so shards never exchange data.  Weak scaling (fixed work per GPU per
+step): rank r of N owns shard r of the node's workload -- its own dictionary, ESSID set or ESSID -- so no two ranks
+ever derive the same (ESSID, candidate) PMK however many ranks there are, and scans its shard batch by batch.
+Strong scaling and crack_files split one keyspace or dictionary chunk into N contiguous equal ranges
+(dwpa_amd/csrc/crack.cpp).  The only cross-rank traffic is the bench's control plane: a barrier around the timed
+region, the max elapsed time and the total PMK count.
 """
 from __future__ import annotations
 
 
-def batch_ids(rank: int, world: int, first_step: int, steps: int, nbatches: int):
-    """Dictionary batch index of each step of `rank` (step s -> batch (rank + s*world) mod nbatches)."""
-    return [(rank + s * world) % nbatches for s in range(first_step, first_step + steps)]
+def weak_units(rank: int, first_step: int, steps: int, nbatches: int):
+    """(shard, batch) scanned by `rank` at each step: its own shard, step s -> batch s mod nbatches."""
+    return [(rank, s % nbatches) for s in range(first_step, first_step + steps)]
 
 
 def contiguous_shard(n: int, k: int, g: int):

@@ -7,7 +7,7 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from dwpa_amd.shard import batch_ids, contiguous_shard, reduce_timing
+from dwpa_amd.shard import contiguous_shard, reduce_timing, weak_units
 
 
 def _free_port():
@@ -22,7 +22,7 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ids = batch_ids(rank, world, 2, 8, 24)
+    ids = weak_units(rank, 2, 8, 6)
     gathered = [None] * world
     dist.all_gather_object(gathered, ids)
     dist.barrier()
@@ -46,16 +46,20 @@ def test_shards_disjoint_and_reductions(world):
     for rank, gathered, el, tot in res:
         assert el == float(world)                     # max over ranks
         assert tot == 100 * world * (world + 1) / 2   # sum over ranks
-        # within a step, ranks scan distinct batches
-        for s in range(8):
-            step_batches = [g[s] for g in gathered]
-            assert len(set(step_batches)) == world
+        # every rank scans its own shard, so no (shard, batch) unit is scanned by two ranks, even with more ranks
+        # than batches per shard (8 ranks of a 6-batch dictionary on a node)
+        for r, g in enumerate(gathered):
+            assert all(tuple(u)[0] == r for u in g)
+        units = [tuple(u) for g in gathered for u in g[:6]]
+        assert len(set(units)) == len(units)
 
 
-def test_batch_schedule_covers_keyspace():
-    n, world = 24, 4
-    seen = sorted(b for r in range(world) for b in batch_ids(r, world, 0, n // world, n))
-    assert seen == list(range(n))
+def test_weak_schedule_covers_each_shard():
+    nb = 6
+    for world in (1, 2, 8):
+        for r in range(world):
+            units = weak_units(r, 0, nb, nb)
+            assert sorted(b for _, b in units) == list(range(nb)) and {s for s, _ in units} == {r}
 
 
 def test_contiguous_shards():
