@@ -6,12 +6,15 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/legs}
 mkdir -p $OUT
-LEGS=${LEGS:-"peak c2 c4 c3 c5 c5k2 c1 c2files c2files_warm"}
+LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm"}
 for leg in $LEGS; do
   case $leg in
     peak)    OUT=$OUT/peak tools/regen_peak.sh > /dev/null ;;
     c2)      timeout -k 10 240 python3 bench.py --steps 8 --warmup 2 > $OUT/c2.json 2> $OUT/c2.err ;;
     c4)      timeout -k 10 240 python3 bench.py --workload c4 --steps 8 --warmup 2 > $OUT/c4.json 2> $OUT/c4.err ;;
+    c4strong) timeout -k 10 240 python3 bench.py --workload c4 --scaling strong --steps 2 --warmup 1 --no-cpu-baseline \
+               > $OUT/c4strong.json 2> $OUT/c4strong.err ;;
+    c1lat)   timeout -k 10 240 python3 bench.py --workload c1lat --steps 9 > $OUT/c1lat.json 2> $OUT/c1lat.err ;;
     c3)      timeout -k 10 300 python3 bench.py --workload c3 --steps 4 --warmup 1 > $OUT/c3.json 2> $OUT/c3.err ;;
     c5)      timeout -k 10 240 python3 bench.py --workload c5 --steps 20 --warmup 3 > $OUT/c5.json 2> $OUT/c5.err ;;
     c5k2)    timeout -k 10 240 python3 bench.py --workload c5 --callers 2 --steps 20 --warmup 3 --no-cpu-baseline \
