@@ -109,6 +109,46 @@ def test_random_batch_vs_oracle():
     assert sum(1 for e in exp if e) > 60
 
 
+def test_mutated_lines_vs_oracle():
+    """Parse semantics by mutation (tests/mutate.py): 1,500 valid PMKID/keyver 1/2/3 lines with one or two random
+    mutations each (type field spellings, dropped/inserted/replaced characters, upper-case fields, odd or short or
+    long hex fields, extra/missing/empty fields, key-version bits, EAPOL frames around the 49-byte unpack), the
+    planted key among decoys, nc in {0, 1, 8, -3, 6}.  One batch call and one call per job for the first 200 must
+    equal the oracle exactly, whether the line was rejected, stopped matching or stayed valid."""
+    from tests.mutate import mutated_jobs
+    jobs = mutated_jobs(2, 1500)
+    exp = _oracle_many(jobs)
+    got = dwpa_amd.check_batch(jobs)
+    mism = [(i, jobs[i][0], g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    assert not mism, mism[:3]
+    for i in range(200):
+        assert dwpa_amd.check_key_m22000(*jobs[i]) == exp[i], jobs[i][0]
+    assert sum(1 for e in exp if e) > 100
+
+
+def test_long_eapol_frames_vs_oracle():
+    """EAPOL frames up to the longest a hashline can carry: nets.struct is varchar(2000) (db/wpa.sql:162), so a
+    frame has at most ~900 bytes -- 15 SHA-1/MD5 blocks, 57 CMAC blocks.  Keyver 1/2/3 at 99..900 bytes, hits at
+    +-nc in both endians and decoys, through the key-parallel (nc 8) and attempt-parallel (nc 128) verifiers, in
+    one batch and per job."""
+    rng = random.Random(61)
+    jobs = []
+    for el in (99, 100, 111, 112, 119, 120, 128, 175, 176, 255, 256, 400, 512, 777, 900):
+        for kv in (1, 2, 3):
+            essid, ap, sta, an, sn = S.random_net(rng)
+            psk = S.random_psk(rng)
+            nc = rng.choice([8, 128])
+            off = rng.choice([0, 1, -1, 4, -4]) if nc == 8 else rng.choice([0, 30, -65, 65])
+            line = S.eapol_line(psk, essid, ap, sta, an, sn, kv, off, rng.choice(["LE", "BE"]), eapol_len=el, rng=rng)
+            assert len(line) <= 2000 or el > 900
+            jobs.append((line, [S.random_psk(rng), psk, S.random_psk(rng)], False, nc))
+    exp = _oracle_many(jobs)
+    assert all(exp)
+    assert dwpa_amd.check_batch(jobs) == exp
+    for j, e in zip(jobs, exp):
+        assert dwpa_amd.check_key_m22000(*j) == e
+
+
 def test_scan_dictionary_hbm():
     from dwpa_amd.device import Dictionary
     rng = random.Random(3)
