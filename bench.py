@@ -107,6 +107,10 @@ def parse():
     ap.add_argument("--short-words", action="store_true",
                     help="c2files: lengths geometric(0.3)+6 so ~30 %% of the words are shorter than 8 and dropped "
                          "by the m22000 filter (as in real wordlists); PMK/s counts only 8..63-byte words")
+    ap.add_argument("--start-at", type=float, default=None,
+                    help="c1/c5: after the warmup, wait until this Unix time before the timed calls, so that separate "
+                         "bench processes on one GPU (PHP-FPM workers) time the same window; the line then carries "
+                         "the window's Unix start and end")
     ap.add_argument("--callers", type=int, default=1,
                     help="c1/c5: concurrent callers (host threads, as PHP ZTS workers or a threaded server), each "
                          "making the step's call on its own argument block; the library runs up to "
@@ -755,13 +759,16 @@ def main_ffi(args, world, rank, local):
         batch.run()
     if world > 1:
         dist.barrier()
+    if args.start_at:
+        time.sleep(max(0.0, args.start_at - time.time()))
     go.wait()
-    t0 = time.perf_counter()
+    t0, u0 = time.perf_counter(), time.time()
     for _ in range(args.steps):
         batch.run()
     for t in threads:
         t.join()
     elapsed = time.perf_counter() - t0
+    window = [round(u0, 4), round(u0 + elapsed, 4)]
     if errors:
         raise errors[0]
     keys_all = float(batch.nkeys * args.steps * callers)
@@ -803,6 +810,7 @@ def main_ffi(args, world, rank, local):
             "roofline": None, "cpu_baseline": cpu, "hits_verified": verified,
             "hits": sum(1 for g in got if g),
             "mismatches": mismatches if args.workload == "c5" else None,
+            "window_unix": window,
             "hits_checked": "every job's result against its planted key's [PSK, NC, endian, PMK] (re-derived by the "
                             "CPU oracle) or False" if args.workload == "c5" else "the planted PSK and its PMK"})
     if world > 1:
