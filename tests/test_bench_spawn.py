@@ -76,3 +76,22 @@ def test_launcher_world_size_must_match_gpus():
 def test_strong_scaling_only_for_c4():
     r = _bench("--dry-run", "--scaling", "strong")
     assert r.returncode != 0
+
+
+def test_torchrun_launcher_form():
+    """The driver's N>1 command: `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr
+    127.0.0.1 --master-port P bench.py --gpus N ...`.  Each rank reads WORLD_SIZE/RANK from the launcher (no
+    spawn), and stdout carries rank 0's JSON line alone."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, env=env, timeout=180, cwd=ROOT)
+    out = _line(r)
+    assert out["n_gpus"] == 2 and len(out["coverage"]) == 2 and out["pid"] != os.getpid()
