@@ -18,6 +18,8 @@ Rules (comma-separated, applied in the loop body only):
   before_alb / before_ad3  s_nop before every alignbit / add3
   before_full_trans  s_nop before a 2-cycle VALU that follows a 4-cycle VALU
   nop1            use s_nop 1 instead of s_nop 0
+  split_add3      rewrite every v_add3_u32 as two v_add_u32_e32 (same adds, mod 2^32; 4-cycle op -> two 2-cycle
+                  ops), applied before the nop rules (A/B: fewer half-rate ops in the stream)
   none            copy through
 """
 import re
@@ -47,8 +49,41 @@ def main_loop_range(lines, kernel):
     return best
 
 
+def _vgpr(x):
+    return re.fullmatch(r"v\d+", x) is not None
+
+
+def split_add3(line):
+    """v_add3_u32 D, A, B, C -> v_add_u32_e32 D, X, Y ; v_add_u32_e32 D, Z, D.  The first add takes every operand
+    that is D itself (it is overwritten), and VOP2 takes a non-VGPR operand only as src0.  Returns the lines, or None
+    when the operands do not fit that form (the line is then kept as it is)."""
+    m = re.match(r"(\s+)v_add3_u32\s+(v\d+),\s*(\S+),\s*(\S+),\s*(\S+)\s*$", line)
+    if not m:
+        return None
+    ind, d, ops = m.group(1), m.group(2), list(m.groups()[2:])
+    if sum(1 for o in ops if not _vgpr(o)) > 1:
+        return None
+    # the operand left for the second add: never D (it is overwritten by the first), preferably the non-VGPR one
+    cand = [i for i, o in enumerate(ops) if o != d]
+    if not cand:  # D + D + D
+        return None
+    z = next((i for i in cand if not _vgpr(ops[i])), cand[-1])
+    x, y = [o for i, o in enumerate(ops) if i != z]
+    if not _vgpr(y):
+        x, y = y, x
+    if not _vgpr(y):
+        return None
+    return [f"{ind}v_add_u32_e32 {d}, {x}, {y}", f"{ind}v_add_u32_e32 {d}, {ops[z]}, {d}"]
+
+
 def nopify(lines, kernel, rules):
     h, e, nv = main_loop_range(lines, kernel)
+    if "split_add3" in rules:
+        body = []
+        for l in lines[h + 1:e]:
+            body += split_add3(l) or [l]
+        lines = lines[:h + 1] + body + lines[e:]
+        e = h + 1 + len(body)
     sys.stderr.write(f"issue_pass: {kernel}: main loop {nv} VALU, rules {','.join(rules)}\n")
     out = lines[:h + 1]
     k = 0
