@@ -20,6 +20,9 @@ Rules (comma-separated, applied in the loop body only):
   nop1            use s_nop 1 instead of s_nop 0
   split_add3      rewrite every v_add3_u32 as two v_add_u32_e32 (same adds, mod 2^32; 4-cycle op -> two 2-cycle
                   ops), applied before the nop rules (A/B: fewer half-rate ops in the stream)
+  sched=D[:alt]   list-schedule the loop body again (VGPR/SGPR/SCC dependences kept, registers unchanged) so that an
+                  instruction issues at least D VALU slots after the producers of its operands where the dependences
+                  allow; `alt` also prefers alternating 2-/4-cycle ops.  Applied before the nop rules (A/B)
   none            copy through
 """
 import re
@@ -76,8 +79,97 @@ def split_add3(line):
     return [f"{ind}v_add_u32_e32 {d}, {x}, {y}", f"{ind}v_add_u32_e32 {d}, {ops[z]}, {d}"]
 
 
+_REG = re.compile(r"^(v\d+|s\d+|vcc|exec|scc)$")
+
+
+def _defs_uses(line):
+    """(op, defs, uses) of one loop-body instruction; None for a line that is not an instruction."""
+    m = re.match(r"\s+([vs]_\w+)\s*(.*)", line)
+    if not m:
+        return None
+    op = m.group(1)
+    toks = [t.strip().split()[0] for t in m.group(2).split(",") if t.strip()]
+    regs = [t if _REG.match(t) else None for t in toks]
+    if op.startswith("v_"):
+        if not regs or regs[0] is None or not regs[0].startswith("v"):
+            raise ValueError(f"unexpected VALU form: {line!r}")
+        return op, {regs[0]}, {r for r in regs[1:] if r}
+    if op.startswith("s_cmp"):
+        return op, {"scc"}, {r for r in regs if r}
+    if op in ("s_add_i32", "s_sub_i32", "s_add_u32", "s_sub_u32"):
+        return op, {regs[0], "scc"}, {r for r in regs[1:] if r}
+    raise ValueError(f"unexpected instruction in the loop body: {line!r}")
+
+
+def reschedule(body, dmin, alt):
+    """Greedy list schedule of a straight-line loop body (see the sched rule)."""
+    ins = []
+    for l in body:
+        du = _defs_uses(l)
+        if du:
+            ins.append((l,) + du)
+    n = len(ins)
+    preds = [set() for _ in range(n)]
+    raw = [set() for _ in range(n)]
+    last_w, readers = {}, {}
+    for i, (_, op, defs, uses) in enumerate(ins):
+        for r in uses:
+            if r in last_w:
+                preds[i].add(last_w[r])
+                raw[i].add(last_w[r])
+        for r in defs:
+            if r in last_w:
+                preds[i].add(last_w[r])
+            for j in readers.get(r, ()):
+                if j != i:
+                    preds[i].add(j)
+        for r in uses:
+            readers.setdefault(r, set()).add(i)
+        for r in defs:
+            last_w[r] = i
+            readers[r] = set()
+    salu = [i for i in range(n) if ins[i][1].startswith("s_")]
+    for i in salu:  # the loop counter stays at the end, next to the branch
+        for j in range(n):
+            if j not in salu and (ins[i][2] & (ins[j][2] | ins[j][3]) - {"scc"}):
+                raise ValueError("a VALU touches the loop counter")
+    succs = [[] for _ in range(n)]
+    for i in range(n):
+        for j in preds[i]:
+            succs[j].append(i)
+    cp = [0] * n  # longest path to the end (critical path)
+    for i in range(n - 1, -1, -1):
+        cp[i] = 1 + max((cp[j] for j in succs[i]), default=0)
+    left = [len(preds[i]) for i in range(n)]
+    ready = {i for i in range(n) if not left[i] and i not in salu}
+    pos, order, prev_half = {}, [], None
+    while ready:
+        def key(i):
+            dist = min((len(order) - pos[j] for j in raw[i]), default=dmin)
+            half = ins[i][1].replace("_e32", "").replace("_e64", "") in HALF
+            return (min(dist, dmin), alt and prev_half is not None and half != prev_half, cp[i], -i)
+        i = max(ready, key=key)
+        ready.discard(i)
+        pos[i] = len(order)
+        order.append(i)
+        prev_half = ins[i][1].replace("_e32", "").replace("_e64", "") in HALF
+        for j in succs[i]:
+            left[j] -= 1
+            if not left[j] and j not in salu:
+                ready.add(j)
+    if len(order) + len(salu) != n:
+        raise ValueError("schedule incomplete")
+    return [ins[i][0] for i in order + salu]
+
+
 def nopify(lines, kernel, rules):
     h, e, nv = main_loop_range(lines, kernel)
+    for r in rules:
+        if r.startswith("sched="):
+            arg = r.split("=", 1)[1].split(":")
+            body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:])
+            lines = lines[:h + 1] + body + lines[e:]
+            e = h + 1 + len(body)
     if "split_add3" in rules:
         body = []
         for l in lines[h + 1:e]:
