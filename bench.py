@@ -96,10 +96,14 @@ def parse():
                     help="batches in flight (c2/c3/c4), each on its own scan working set and HIP stream.  Measured "
                          "A/B (profiles/r01/pipeline/): 2 gains 0.2 %% -- the next batch's PBKDF2 waves hold the "
                          "SIMDs, so the verify runs starved beside it -- and blurs the per-kernel events; default 1")
-    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files", "c1lat"], default="c2",
+    ap.add_argument("--rule-words", type=int, default=1_000_000,
+                    help="c3files: base words of the gz dictionary the WPA rule set is applied to")
+    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files", "c3files", "c1lat"], default="c2",
                     help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs; "
                          "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
-                         "dwpa_crack_files from a gz dictionary on disk (the help_crack client path); c1lat = "
+                         "dwpa_crack_files from a gz dictionary on disk (the help_crack client path); c3files = "
+                         "the client's rule pass: a gz dictionary x the WPA rule set through dwpa_crack_files; "
+                         "c1lat = "
                          "server call latency at 1/16/202 keys per call beside one CPU core")
     ap.add_argument("--essids", type=int, default=1000, help="c3: number of ESSIDs (BASELINE: 1000)")
     ap.add_argument("--scan-run", action="store_true",
@@ -418,6 +422,8 @@ def main():
         return main_ffi(args, world, rank, local)
     if args.workload == "c2files":
         return main_files(args, world, rank, local)
+    if args.workload == "c3files":
+        return main_files_rules(args, world, rank, local)
     if args.workload == "c1lat":
         return main_latency(args, world, rank, local)
     if args.scaling == "strong":
@@ -977,6 +983,103 @@ def main_files(args, world, rank, local):
             "pass_s": all_passes,
             "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked), "reader": reader})
     for x in (dpath, hpath, opath):
+        if os.path.exists(x):
+            os.remove(x)
+    os.rmdir(tmp)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0 and not cracked:
+        sys.exit(3)
+
+
+def main_files_rules(args, world, rank, local):
+    """The client's rule pass through dwpa_crack_files (help_crack.py:929-933: `-S -r <rules>` over the work
+    unit's dictionaries): a gzip dictionary of --rule-words base words (6..16
+    printable bytes) on local disk x the WPA rule set (dwpa_amd/rulesets.py, 148 rules of bestWPA.rule's ops) in a
+    rules file, amplified on the GPU, one EAPOL keyver-2 line in hashcat NC mode 8.  The planted PSK is one rule's
+    output of the 1000th-last word, so a pass covers the dictionary up to there.  PMKs counted = candidates inside
+    the 8..63 filter: every rule of the set changes a word's length as a function of that length only, so the
+    count is sum over word lengths of (words of that length) x (rules whose output length is in 8..63), taken from
+    the library's own rule expansion of one word per length.  One pass = one step; N>1 runs replicas."""
+    import gzip
+    import random
+    import tempfile
+    import numpy as np
+    import torch.distributed as dist
+    import dwpa_amd
+    from dwpa_amd import synth as S
+    from dwpa_amd.rulesets import wpa_rules
+    from dwpa_amd.shard import reduce_timing
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    n = max(2000, args.rule_words)
+    rules = wpa_rules()
+    rules_text = "\n".join(rules)
+    rng = np.random.default_rng(6)
+    lens = rng.integers(6, 17, n).astype(np.int64)
+    ends = np.cumsum(lens + 1)
+    text = rng.integers(0x21, 0x7F, int(ends[-1]), dtype=np.uint8)
+    text[text == ord("$")] = ord("%")  # no word starts a $HEX[] form
+    text[ends - 1] = 0x0A
+    plant_word = n - 1000
+    word = text[int(ends[plant_word - 1]):int(ends[plant_word]) - 1].tobytes()
+    row = dwpa_amd.rules_expand(rules_text, [word], device=local)[0]
+    good = [r for r, c in enumerate(row) if c is not None and 8 <= len(c) <= 63]
+    plant_rule = good[len(good) // 2]
+    psk = row[plant_rule]
+    # candidates inside the filter per base-word length (rule output lengths depend on the input length only)
+    reps = [bytes(b"abcdefghijklmnop"[:L]) for L in range(6, 17)]
+    per_len = {L: sum(1 for c in r if c is not None and 8 <= len(c) <= 63)
+               for L, r in zip(range(6, 17), dwpa_amd.rules_expand(rules_text, reps, device=local))}
+    counts = np.bincount(lens[:plant_word + 1], minlength=17)
+    cands = int(sum(int(counts[L]) * per_len[L] for L in range(6, 17)))
+    rr = random.Random(1)
+    essid, ap, sta, an, sn = S.random_net(rr, essid_len=10)
+    line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rr)
+    tmp = tempfile.mkdtemp(prefix="dwpa_c3files_")
+    dpath, rpath, hpath, opath = (os.path.join(tmp, x) for x in ("dict.txt.gz", "wpa.rule", "h.hash", "o.key"))
+    with gzip.open(dpath, "wb", compresslevel=6) as f:
+        f.write(text.tobytes())
+    del text
+    with open(rpath, "w") as f:
+        f.write(rules_text + "\n")
+    with open(hpath, "wb") as f:
+        f.write(line + b"\n")
+    cracked = True
+    times, all_passes = [], []
+    for rep in range(args.warmup + args.steps):
+        if os.path.exists(opath):
+            os.remove(opath)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        rc = dwpa_amd.crack_files(hpath, [dpath], rpath, 8, opath, device_mask=1 << local, batch=args.batch)
+        el = time.perf_counter() - t0
+        all_passes.append(round(el, 3))
+        if rep >= args.warmup:
+            times.append(el)
+        recs = open(opath, "rb").read().strip().split(b"\n") if os.path.exists(opath) else []
+        cracked &= rc == 0 and len(recs) == 1 and recs[0].endswith(b":" + psk)
+    elapsed = sum(times) / len(times)
+    if world > 1:
+        elapsed, total = reduce_timing(dist, elapsed, float(cands))
+    else:
+        total = float(cands)
+    if rank == 0:
+        emit({
+            "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"client rule pass via dwpa_crack_files: {n}-word gzip dictionary x {len(rules)} "
+                                   "WPA rules (rules file, amplified on the GPU, 8..63 filter), one EAPOL keyver-2 "
+                                   "line, hashcat NC mode 8", "rule_words": n, "rules": len(rules),
+                       "candidates_per_pass": cands, "batch": args.batch, "parallelism": f"replicas x{world}",
+                       "plant": [plant_word, plant_rule]},
+            "pass_s": all_passes,
+            "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked)})
+    for x in (dpath, rpath, hpath, opath):
         if os.path.exists(x):
             os.remove(x)
     os.rmdir(tmp)

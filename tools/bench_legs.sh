@@ -6,7 +6,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/legs}
 mkdir -p $OUT
-LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm"}
+LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm c3files"}
 for leg in $LEGS; do
   case $leg in
     peak)    OUT=$OUT/peak tools/regen_peak.sh > /dev/null ;;
@@ -24,6 +24,8 @@ for leg in $LEGS; do
                > $OUT/c2files.json 2> $OUT/c2files.err ;;
     c2files_warm) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c2files --steps 1 --warmup 1 \
                > $OUT/c2files_warm.json 2> $OUT/c2files_warm.err ;;
+    c3files) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --steps 2 --warmup 0 \
+               > $OUT/c3files.json 2> $OUT/c3files.err ;;
     *) echo "unknown leg $leg" >&2; exit 2 ;;
   esac
   echo "leg $leg done" >&2
