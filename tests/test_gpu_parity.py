@@ -549,6 +549,58 @@ def test_crack_files_dictionary_cache_next_work_unit(tmp_path, capfd, monkeypatc
     assert after == before + 1
 
 
+def test_crack_files_degenerate_inputs(tmp_path):
+    """Empty and ragged inputs of the client path, with hashcat's outcomes (help_crack.py:776-786): an empty plain
+    or gzip dictionary, a dictionary of words outside 8..63 only, and no dictionary at all exhaust the work unit
+    (rc 1, nothing written); a hash file that is empty or holds no valid line is hashcat's "No hashes loaded" (rc
+    -1); the 8- and 63-byte PSKs at the filter's edges are found and the 64-byte word beside them is not
+    (m22000 keys are 8..63 bytes, INSTALL.md:83); the check path returns [] for no jobs and False for no keys."""
+    rng = random.Random(71)
+    essid, ap, sta, an, sn = S.random_net(rng)
+    good = S.pmkid_line(b"edge-psk-1", essid, ap, sta)
+    hf = tmp_path / "h.hash"
+    hf.write_bytes(good + b"\n")
+    out = tmp_path / "o.key"
+
+    def run(dicts, hfile=hf):
+        if out.exists():
+            out.unlink()
+        rc = dwpa_amd.crack_files(str(hfile), [str(d) for d in dicts], None, 8, str(out))
+        recs = out.read_bytes().strip().split(b"\n") if out.exists() and out.stat().st_size else []
+        return rc, recs
+
+    empty = tmp_path / "empty.txt"
+    empty.write_bytes(b"")
+    empty_gz = tmp_path / "empty.txt.gz"
+    empty_gz.write_bytes(gzip.compress(b""))
+    ragged = tmp_path / "ragged.txt"
+    ragged.write_bytes(b"\n".join([b"", b"short", b"x" * 64, b"y" * 100, b"\r", b"1234567"]) + b"\n\n")
+    assert run([empty]) == (1, [])
+    assert run([empty_gz]) == (1, [])
+    assert run([ragged]) == (1, [])
+    assert run([]) == (1, [])
+    bad = tmp_path / "bad.hash"
+    bad.write_bytes(b"WPA*01*zz*aa*bb*cc***\nnot a hashline\n\n")
+    assert run([ragged], bad)[0] == -1
+    none = tmp_path / "none.hash"
+    none.write_bytes(b"")
+    assert run([ragged], none)[0] == -1
+    # the filter's edges: 8 and 63 bytes are candidates, 7 and 64 are not
+    p8, p63 = b"e" * 7 + b"8", bytes(rng.choice(b"abcdef0123") for _ in range(63))
+    e2, ap2, sta2, an2, sn2 = S.random_net(rng)
+    lines = [S.pmkid_line(p8, e2, ap2, sta2), S.pmkid_line(p63, e2, rng.randbytes(6), sta2),
+             S.pmkid_line(p63 + b"z", e2, rng.randbytes(6), sta2), S.pmkid_line(p8[:7], e2, rng.randbytes(6), sta2)]
+    hf2 = tmp_path / "edges.hash"
+    hf2.write_bytes(b"\n".join(lines) + b"\n")
+    edges = tmp_path / "edges.txt"
+    edges.write_bytes(b"\n".join([p8[:7], p8, p63, p63 + b"z"]) + b"\n")
+    rc, recs = run([edges], hf2)
+    assert rc == 1 and sorted(r.rsplit(b":", 1)[1] for r in recs) == sorted([p8, p63])
+    assert dwpa_amd.check_batch([]) == []
+    assert dwpa_amd.check_key_m22000(good, []) is False
+    assert dwpa_amd.check_key_m22000(good, [None]) is False
+
+
 @pytest.mark.skipif(os.environ.get("DWPA_PBKDF2_ISSUE") == "1", reason="already the forced issue-pass run")
 def test_issue_pass_kernels_at_small_sizes():
     """Launches of at most one wave per SIMD take the plain-schedule PBKDF2 kernel (pbkdf2_module.cpp), so the
