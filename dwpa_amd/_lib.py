@@ -45,6 +45,11 @@ class Config(ctypes.Structure):
                 ("nc_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
+class CrackStats(ctypes.Structure):
+    _fields_ = [("words", ctypes.c_uint64), ("candidates", ctypes.c_uint64), ("hashes", ctypes.c_uint32),
+                ("cracked", ctypes.c_uint32), ("seconds", ctypes.c_double)]
+
+
 class LineInfo(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("keyver", ctypes.c_int32), ("essid_len", ctypes.c_uint32),
                 ("mac_ap_len", ctypes.c_uint32), ("mac_sta_len", ctypes.c_uint32), ("target_len", ctypes.c_uint32),
@@ -75,6 +80,7 @@ SIGNATURES = {
     "dwpa_parse_m22000": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_void_p], ctypes.c_int),
     "dwpa_crack_files": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
                           ctypes.c_char_p, ctypes.POINTER(Config)], ctypes.c_int),
+    "dwpa_crack_last_stats": ([ctypes.POINTER(CrackStats)], ctypes.c_int),
     "dwpa_crack_files_ex": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p,
                              ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_int32)],
                             ctypes.c_int),

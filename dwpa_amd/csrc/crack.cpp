@@ -106,7 +106,8 @@ struct DevWork {
     hipEvent_t staged[2] = {nullptr, nullptr};
     double keep = 1.0;              // surviving candidates per (word x rule), carried from item to item
     uint32_t seen_version = 0;      // sh.version this scan's retired lines reflect
-    size_t items = 0, words = 0;    // statistics (DWPA_TRACE)
+    size_t items = 0, words = 0;    // statistics (DWPA_TRACE, dwpa_crack_last_stats)
+    uint64_t cands = 0;             // candidates loaded inside the 8..63 filter (after rules)
     double wait_s = 0;              // scanner time spent waiting for a staged item
     // stager -> scanner hand-over
     std::mutex mu;
@@ -189,6 +190,7 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
         sync_retired(w, sh);
         if ((r = scan_run(w.scan, w.stream)) < 0) return r;  // all ESSID groups, grouped per launch
         wb += nw;
+        w.cands += raw;
         std::vector<HitDev> hits;
         if ((r = scan_hits_raw(w.scan, hits, w.stream)) < 0) return r;
         if (hits.empty()) continue;
@@ -222,6 +224,10 @@ static size_t shards_per_device() {
     return (size_t)std::min<long>(8, std::max<long>(1, k));
 }
 
+// dwpa_crack_last_stats: the calling thread's last crack call
+static thread_local dwpa_crack_stats g_last_stats;
+static thread_local bool g_have_stats = false;
+
 static bool trace_on() {
     const char* e = getenv("DWPA_TRACE");
     return e && *e == '1';
@@ -234,6 +240,9 @@ static bool trace_on() {
 
 static int crack_impl(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file, int nec,
                       const char* out_file, const dwpa_config* cfg, int32_t* dict_status) {
+    const auto t_call = std::chrono::steady_clock::now();
+    g_last_stats = dwpa_crack_stats{};  // an early return reports zeros, never the previous call
+    g_have_stats = true;
     if (dict_status)
         for (size_t i = 0; i < ndicts; i++) dict_status[i] = DWPA_DICT_OK;
     if (!hash_file || !out_file || (!dicts && ndicts)) return DWPA_RC_ERROR;
@@ -444,6 +453,13 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
         if (w.up) (void)hipStreamDestroy(w.up);
     }
     fclose(sh.out);
+    for (auto& wp : work) {
+        g_last_stats.words += wp->words;
+        g_last_stats.candidates += wp->cands;
+    }
+    g_last_stats.hashes = (uint32_t)sh.valid;
+    g_last_stats.cracked = (uint32_t)sh.ncracked;
+    g_last_stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_call).count();
     if (rc < 0 || sh.error.load() < 0 || ioerr) return DWPA_RC_ERROR;
     return sh.ncracked == sh.valid ? DWPA_RC_CRACKED : DWPA_RC_EXHAUSTED;
 }
@@ -455,6 +471,12 @@ extern "C" {
 int dwpa_crack_files(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,
                      int nonce_error_corrections, const char* out_file, const dwpa_config* cfg) {
     return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg, nullptr);
+}
+
+int dwpa_crack_last_stats(dwpa_crack_stats* out) {
+    if (!out || !dwpa::g_have_stats) return DWPA_E_ARG;
+    *out = dwpa::g_last_stats;
+    return 0;
 }
 
 int dwpa_crack_files_ex(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,

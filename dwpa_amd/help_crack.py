@@ -15,7 +15,7 @@ Usage from help_crack.py (the one-line change INTEGRATION.md shows)::
 
     from dwpa_amd.help_crack import run_cracker as _gpu_run_cracker
     HelpCrack.run_cracker = lambda self, dictlist, disablestdout=False: _gpu_run_cracker(
-        self.conf, dictlist, sleepy=self.sleepy, pprint=self.pprint)
+        self.conf, dictlist, sleepy=self.sleepy, pprint=self.pprint, quiet=disablestdout)
 """
 from __future__ import annotations
 
@@ -68,8 +68,27 @@ def _truncate(path: str, size) -> None:
             f.truncate(size)
 
 
+def _summary(rc: int) -> str:
+    """hashcat's end-of-run block (Status / Recovered / Progress / Speed), from dwpa_crack_last_stats."""
+    st = M.crack_stats()
+    status = "Cracked" if rc == L.DWPA_RC_CRACKED else "Exhausted"
+    speed = st["candidates"] / st["seconds"] if st["seconds"] > 0 else 0.0
+    unit = next((u for u, f in (("MH/s", 1e6), ("kH/s", 1e3)) if speed >= f), "H/s")
+    scale = {"MH/s": 1e6, "kH/s": 1e3, "H/s": 1.0}[unit]
+    pct = 100.0 * st["cracked"] / st["hashes"] if st["hashes"] else 0.0
+    return "\n".join([
+        "Session..........: help_crack (libdwpa22000, gfx950)",
+        f"Status...........: {status}",
+        "Hash.Mode........: 22000 (WPA-PBKDF2-PMKID+EAPOL)",
+        f"Recovered........: {st['cracked']}/{st['hashes']} ({pct:.2f}%) Digests",
+        f"Progress.........: {st['candidates']} candidates from {st['words']} words",
+        f"Speed.#*.........: {speed / scale:8.1f} {unit}",
+        f"Time.............: {st['seconds']:.2f} s",
+    ])
+
+
 def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR_CORRECTIONS, sleepy=None,
-                pprint=None, max_tries: int | None = None) -> int:
+                pprint=None, max_tries: int | None = None, quiet: bool = False) -> int:
     """In-process equivalent of the hashcat command line at help_crack.py:773 with the reference's retry loop
     (:776-786): a failed attempt (library or GPU error -- hashcat's -1 / >= 2) is logged, followed by ``sleepy()``
     and retried, so only 0 (all cracked) or 1 (exhausted) ever reaches run(): returning -1 there would skip the
@@ -87,7 +106,9 @@ def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR
 
     ``sleepy``/``pprint`` are the HelpCrack methods when bound from help_crack.py.  ``max_tries`` (None = retry
     forever, as the reference does) ends the device-error loop with a DwpaError instead of a return value.  A
-    missing hash file raises FileNotFoundError (the reference would fail on an unbound ``rc``)."""
+    missing hash file raises FileNotFoundError (the reference would fail on an unbound ``rc``).  Unless ``quiet``
+    (help_crack's ``disablestdout``, the challenge run) a finished run prints hashcat's end-of-run block (Status,
+    Recovered, Progress, Speed) on stdout, where help_crack shows hashcat's output (:776)."""
     if not os.path.exists(conf["hash_file"]):
         raise FileNotFoundError(conf["hash_file"])
     sleepy = sleepy or _sleepy
@@ -111,6 +132,11 @@ def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR
                 if os.path.exists(d):
                     os.unlink(d)
         if rc in (L.DWPA_RC_CRACKED, L.DWPA_RC_EXHAUSTED):
+            if not quiet:
+                try:
+                    print(_summary(rc), flush=True)
+                except L.DwpaError:  # no crack call ran in this thread (a stubbed library): nothing to summarise
+                    pass
             return rc
         _truncate(key_file, size0)
         unreadable = [d for d, st in zip(dictlist, status) if st == L.DWPA_E_IO]

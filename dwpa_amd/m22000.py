@@ -197,6 +197,14 @@ def crack_files_ex(hash_file, dicts, rules_file=None, nonce_error_corrections: i
     return rc, [int(st[i]) for i in range(len(dl))]
 
 
+def crack_stats():
+    """dwpa_crack_last_stats: {words, candidates, hashes, cracked, seconds} of this thread's last crack call."""
+    st = L.CrackStats()
+    L.check(L.load().dwpa_crack_last_stats(ctypes.byref(st)), "crack_last_stats")
+    return {"words": st.words, "candidates": st.candidates, "hashes": st.hashes, "cracked": st.cracked,
+            "seconds": st.seconds}
+
+
 class Scan:
     """Device-resident scan of one work unit (hashlines grouped by ESSID) -- the client hot loop.
 

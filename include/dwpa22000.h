@@ -166,6 +166,18 @@ int dwpa_crack_files(const char *hash_file, const char *const *dicts, size_t ndi
 int dwpa_crack_files_ex(const char *hash_file, const char *const *dicts, size_t ndicts, const char *rules_file,
                         int nonce_error_corrections, const char *out_file, const dwpa_config *cfg,
                         int32_t *dict_status);
+/* What the calling thread's last dwpa_crack_files(_ex) call did, for a hashcat-style end-of-run summary
+ * (help_crack shows hashcat's output, help_crack.py:776): dictionary words read, candidates derived (inside the
+ * 8..63 filter, after the rules), hashlines loaded and cracked, wall time.  Returns 0, or DWPA_E_ARG before any
+ * call in this thread. */
+typedef struct {
+    uint64_t words;
+    uint64_t candidates;
+    uint32_t hashes;
+    uint32_t cracked;
+    double seconds;
+} dwpa_crack_stats;
+int dwpa_crack_last_stats(dwpa_crack_stats *out);
 
 /* GPU rule application (replaces `hashcat --stdout -r rules words`, help_crack.py:508,575): out holds
  * nwords*nrules candidates of 256 bytes (word-major), out_len their lengths (0xFFFFFFFF = input rejected).

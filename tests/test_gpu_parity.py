@@ -601,6 +601,41 @@ def test_crack_files_degenerate_inputs(tmp_path):
     assert dwpa_amd.check_key_m22000(good, [None]) is False
 
 
+def test_crack_last_stats(tmp_path, capsys):
+    """dwpa_crack_last_stats after an exhausted pass and a rules pass: every dictionary word read, candidates =
+    the words (or word x rule outputs) inside 8..63, valid hashlines loaded, lines cracked; the drop-in prints
+    them as hashcat's end-of-run block."""
+    from dwpa_amd import m22000 as M
+    from dwpa_amd.help_crack import run_cracker
+    rng = random.Random(73)
+    words = [S.random_psk(rng, 4, 70) for _ in range(5000)]
+    essid, ap, sta, an, sn = S.random_net(rng)
+    psk = next(w for w in words[3000:] if 8 <= len(w) <= 63)
+    hf = tmp_path / "h.hash"
+    hf.write_bytes(S.pmkid_line(psk, essid, ap, sta) + b"\n" + S.pmkid_line(b"not-there!", essid, ap, sta) +
+                   b"\nWPA*01*bad\n")
+    d = tmp_path / "d.txt"
+    d.write_bytes(b"\n".join(words) + b"\n")
+    out = tmp_path / "o.key"
+    assert dwpa_amd.crack_files(str(hf), [str(d)], None, 8, str(out)) == 1
+    st = M.crack_stats()
+    assert st["words"] == len(words) and st["candidates"] == sum(1 for w in words if 8 <= len(w) <= 63)
+    assert st["hashes"] == 2 and st["cracked"] == 1 and st["seconds"] > 0
+    rules = ["", ":", "$1", "]", "'7", "d"]
+    rf = tmp_path / "r.rule"
+    rf.write_text("\n".join(rules[1:]) + "\n")
+    out.unlink()
+    assert dwpa_amd.crack_files(str(hf), [str(d)], str(rf), 8, str(out)) == 1
+    exp = dwpa_amd.rules_expand("\n".join(rules[1:]), words)
+    st = M.crack_stats()
+    assert st["candidates"] == sum(1 for row in exp for c in row if c is not None and 8 <= len(c) <= 63)
+    conf = {"hash_file": str(hf), "key_file": str(out), "rules": "", "coptions": ""}
+    capsys.readouterr()
+    assert run_cracker(conf, [str(d)], sleepy=lambda: None, pprint=lambda *a: None) == 1
+    text = capsys.readouterr().out
+    assert "Status...........: Exhausted" in text and "Recovered........: 1/2 (50.00%) Digests" in text
+
+
 @pytest.mark.skipif(os.environ.get("DWPA_PBKDF2_ISSUE") == "1", reason="already the forced issue-pass run")
 def test_issue_pass_kernels_at_small_sizes():
     """Launches of at most one wave per SIMD take the plain-schedule PBKDF2 kernel (pbkdf2_module.cpp), so the

@@ -137,3 +137,19 @@ def test_missing_hash_file_raises(tmp_path):
     conf["hash_file"] = str(tmp_path / "nope.hash")
     with pytest.raises(FileNotFoundError):
         run_cracker(conf, [], max_tries=1)
+
+
+def test_end_of_run_summary(tmp_path, monkeypatch, capsys):
+    """Like hashcat, each finished attempt prints Status / Recovered / Progress / Speed on stdout (help_crack shows
+    hashcat's output, help_crack.py:776), from dwpa_crack_last_stats; quiet (help_crack's disablestdout, the
+    challenge run) prints nothing."""
+    conf = _conf(tmp_path)
+    monkeypatch.setattr(H.M, "crack_files_ex", lambda *a, **k: (1, [L.DWPA_DICT_OK]))
+    monkeypatch.setattr(H.M, "crack_stats", lambda: {"words": 1000, "candidates": 9_790_000, "hashes": 4,
+                                                     "cracked": 1, "seconds": 2.0})
+    assert run_cracker(conf, [_dict(tmp_path)], sleepy=lambda: None, pprint=lambda *a: None) == 1
+    out = capsys.readouterr().out
+    assert "Status...........: Exhausted" in out and "Recovered........: 1/4 (25.00%) Digests" in out
+    assert "Progress.........: 9790000 candidates from 1000 words" in out and "4.9 MH/s" in out
+    assert run_cracker(conf, [_dict(tmp_path)], sleepy=lambda: None, pprint=lambda *a: None, quiet=True) == 1
+    assert capsys.readouterr().out == ""
