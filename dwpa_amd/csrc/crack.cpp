@@ -58,10 +58,17 @@ struct WorkItem {
 // Cuts the reader's chunks into work items that every shard worker pulls for itself: a device that finishes its
 // item early takes the next one, so no device waits for the slowest at a chunk boundary.  Items start at `first`
 // words (a sixteenth of a batch of candidates, so every device starts after a short read) and double up to `most`.
+// With several workers the end of the work unit is balanced by guided self-scheduling: an item takes at most
+// 1/(2 workers) of the words read and not yet handed out (each worker stages its next item while it scans the
+// current one; never under `first`).  The readers run ahead of the devices, so mid-way that leaves the items at
+// their doubling size, while at the end, when the last chunk holds all that remains, the items shrink and the
+// devices finish within about one small item of each other.  Without it a 20M-word dictionary on 8 workers went
+// out as items of 1, 2, 4, 1 and 11.6M words, three workers idle (profiles/r03/crack_balance/).
 class ItemQueue {
   public:
-    ItemQueue(ChunkSource& src, size_t first, size_t most) : src_(src), size_(std::max<size_t>(1, first)),
-                                                             most_(std::max<size_t>(1, most)) {}
+    ItemQueue(ChunkSource& src, size_t first, size_t most, size_t workers)
+        : src_(src), size_(std::max<size_t>(1, first)), first_(std::max<size_t>(1, first)),
+          most_(std::max<size_t>(1, most)), workers_(std::max<size_t>(1, workers)) {}
     bool next(WorkItem& it) {
         std::lock_guard<std::mutex> lk(mu_);
         while (!cur_ || pos_ >= cur_->words()) {
@@ -73,7 +80,11 @@ class ItemQueue {
             }
             pos_ = 0;
         }
-        const size_t n = std::min(size_, cur_->words() - pos_);
+        size_t n = std::min(size_, cur_->words() - pos_);
+        if (workers_ > 1) {  // the words read and not yet handed out (all that remains once the readers end)
+            const size_t rem = cur_->words() - pos_ + src_.pending_words();
+            n = std::min(n, std::max(first_, (rem + 2 * workers_ - 1) / (2 * workers_)));
+        }
         it.chunk = cur_;
         it.b = pos_;
         it.e = pos_ + n;
@@ -90,7 +101,7 @@ class ItemQueue {
     ChunkSource& src_;
     std::mutex mu_;
     std::shared_ptr<const Chunk> cur_;
-    size_t pos_ = 0, size_, most_;
+    size_t pos_ = 0, size_, first_, most_, workers_;
     bool done_ = false, err_ = false;
 };
 
@@ -340,7 +351,10 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     const size_t nr = rp ? rp->size() : 1;
     const size_t first_item = std::max<size_t>(1, batch / nr / 16), most_item = std::max<size_t>(1, 16 * (size_t)batch / nr);
     ChunkSource source(dpaths, first_item * G, 2 * most_item * G);
-    ItemQueue items(source, first_item, most_item);
+    // several workers: items of at most 2 batches, so an item handed out just before the readers reach the end
+    // cannot outlast the balanced tail by more than that
+    ItemQueue items(source, first_item, G > 1 ? std::min(most_item, std::max<size_t>(first_item, 2 * (size_t)batch / nr))
+                                              : most_item, G);
     const auto t0 = std::chrono::steady_clock::now();
 
     auto stop_all = [&]() {

@@ -496,6 +496,13 @@ class ChunkSource {
         cv_.notify_all();
         return true;
     }
+    // Words of the chunks read but not yet taken.
+    size_t pending_words() {
+        std::lock_guard<std::mutex> lk(mu_);
+        size_t n = 0;
+        for (const auto& c : q_) n += c->words();
+        return n;
+    }
     bool next(Chunk& c, bool& err) {  // by value (tools/inflate_bench)
         std::shared_ptr<const Chunk> p;
         if (!next(p, err)) return false;
