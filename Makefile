@@ -58,7 +58,7 @@ clean:
 .PHONY: all oracle clean asm
 
 tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
-       tools/bin/inflate_check
+       tools/bin/inflate_check tools/bin/item_queue_check
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -86,3 +86,8 @@ tools/bin/inflate_bench: tools/inflate_bench.cpp $(SRC)/dict_reader.hpp $(SRC)/i
 tools/bin/inflate_check: tools/inflate_check.cpp $(SRC)/inflate.hpp $(SRC)/pinflate.hpp
 	@mkdir -p tools/bin
 	g++ -O3 -std=c++17 -Wall -I$(SRC) -o $@ tools/inflate_check.cpp -lz -lpthread
+
+tools/bin/item_queue_check: tools/item_queue_check.cpp $(SRC)/dict_reader.hpp $(SRC)/inflate.hpp $(SRC)/pinflate.hpp \
+                            $(SRC)/m22000_host.cpp $(SRC)/m22000_host.hpp
+	@mkdir -p tools/bin
+	g++ -O2 -std=c++17 -Wall -Iinclude -I$(SRC) -o $@ tools/item_queue_check.cpp $(SRC)/m22000_host.cpp -lz -lpthread

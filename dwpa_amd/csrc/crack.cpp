@@ -49,62 +49,6 @@ static std::string outfile_record(const ParsedLine& p, const std::string& psk) {
            hashcat_plain(p.essid) + ":" + hashcat_plain(psk) + "\n";
 }
 
-// One contiguous word range of a dictionary chunk.  The chunk stays alive until its last range is scanned.
-struct WorkItem {
-    std::shared_ptr<const Chunk> chunk;
-    size_t b = 0, e = 0;
-};
-
-// Cuts the reader's chunks into work items that every shard worker pulls for itself: a device that finishes its
-// item early takes the next one, so no device waits for the slowest at a chunk boundary.  Items start at `first`
-// words (a sixteenth of a batch of candidates, so every device starts after a short read) and double up to `most`.
-// With several workers the end of the work unit is balanced by guided self-scheduling: an item takes at most
-// 1/(2 workers) of the words read and not yet handed out (each worker stages its next item while it scans the
-// current one; never under `first`).  The readers run ahead of the devices, so mid-way that leaves the items at
-// their doubling size, while at the end, when the last chunk holds all that remains, the items shrink and the
-// devices finish within about one small item of each other.  Without it a 20M-word dictionary on 8 workers went
-// out as items of 1, 2, 4, 1 and 11.6M words, three workers idle (profiles/r03/crack_balance/).
-class ItemQueue {
-  public:
-    ItemQueue(ChunkSource& src, size_t first, size_t most, size_t workers)
-        : src_(src), size_(std::max<size_t>(1, first)), first_(std::max<size_t>(1, first)),
-          most_(std::max<size_t>(1, most)), workers_(std::max<size_t>(1, workers)) {}
-    bool next(WorkItem& it) {
-        std::lock_guard<std::mutex> lk(mu_);
-        while (!cur_ || pos_ >= cur_->words()) {
-            if (done_) return false;
-            if (!src_.next(cur_, err_)) {
-                done_ = true;
-                cur_.reset();
-                return false;
-            }
-            pos_ = 0;
-        }
-        size_t n = std::min(size_, cur_->words() - pos_);
-        if (workers_ > 1) {  // the words read and not yet handed out (all that remains once the readers end)
-            const size_t rem = cur_->words() - pos_ + src_.pending_words();
-            n = std::min(n, std::max(first_, (rem + 2 * workers_ - 1) / (2 * workers_)));
-        }
-        it.chunk = cur_;
-        it.b = pos_;
-        it.e = pos_ + n;
-        pos_ += n;
-        size_ = std::min(most_, 2 * size_);
-        return true;
-    }
-    bool io_error() {
-        std::lock_guard<std::mutex> lk(mu_);
-        return err_;
-    }
-
-  private:
-    ChunkSource& src_;
-    std::mutex mu_;
-    std::shared_ptr<const Chunk> cur_;
-    size_t pos_ = 0, size_, first_, most_, workers_;
-    bool done_ = false, err_ = false;
-};
-
 // One shard worker (one per device, or DWPA_CRACK_SHARDS_PER_DEVICE per device).  Its stager thread uploads the
 // next item into the free one of two buffer slots on the `up` stream while its scanner thread scans the other.
 struct DevWork {
