@@ -333,12 +333,16 @@ def spawn_ranks(args) -> int:
     port = s.getsockname()[1]
     s.close()
     cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+
+    def die_with_parent():  # a rank gets SIGTERM if this parent is killed (e.g. by a time limit): no orphan ranks
+        import ctypes
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
-                                      start_new_session=True))
+                                      start_new_session=True, preexec_fn=die_with_parent))
     lines = []
 
     def relay():
@@ -582,6 +586,8 @@ def main_dry(args, world, rank):
     of every rank.  tests/test_bench_spawn.py checks N ranks and disjoint coverage through `--gpus N`."""
     import torch.distributed as dist
     from dwpa_amd.shard import reduce_timing, strong_batches, weak_units
+    if os.environ.get("DWPA_TEST_RANK_SLEEP"):  # tests/test_bench_spawn.py: keep the ranks alive while it kills the parent
+        time.sleep(float(os.environ["DWPA_TEST_RANK_SLEEP"]))
     if world > 1:
         dist.init_process_group("gloo")
     B = (args.batch + 63) & ~63

@@ -95,3 +95,27 @@ def test_torchrun_launcher_form():
                        capture_output=True, text=True, env=env, timeout=180, cwd=ROOT)
     out = _line(r)
     assert out["n_gpus"] == 2 and len(out["coverage"]) == 2 and out["pid"] != os.getpid()
+
+
+def test_ranks_die_with_the_parent():
+    """A killed parent (a driver's time limit) must not leave its rank processes running: each rank is started with
+    PR_SET_PDEATHSIG.  The ranks here sleep before their rendezvous (DWPA_TEST_RANK_SLEEP) while the parent is
+    killed."""
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "LOCAL_WORLD_SIZE")}
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1",
+                          "--warmup", "0"], env=dict(env, DWPA_TEST_RANK_SLEEP="60"), cwd=ROOT,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    time.sleep(3)
+    kids = [int(x) for x in open(f"/proc/{p.pid}/task/{p.pid}/children").read().split()]
+    assert len(kids) == 2
+    p.send_signal(signal.SIGKILL)
+    p.wait()
+    deadline = time.time() + 20
+    while time.time() < deadline and any(os.path.exists(f"/proc/{k}") and
+                                         open(f"/proc/{k}/stat").read().split()[2] != "Z" for k in kids):
+        time.sleep(0.2)
+    alive = [k for k in kids if os.path.exists(f"/proc/{k}") and open(f"/proc/{k}/stat").read().split()[2] != "Z"]
+    assert not alive, alive
