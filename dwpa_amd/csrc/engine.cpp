@@ -805,6 +805,21 @@ static int collect_hits(Device& d, std::vector<HitDev>& hits_out) {
     return 0;
 }
 
+// Declared right after a call context's lock: when the call returns -- above all on an error after its first
+// launch -- every stream of the context has drained before the lock is released, so the next call on this context
+// never overwrites staging or device buffers that queued copies and kernels of this one still use.
+// The success paths have synchronised already and disarm it.
+struct DrainOnExit {
+    Device& d;
+    bool armed = true;
+    ~DrainOnExit() {
+        if (!armed) return;
+        (void)hipSetDevice(d.id);
+        for (hipStream_t s : {d.stream, d.side, d.tail})
+            if (s) (void)hipStreamSynchronize(s);
+    }
+};
+
 // A call context, locked: an idle one of the device with the fewest calls in flight (ties: round-robin from
 // g_rr; within a device the lowest context, so one caller keeps reusing context 0's buffers), else wait for the
 // first context of the next device in round-robin order.
@@ -840,6 +855,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     Device* dp = pick_device();
     if (!dp) return DWPA_E_NODEV;
     std::lock_guard<std::mutex> lk(dp->mu, std::adopt_lock);
+    DrainOnExit drain{*dp};
     Device& d = *dp;
     HIPCHK(hipSetDevice(d.id));
     RCHK(device_stream(d));
@@ -1038,6 +1054,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         }
     }
     tr.mark("results");
+    drain.armed = false;  // collect_hits synchronised every stream of this call
     return 0;
 }
 
@@ -1046,6 +1063,7 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
     Device* dp = pick_device();
     if (!dp) return DWPA_E_NODEV;
     std::lock_guard<std::mutex> lk(dp->mu, std::adopt_lock);
+    DrainOnExit drain{*dp};
     Device& d = *dp;
     HIPCHK(hipSetDevice(d.id));
     RCHK(device_stream(d));
