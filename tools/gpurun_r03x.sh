@@ -1,7 +1,7 @@
 # round 3, call x: end-of-session validation at HEAD -- GPU suite, smoke, the default bench line (what the driver
 # runs), the bench command under rocprofv3 --kernel-trace --stats (CSV), C5 one and two callers.
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/r03x
+O=${O:-gpurun_out/r03x}
 mkdir -p $O
 guard() { case $1 in 0) ;; 124|134|137|139) echo "stop: rc $1" >&2; exit $1;; *) echo "fail: rc $1" >&2; exit 1;; esac; }
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/pytest.log 2>&1
