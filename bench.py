@@ -557,6 +557,9 @@ def main():
                                               / PEAK_LANE_OPS, 4),
                 "frac_guide_valu_peak_basis": f"{SURVEY_OPS_PER_COMPRESSION} ops per compression (SURVEY.md 8(d) "
                                               "ideal count) / 78.64 T int32 lane-ops/s",
+                # the most that basis can show on gfx950: the issue-cost peak (rotates and add3 at half rate)
+                "frac_guide_valu_peak_attainable": round(PEAK_COMPRESSIONS * SURVEY_OPS_PER_COMPRESSION
+                                                         / PEAK_LANE_OPS, 4),
                 "frac_nominal_ops": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * ISSUED_OPS_PER_COMPRESSION
                                           / PEAK_LANE_OPS, 4),
                 "frac_nominal_ops_basis": f"{ISSUED_OPS_PER_COMPRESSION} VALU issued per compression (PMC) / "
