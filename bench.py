@@ -964,6 +964,7 @@ def main_files(args, world, rank, local):
         t0 = time.perf_counter()
         rc = dwpa_amd.crack_files(hpath, [dpath], None, 8, opath, device_mask=1 << local, batch=args.batch)
         el = time.perf_counter() - t0
+        reported = dwpa_amd.m22000.crack_stats()["candidates"]
         all_passes.append(round(el, 3))
         if rep >= args.warmup:
             times.append(el)
@@ -984,7 +985,8 @@ def main_files(args, world, rank, local):
                                    "inflated and uploaded per chunk), one EAPOL keyver-2 line, hashcat NC mode 8"
                                    + (", ~30 % of the words shorter than 8" if args.short_words else ""),
                        "dict_words": n, "gz_bytes": gz_bytes, "gz_write_s": round(gz_s, 2),
-                       "words_scanned_per_pass": words, "batch": args.batch,
+                       "words_scanned_per_pass": words, "candidates_reported_by_library": reported,
+                       "batch": args.batch,
                        "parallelism": f"replicas x{world}",
                        "dict_cache": "passes after the first replay the decoded dictionary from the library's "
                                      "DictCache (no inflate)" if os.environ.get("DWPA_DICT_CACHE_MB", "") != "0"
@@ -1066,6 +1068,7 @@ def main_files_rules(args, world, rank, local):
         t0 = time.perf_counter()
         rc = dwpa_amd.crack_files(hpath, [dpath], rpath, 8, opath, device_mask=1 << local, batch=args.batch)
         el = time.perf_counter() - t0
+        reported = dwpa_amd.m22000.crack_stats()["candidates"]
         all_passes.append(round(el, 3))
         if rep >= args.warmup:
             times.append(el)
@@ -1084,7 +1087,8 @@ def main_files_rules(args, world, rank, local):
             "config": {"workload": f"client rule pass via dwpa_crack_files: {n}-word gzip dictionary x {len(rules)} "
                                    "WPA rules (rules file, amplified on the GPU, 8..63 filter), one EAPOL keyver-2 "
                                    "line, hashcat NC mode 8", "rule_words": n, "rules": len(rules),
-                       "candidates_per_pass": cands, "batch": args.batch, "parallelism": f"replicas x{world}",
+                       "candidates_per_pass": cands, "candidates_reported_by_library": reported,
+                       "batch": args.batch, "parallelism": f"replicas x{world}",
                        "plant": [plant_word, plant_rule]},
             "pass_s": all_passes,
             "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked)})
