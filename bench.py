@@ -507,6 +507,11 @@ def main():
         w.scans[k].hits(streams[k].handle)
     step(w.plant_batch, 0)
     verified = bool(w.check(w.scans[0].hits(streams[0].handle)))
+    if world > 1:  # every rank's own planted PSK must come back (each rank scans its own shard)
+        import torch
+        okt = torch.tensor([1.0 if verified else 0.0], dtype=torch.float64)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        verified = bool(okt.item() == 1.0)
 
     per_launch = list(counts) if w.groups > 1 else [c / w.groups for c in counts]
     pmk_per_launch = sum(per_launch) / len(per_launch)
