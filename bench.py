@@ -508,10 +508,8 @@ def main():
     step(w.plant_batch, 0)
     verified = bool(w.check(w.scans[0].hits(streams[0].handle)))
     if world > 1:  # every rank's own planted PSK must come back (each rank scans its own shard)
-        import torch
-        okt = torch.tensor([1.0 if verified else 0.0], dtype=torch.float64)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        verified = bool(okt.item() == 1.0)
+        from dwpa_amd.shard import all_ranks
+        verified = all_ranks(dist, verified)
 
     per_launch = list(counts) if w.groups > 1 else [c / w.groups for c in counts]
     pmk_per_launch = sum(per_launch) / len(per_launch)
@@ -681,11 +679,9 @@ def main_strong(args, world, rank, local):
     kernel_ms = sum(kms) / len(kms)
     kernel_pmk_s = sum(c for _, c in sched) * args.steps / (sum(kms) * 1e-3)
     if world > 1:
-        import torch
+        from dwpa_amd.shard import all_ranks
         elapsed, total = reduce_timing(dist, elapsed, done)
-        okt = torch.tensor([1.0 if ok_local else 0.0], dtype=torch.float64)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        verified = bool(okt.item() == 1.0)
+        verified = all_ranks(dist, ok_local)
         shards = [None] * world
         dist.all_gather_object(shards, [lo, hi, len(sched), round(elapsed_local, 4)])
     else:
@@ -818,6 +814,9 @@ def main_ffi(args, world, rank, local):
         mismatches = sum(1 for g, e in zip(got, exp) if g != e)
         verified = mismatches == 0 and sum(1 for e in exp if e) >= 0.85 * len(jobs)
     verified = verified and same
+    if world > 1:  # every replica's results must check
+        from dwpa_amd.shard import all_ranks
+        verified = all_ranks(dist, verified)
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -978,6 +977,8 @@ def main_files(args, world, rank, local):
     elapsed = sum(times) / len(times)
     words = int(np.count_nonzero(lens[:plant + 1] >= 8))  # PMKs derived: words inside the 8..63 filter
     if world > 1:
+        from dwpa_amd.shard import all_ranks
+        cracked = all_ranks(dist, cracked)
         elapsed, total = reduce_timing(dist, elapsed, float(words))
     else:
         total = float(words)
@@ -1081,6 +1082,8 @@ def main_files_rules(args, world, rank, local):
         cracked &= rc == 0 and len(recs) == 1 and recs[0].endswith(b":" + psk)
     elapsed = sum(times) / len(times)
     if world > 1:
+        from dwpa_amd.shard import all_ranks
+        cracked = all_ranks(dist, cracked)
         elapsed, total = reduce_timing(dist, elapsed, float(cands))
     else:
         total = float(cands)

@@ -40,3 +40,11 @@ def reduce_timing(dist, elapsed: float, done: float):
     c = torch.tensor([float(done)], dtype=torch.float64)
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     return float(t.item()), float(c.item())
+
+
+def all_ranks(dist, ok: bool) -> bool:
+    """True on every rank iff `ok` is true on every rank (gloo MIN over the ranks' flags)."""
+    import torch
+    t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item() == 1.0)

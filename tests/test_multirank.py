@@ -70,3 +70,27 @@ def test_contiguous_shards():
             for (b0, e0), (b1, e1) in zip(parts, parts[1:]):
                 assert e0 == b1
             assert max(e - b for b, e in parts) - min(e - b for b, e in parts) <= 1
+
+
+def _ok_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from dwpa_amd.shard import all_ranks
+    q.put((rank, all_ranks(dist, True), all_ranks(dist, rank != 1)))
+    dist.destroy_process_group()
+
+
+def test_all_ranks_verification():
+    """bench.py's hits_verified over N ranks: true only if every rank found its own planted PSK."""
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ok_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(a is True and b is False for _, a, b in res)
