@@ -47,7 +47,8 @@ class Config(ctypes.Structure):
 
 class CrackStats(ctypes.Structure):
     _fields_ = [("words", ctypes.c_uint64), ("candidates", ctypes.c_uint64), ("hashes", ctypes.c_uint32),
-                ("cracked", ctypes.c_uint32), ("seconds", ctypes.c_double)]
+                ("cracked", ctypes.c_uint32), ("seconds", ctypes.c_double), ("rules", ctypes.c_uint32),
+                ("rules_skipped", ctypes.c_uint32)]
 
 
 class LineInfo(ctypes.Structure):
@@ -86,6 +87,10 @@ SIGNATURES = {
                             ctypes.c_int),
     "dwpa_rules_expand": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Bytes), ctypes.c_size_t, _P, _P,
                            ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "dwpa_rules_count": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
+                          ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "dwpa_rules_apply_host": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, _P,
+                               ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "dwpa_scan_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
                           ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_P)], ctypes.c_int),
     "dwpa_scan_num_groups": ([_P], ctypes.c_int),

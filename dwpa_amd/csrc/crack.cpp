@@ -157,7 +157,7 @@ static int scan_shard(DevWork& w, CrackShared& sh, const Chunk& c, size_t b, siz
             if (sh.cracked[ph.line]) continue;
             const uint64_t word = h.cand / nrules, rule = h.cand % nrules;
             std::string plain(c.bytes.data() + c.off[b + word], c.off[b + word + 1] - c.off[b + word]);
-            if (rules) plain = rules->apply_host((size_t)rule, plain);
+            if (rules && !rules->apply_host((size_t)rule, plain, &plain)) continue;  // cannot happen: the GPU kept it
             sh.cracked[ph.line] = 1;
             sh.ncracked++;
             sh.version.fetch_add(1, std::memory_order_acq_rel);
@@ -252,10 +252,15 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     }
     if (sh.valid == 0) return DWPA_RC_ERROR;  // hashcat: "No hashes loaded"
 
+    // hashcat -r: lines that do not parse are skipped with a message each (RuleSet::add_line) and counted in
+    // dwpa_crack_last_stats; a file with no valid rule left fails the call, as hashcat refuses to start
     RuleSet rules;
     const RuleSet* rp = nullptr;
     if (rules_file) {
-        if (rules.load_file(rules_file) < 0) return DWPA_RC_ERROR;
+        const int lr = rules.load_file(rules_file);
+        g_last_stats.rules = (uint32_t)rules.size();
+        g_last_stats.rules_skipped = (uint32_t)rules.skipped.size();
+        if (lr < 0) return DWPA_RC_ERROR;
         if (!rules.all_noop()) rp = &rules;
     }
 

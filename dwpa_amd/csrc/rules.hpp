@@ -1,11 +1,20 @@
-// rules.hpp -- hashcat rule engine (CPU rule-processor semantics, as used by help_crack's `hashcat --stdout -r`
-// (help_crack.py:508,575) and `-S -r` (:445-447,931-933)).  Parsing on the host, application on the GPU.
+// rules.hpp -- hashcat rule engine: the whole rule language of hashcat >= 6.2.6 (help_crack.py:46), as help_crack
+// uses it through `hashcat --stdout -r` (help_crack.py:508,575) and `-S -r` with the server's merged per-dictionary
+// rules (help_crack.py:445-447,931-933; get_work.php:86-92; db/wpa.sql:48).  Parsing on the host, application on
+// the GPU (rules_dev.hip); RuleSet::apply_host re-applies a rule on the host to report a hit's PSK.
 //
-// Supported ops: the 16 used by help_crack/bestWPA.rule plus a few neighbours from the same family:
-//   :  l  u  c  C  t  r  d  f  {  }  [  ]  q  TN  pN  DN  'N  zN  ZN  $X  ^X  sXY  @X
-// Positions N are 0-9 then A-Z (10-35).  Work buffer = hashcat's RP_PASSWORD_SIZE (256): an op whose result
-// would not fit leaves the word unchanged.  Rules that fail to parse are skipped (hashcat: "Skipping invalid
-// or unsupported rule").  Semantics of the third-party engine are unpinned by the reference's tests.
+// Functions (N, M, I = position/length 0-9 then A-Z; X, Y = any byte):
+//   no argument   :  l  u  c  C  t  r  d  f  {  }  [  ]  k  K  q  E  M  4  6  Q
+//   N             TN pN DN zN ZN 'N yN YN LN RN +N -N .N ,N <N >N _N
+//   X             $X ^X @X eX !X /X (X )X
+//   N X           iNX oNX =NX %NX 3NX
+//   X Y           sXY
+//   N M           xNM ONM *NM
+//   N M I         XNMI
+// Work buffer = hashcat's RP_PASSWORD_SIZE (256).  Semantics (bounds, reject and memory functions) are stated in
+// oracle/rules.py, the test oracle all three implementations are held to; hashcat itself is third party, so they
+// are parity unpinned by the reference.  A rule line that does not parse is skipped and reported (stderr, hashcat's
+// "Skipping invalid or unsupported rule", and the counts below), never dropped silently.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,21 +28,33 @@ namespace dwpa {
 
 constexpr int RP_PASSWORD_SIZE = 256;
 
+// One rule function: op byte + up to three arguments (positions already converted to 0..35).  The device image
+// stores each as one u32 word {op, p1, p2, p3} (little-endian bytes).
 struct RuleOp {
-    uint8_t op, p1, p2;
+    uint8_t op, p1, p2, p3;
 };
 
 struct RuleSet {
     std::vector<std::vector<RuleOp>> rules;
     std::vector<std::string> text;
+    uint32_t present = 0;                 // rule lines seen (not empty, not a '#' comment)
+    std::vector<std::string> skipped;     // lines that did not parse
+    std::vector<uint32_t> skipped_lines;  // their 1-based line numbers
+    std::string source = "rules";         // file name for the messages
+    bool quiet = false;                   // no stderr message per skipped line
     size_t size() const { return rules.size(); }
     int load_file(const char* path);
-    int add_line(const std::string& line);  // 1 added, 0 skipped (comment/empty/invalid)
+    void load_text(const char* text, size_t len);
+    int add_line(const std::string& line, uint32_t lineno = 0);  // 1 added, 0 not a rule, -1 skipped (invalid)
     bool all_noop() const;
-    std::string apply_host(size_t rule, const std::string& word) const;
-    // flat device image: offsets[nrules+1] into a byte code of (op,p1,p2) triples
-    void flatten(std::vector<uint32_t>& offs, std::vector<uint8_t>& code) const;
+    // the candidate, or false when the input or a reject / memory function rejects it
+    bool apply_host(size_t rule, const std::string& word, std::string* out) const;
+    // flat device image: offsets[nrules+1] (in ops) into u32 op words
+    void flatten(std::vector<uint32_t>& offs, std::vector<uint32_t>& code) const;
 };
+
+// Parse one rule line; returns false if it is not a complete rule.  *ops empty for a comment / empty line.
+bool parse_rule(const std::string& line, std::vector<RuleOp>* ops, bool* is_rule);
 
 struct DevRules {
     int device = -1;
@@ -45,15 +66,15 @@ struct DevRules {
 int rules_upload(int device, const RuleSet& rs, DevRules* out);
 void rules_release(DevRules* r);
 // Stage 1 for word x rule candidates: words [first, first+nwords) of an HBM dictionary, every rule; candidates
-// outside 8..63 bytes are dropped; candidate id = word * nrules + rule.
+// outside 8..63 bytes (or rejected by a rule) are dropped; candidate id = word * nrules + rule.
 int rules_load(dwpa_scan* scan, const DevRules* r, const uint64_t* off, const uint8_t* bytes, uint64_t first,
                uint32_t nwords, hipStream_t s, bool fill = false);
 
 hipError_t launch_rules_expand(const uint64_t* off, const uint8_t* bytes, uint32_t nwords, const uint32_t* roffs,
-                               const uint8_t* rcode, uint32_t nrules, uint8_t* out, uint32_t* out_len,
+                               const uint32_t* rcode, uint32_t nrules, uint8_t* out, uint32_t* out_len,
                                hipStream_t s);
 hipError_t launch_rules_prep(const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t nwords,
-                             const uint32_t* roffs, const uint8_t* rcode, uint32_t nrules, uint32_t minlen,
+                             const uint32_t* roffs, const uint32_t* rcode, uint32_t nrules, uint32_t minlen,
                              uint32_t maxlen, uint32_t* mid, uint64_t* ids, uint32_t* counter, uint32_t cap,
                              hipStream_t s);
 

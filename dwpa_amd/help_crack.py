@@ -76,7 +76,7 @@ def _summary(rc: int) -> str:
     unit = next((u for u, f in (("MH/s", 1e6), ("kH/s", 1e3)) if speed >= f), "H/s")
     scale = {"MH/s": 1e6, "kH/s": 1e3, "H/s": 1.0}[unit]
     pct = 100.0 * st["cracked"] / st["hashes"] if st["hashes"] else 0.0
-    return "\n".join([
+    lines = [
         "Session..........: help_crack (libdwpa22000, gfx950)",
         f"Status...........: {status}",
         "Hash.Mode........: 22000 (WPA-PBKDF2-PMKID+EAPOL)",
@@ -84,7 +84,10 @@ def _summary(rc: int) -> str:
         f"Progress.........: {st['candidates']} candidates from {st['words']} words",
         f"Speed.#*.........: {speed / scale:8.1f} {unit}",
         f"Time.............: {st['seconds']:.2f} s",
-    ])
+    ]
+    if st.get("rules") or st.get("rules_skipped"):
+        lines.insert(4, f"Rules............: {st['rules']} loaded, {st['rules_skipped']} skipped (invalid or unsupported)")
+    return "\n".join(lines)
 
 
 def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR_CORRECTIONS, sleepy=None,
@@ -121,17 +124,20 @@ def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR
         size0 = os.path.getsize(key_file) if os.path.exists(key_file) else None
         rc, status = M.crack_files_ex(conf["hash_file"], dictlist, rules_file, nonce_error_corrections, key_file,
                                       device_mask=mask)
-        for d, st in zip(dictlist, status):
-            if st != L.DWPA_DICT_DAMAGED:
-                continue
-            if d == conf.get("additional"):
-                pprint(f"Dictionary {d} is damaged (truncated or corrupt gzip); scanned up to the damage", "WARNING")
-            else:
-                pprint(f"Dictionary {d} is damaged (truncated or corrupt gzip); scanned up to the damage, "
-                       "removed so that it is downloaded again", "WARNING")
-                if os.path.exists(d):
-                    os.unlink(d)
         if rc in (L.DWPA_RC_CRACKED, L.DWPA_RC_EXHAUSTED):
+            # a damaged download is removed only once the attempt has counted (its scan up to the damage is the
+            # result); a failed attempt is retried below with the same dictionary list, which must still exist
+            for d, st in zip(dictlist, status):
+                if st != L.DWPA_DICT_DAMAGED:
+                    continue
+                if d == conf.get("additional"):
+                    pprint(f"Dictionary {d} is damaged (truncated or corrupt gzip); scanned up to the damage",
+                           "WARNING")
+                else:
+                    pprint(f"Dictionary {d} is damaged (truncated or corrupt gzip); scanned up to the damage, "
+                           "removed so that it is downloaded again", "WARNING")
+                    if os.path.exists(d):
+                        os.unlink(d)
             if not quiet:
                 try:
                     print(_summary(rc), flush=True)
@@ -155,6 +161,15 @@ def expand_rules(rules_file: str, source: str, out_gz: str, chunk: int = 1 << 16
     Rejected words are skipped like hashcat does; returns the number of candidates written."""
     with open(rules_file, "rb") as f:
         rules_text = f.read()
+    present, parsed, _ = M.rules_count(rules_text)
+    if parsed < present:  # hashcat: "Skipping invalid or unsupported rule in file ... on line ...: ..."
+        for no, line in enumerate(rules_text.split(b"\n"), 1):
+            line = line.rstrip(b"\r")
+            if line and not line.startswith(b"#") and M.rules_count(line)[1] == 0:
+                print(f"Skipping invalid or unsupported rule in file {rules_file} on line {no}: "
+                      f"{line.decode('latin-1')}", file=sys.stderr)
+    if parsed == 0:
+        raise L.DwpaError(L.DWPA_E_RULE, f"{rules_file}: no valid rules left")  # hashcat refuses to start
     written = 0
     opener = gzip.open if source.endswith(".gz") else open
     with opener(source, "rb") as src, gzip.open(out_gz, "wb") as dst:

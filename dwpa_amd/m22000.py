@@ -152,6 +152,25 @@ def pbkdf2_pmk(keys, essid) -> list:
     return [raw[32 * i:32 * i + 32] for i in range(len(keys))]
 
 
+def rules_count(rules_text):
+    """(rule lines present, rules that parse, 1-based line of the first that does not or 0) -- host only."""
+    rt = _b(rules_text)
+    present, parsed, first = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_uint32(0)
+    L.check(L.load().dwpa_rules_count(rt, len(rt), ctypes.byref(present), ctypes.byref(parsed), ctypes.byref(first)),
+            "rules_count")
+    return present.value, parsed.value, first.value
+
+
+def rules_apply_host(rules_text, rule_index: int, word):
+    """Rule `rule_index` of rules_text applied to `word` on the host by the GPU's interpreter: bytes or None."""
+    rt, w = _b(rules_text), _b(word)
+    out = ctypes.create_string_buffer(256)
+    n = ctypes.c_uint32(0)
+    L.check(L.load().dwpa_rules_apply_host(rt, len(rt), int(rule_index), w, len(w), out, ctypes.byref(n)),
+            "rules_apply_host")
+    return None if n.value == 0xFFFFFFFF else out.raw[:n.value]
+
+
 def rules_expand(rules_text, words, device: int = 0):
     """GPU rule application (hashcat --stdout -r): returns [[candidate or None (rejected)] per rule] per word."""
     rt = _b(rules_text)
@@ -198,11 +217,12 @@ def crack_files_ex(hash_file, dicts, rules_file=None, nonce_error_corrections: i
 
 
 def crack_stats():
-    """dwpa_crack_last_stats: {words, candidates, hashes, cracked, seconds} of this thread's last crack call."""
+    """dwpa_crack_last_stats: {words, candidates, hashes, cracked, seconds, rules, rules_skipped} of this thread's
+    last crack call."""
     st = L.CrackStats()
     L.check(L.load().dwpa_crack_last_stats(ctypes.byref(st)), "crack_last_stats")
     return {"words": st.words, "candidates": st.candidates, "hashes": st.hashes, "cracked": st.cracked,
-            "seconds": st.seconds}
+            "seconds": st.seconds, "rules": st.rules, "rules_skipped": st.rules_skipped}
 
 
 class Scan:

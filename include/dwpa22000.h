@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DWPA_ABI_VERSION 1
+#define DWPA_ABI_VERSION 2   /* 2: dwpa_crack_stats.rules / rules_skipped, dwpa_rules_count */
 
 /* ---- return codes ------------------------------------------------------------------------------------------ */
 #define DWPA_MISS 0            /* no key matched (PHP: False)                                                 */
@@ -127,7 +127,9 @@ int dwpa_pbkdf2_pmk(const dwpa_bytes *keys, size_t nkeys, const uint8_t *essid, 
 int dwpa_hc_unhex(const uint8_t *in, size_t in_len, uint8_t *out, size_t *out_len);
 /* Parse one hashline with check_key_m22000's acceptance rules (common.php:157-237) and describe the nonce-
  * correction attempt lists the verifier would run for `nc` (host only, no device needed).  Returns 0 or the
- * negative parse code.  essid is copied up to essid_cap bytes (essid_len holds the full length). */
+ * negative parse code.  essid holds the first min(essid_len, 32) bytes of the decoded ESSID and essid_len its full
+ * length: PHP accepts longer ESSIDs (any even-length hex, common.php:28-36) and the check uses all of them; only
+ * this description is cut.  mac_ap / mac_sta likewise hold the first 16 bytes. */
 typedef struct {
     int32_t type;              /* 1 PMKID, 2 EAPOL */
     int32_t keyver;            /* EAPOL key version (0 if unknown) */
@@ -168,22 +170,36 @@ int dwpa_crack_files_ex(const char *hash_file, const char *const *dicts, size_t 
                         int32_t *dict_status);
 /* What the calling thread's last dwpa_crack_files(_ex) call did, for a hashcat-style end-of-run summary
  * (help_crack shows hashcat's output, help_crack.py:776): dictionary words read, candidates derived (inside the
- * 8..63 filter, after the rules), hashlines loaded and cracked, wall time.  Returns 0, or DWPA_E_ARG before any
- * call in this thread. */
+ * 8..63 filter, after the rules), hashlines loaded and cracked, wall time, and the rules file's rules loaded and
+ * skipped (a line that does not parse is skipped with a stderr message, as hashcat's "Skipping invalid or
+ * unsupported rule"; 0 / 0 without a rules file).  Returns 0, or DWPA_E_ARG before any call in this thread. */
 typedef struct {
     uint64_t words;
     uint64_t candidates;
     uint32_t hashes;
     uint32_t cracked;
     double seconds;
+    uint32_t rules;            /* rules loaded from rules_file (ABI 2) */
+    uint32_t rules_skipped;    /* rule lines of rules_file that did not parse (ABI 2) */
 } dwpa_crack_stats;
 int dwpa_crack_last_stats(dwpa_crack_stats *out);
 
-/* GPU rule application (replaces `hashcat --stdout -r rules words`, help_crack.py:508,575): out holds
- * nwords*nrules candidates of 256 bytes (word-major), out_len their lengths (0xFFFFFFFF = input rejected).
- * With out == NULL only *nrules_out is set (number of rules that parse). */
+/* hashcat rules (the whole rule language of hashcat >= 6.2.6: every mangling, reject and memory function; one
+ * rule per line, '#' comments; semantics in dwpa_amd/csrc/rules.hpp and oracle/rules.py).
+ * GPU rule application (replaces `hashcat --stdout -r rules words`, help_crack.py:508,575): out holds
+ * nwords*nrules candidates of 256 bytes (word-major), out_len their lengths (0xFFFFFFFF = the input word or a
+ * reject / memory function rejected it).  With out == NULL only *nrules_out is set (number of rules that parse).
+ * Rule lines that do not parse are skipped with a stderr message each (out != NULL). */
 int dwpa_rules_expand(int device, const char *rules_text, size_t rules_len, const dwpa_bytes *words, size_t nwords,
                       uint8_t *out, uint32_t *out_len, uint32_t *nrules_out);
+/* Host only: rule `rule_index` (0-based among the rules that parse) applied to one word by the same interpreter the
+ * GPU runs, compiled for the host; *out_len = 0xFFFFFFFF when rejected.  out holds 256 bytes. */
+int dwpa_rules_apply_host(const char *rules_text, size_t rules_len, uint32_t rule_index, const uint8_t *word,
+                          size_t word_len, uint8_t *out, uint32_t *out_len);
+/* Host only: rule lines present (neither empty nor '#' comments), how many of them parse, and the 1-based line
+ * number of the first one that does not (0 = none). */
+int dwpa_rules_count(const char *rules_text, size_t rules_len, uint32_t *nrules_present, uint32_t *nrules_parsed,
+                     uint32_t *first_skipped_line);
 
 /* ---- device-resident scan API (inputs already in HBM; used by the client loop and bench.py) --------------- */
 typedef struct dwpa_scan dwpa_scan;
@@ -213,8 +229,10 @@ int dwpa_scan_verify(dwpa_scan *scan, int group, void *hip_stream);
  * over all of their uncracked lines.  Hits are the same as the per-group calls'.  batch must be a multiple of
  * 64 (dwpa_scan_create rounds it up). */
 int dwpa_scan_run(dwpa_scan *scan, void *hip_stream);
-/* Synchronises the stream, returns hits found since the last call (*nhits may exceed cap: then call again
- * with a bigger buffer is not possible -- size cap >= batch). */
+/* Synchronises the stream and copies the hits found since the last call into out[0..min(*nhits, cap)).  *nhits is
+ * the number found, which can exceed cap; the hits beyond cap are lost, because the call also clears the device's
+ * hit buffer.  A cap of at least the scan's batch size always suffices: a batch yields at most one hit per
+ * candidate slot and line. */
 int dwpa_scan_hits(dwpa_scan *scan, dwpa_hit *out, size_t cap, size_t *nhits, void *hip_stream);
 /* Candidate slots filled by the last load (synchronises). */
 int dwpa_scan_loaded(dwpa_scan *scan, uint32_t *count, void *hip_stream);

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = L.load()
-    assert lib.dwpa_abi_version() == 1
+    assert lib.dwpa_abi_version() == 2  # 2: dwpa_crack_stats.rules / rules_skipped, dwpa_rules_count
     for code in [0, 1, -1, -2, -3, -4, -10, -12, -13, -14, -15, -16, -999]:
         assert lib.dwpa_strerror(code)
 
@@ -50,6 +50,20 @@ def test_hash_m22000_matches_oracle():
     import dwpa_amd
     for line in S.CHALLENGE_LINES + [b"WPA*01*a*b*c*d*e*f*g*h*i", b"WPA*01*x", b""]:
         assert dwpa_amd.hash_m22000(line) == O.c_hash_m22000(line)
+
+
+def test_line_info_long_essid_prefix_and_length():
+    """dwpa_line_info.essid holds the first 32 bytes of a longer ESSID and essid_len the full length (PHP accepts
+    any even-length hex ESSID, common.php:28-36; the check itself salts with all of it)."""
+    import dwpa_amd
+    essid = bytes(range(65, 65 + 52))
+    line = S.pmkid_line(b"password", essid, bytes(6), bytes([1] * 6))
+    info = L.LineInfo()
+    assert L.load().dwpa_parse_m22000(line, len(line), 128, L.DWPA_NC_PHP, ctypes.byref(info)) == 0
+    assert info.essid_len == 52
+    assert bytes(info.essid) == essid[:32]
+    d = dwpa_amd.parse_m22000(line)
+    assert (d["essid"], d["essid_len"]) == (essid[:32], 52)
 
 
 def _gpu_present():

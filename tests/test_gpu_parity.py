@@ -203,6 +203,72 @@ def test_rules_expand_vs_oracle():
     assert got == exp
 
 
+@pytest.mark.parametrize("group", ["single", "memory", "combo"])
+def test_rules_language_gpu_vs_oracle(group):
+    """every function of hashcat's rule language (mangling, reject and memory functions) at edge
+    arguments -- positions 0, len-1, len and beyond -- on words of 1..256 bytes (and the rejected empty and
+    257-byte words), alone, after M, and in random combinations: the GPU rule engine equals oracle/rules.py."""
+    from tests import rule_corpus as C
+    rules = {"single": C.single_function_rules, "memory": C.memory_rules, "combo": C.combo_rules}[group]()
+    words = C.words()
+    got = dwpa_amd.rules_expand("\n".join(rules).encode("latin-1"), words)
+    exp = R.expand(rules, words)
+    bad = [(rules[j], w[:16], len(w), got[i][j], exp[i][j]) for i, w in enumerate(words) for j in range(len(rules))
+           if got[i][j] != exp[i][j]]
+    assert not bad, bad[:8]
+
+
+def test_crack_files_every_rule_family(tmp_path):
+    """A work unit whose server rule file (-S -r, help_crack.py:931-933) uses every family of the language beyond
+    bestWPA.rule's ops -- insert/overwrite/extract/omit, swaps and byte arithmetic, block duplication, title case and
+    toggle-after-separator, reject functions, memory functions -- plus lines that do not parse.  A PSK planted
+    behind each family is found; a PSK only a rejected candidate would equal is not; the skipped lines are counted
+    in dwpa_crack_last_stats, not dropped silently."""
+    rng = random.Random(21)
+    essid, _, sta, _, _ = S.random_net(rng)
+    base = [S.random_psk(rng, 6, 14) for _ in range(3000)]
+    base[700] = b"pass word-xyz"
+    family = {"insert": "i4! o0P", "extract": "x15 $2 $0 $2 $4", "omit": "O23 ^#", "swap": "*03 k K",
+              "arith": "+0 -1 L2 R3 .4 ,5", "dupe": "y3 Y2", "title": "E $!", "toggle_sep": "30  30-",
+              "reject": ">9 /w !@ (p", "reject_eq": "=4  %1- $X", "memory": "M l 4", "memory_x": "u M X031 6",
+              "memory_q": "M r Q $9"}
+    invalid = ["I", "T", "X01", "3a-", "v12"]
+    rules = list(family.values())
+    rf = tmp_path / "help_crack.rules"
+    rf.write_text("\n".join(rules[:5] + invalid + rules[5:]) + "\n")
+    planted, lines = {}, []
+    for k, (name, rule) in enumerate(family.items()):
+        wi = 700 if name in ("title", "toggle_sep", "reject", "reject_eq") else 100 + 37 * k
+        psk = R.apply(R.parse(rule), base[wi])
+        assert psk is not None and 8 <= len(psk) <= 63, (name, base[wi], psk)
+        ap = bytes([2, 0, 0, 0, 0, k])
+        planted[ap.hex()] = psk
+        lines.append(S.pmkid_line(psk, essid, ap, sta))
+    # only the rejected candidate of word 1500 under '<8 $!' (the word is longer than 8) would equal this PSK
+    assert len(base[1500]) > 8
+    never = base[1500] + b"!"
+    rf.write_text(rf.read_text() + "<8 $!\n")
+    lines.append(S.pmkid_line(never, essid, bytes([2, 0, 0, 0, 1, 0]), sta))
+    hf = tmp_path / "h.hash"
+    hf.write_bytes(b"\n".join(lines) + b"\n")
+    d = tmp_path / "d.txt"
+    d.write_bytes(b"\n".join(base) + b"\n")
+    out = tmp_path / "o.key"
+    rc = dwpa_amd.crack_files(str(hf), [str(d)], str(rf), 8, str(out), batch=1 << 16)
+    assert all(R.apply(R.parse(r), w) != never for r in rules + ["<8 $!"] for w in base)  # no candidate equals it
+    assert rc == 1  # every planted line cracked, the never line not
+    got = {}
+    for rec in out.read_bytes().strip().split(b"\n"):
+        f = rec.split(b":", 4)
+        v = f[4]
+        if v.startswith(b"$HEX[") and v.endswith(b"]"):
+            v = bytes.fromhex(v[5:-1].decode())
+        got[f[1].decode()] = v
+    assert got == {k: v for k, v in planted.items()}
+    st = dwpa_amd.m22000.crack_stats()
+    assert (st["rules"], st["rules_skipped"]) == (len(rules) + 1, len(invalid))
+
+
 def test_crack_files_challenge(tmp_path):
     hf = tmp_path / "help_crack.hash"
     hf.write_bytes(b"\n".join(S.CHALLENGE_LINES) + b"\n")

@@ -99,6 +99,27 @@ def test_damaged_dictionary_is_removed_and_rc_returned(tmp_path, monkeypatch):
     assert sum(1 for _, c in logs if c == "WARNING") == 2
 
 
+def test_damaged_dictionary_kept_for_the_retry_of_a_failed_attempt(tmp_path, monkeypatch):
+    """an attempt that read a damaged download and then failed with a device error (rc -1) is
+    retried with the same dictionary list, so the file must still exist; it is removed only after the attempt that
+    counts (rc 0/1).  Deleting it first made the retry fail the library's up-front open check (DWPA_E_IO) and
+    broke the "device errors are retried, never returned" rule."""
+    conf = _conf(tmp_path)
+    a, b = _dict(tmp_path, "a.txt.gz"), _dict(tmp_path, "b.txt.gz")
+    import os
+    seen = []
+
+    def fake(hash_file, dicts, rules_file, nec, key_file, device_mask=0):
+        seen.append([os.path.exists(d) for d in dicts])
+        if len(seen) == 1:
+            return L.DWPA_RC_ERROR, [L.DWPA_DICT_OK, L.DWPA_DICT_DAMAGED]
+        return L.DWPA_RC_EXHAUSTED, [L.DWPA_DICT_OK, L.DWPA_DICT_DAMAGED]
+    monkeypatch.setattr(H.M, "crack_files_ex", fake)
+    assert run_cracker(conf, [a, b], sleepy=lambda: None, pprint=lambda *a: None) == 1
+    assert seen == [[True, True], [True, True]]
+    assert os.path.exists(a) and not os.path.exists(b)
+
+
 def test_failed_attempt_hits_are_rolled_back(tmp_path, monkeypatch):
     """An attempt that wrote a hit and then failed (device error) must not leave it behind: the retry writes it
     again, once."""
@@ -146,9 +167,10 @@ def test_end_of_run_summary(tmp_path, monkeypatch, capsys):
     conf = _conf(tmp_path)
     monkeypatch.setattr(H.M, "crack_files_ex", lambda *a, **k: (1, [L.DWPA_DICT_OK]))
     monkeypatch.setattr(H.M, "crack_stats", lambda: {"words": 1000, "candidates": 9_790_000, "hashes": 4,
-                                                     "cracked": 1, "seconds": 2.0})
+                                                     "cracked": 1, "seconds": 2.0, "rules": 148, "rules_skipped": 2})
     assert run_cracker(conf, [_dict(tmp_path)], sleepy=lambda: None, pprint=lambda *a: None) == 1
     out = capsys.readouterr().out
+    assert "Rules............: 148 loaded, 2 skipped (invalid or unsupported)" in out
     assert "Status...........: Exhausted" in out and "Recovered........: 1/4 (25.00%) Digests" in out
     assert "Progress.........: 9790000 candidates from 1000 words" in out and "4.9 MH/s" in out
     assert run_cracker(conf, [_dict(tmp_path)], sleepy=lambda: None, pprint=lambda *a: None, quiet=True) == 1

@@ -54,4 +54,4 @@ def test_best_wpa_ops_covered_by_tested_rule_set():
     missing = sorted(best_ops - tested_ops, key=str)
     assert not missing, missing
     # the op kinds the survey lists for the file
-    assert {op for op, _, _ in best_ops} == set(":rulcT$^][sD'dpf")
+    assert {op for op, *_ in best_ops} == set(":rulcT$^][sD'dpf")
