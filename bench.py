@@ -66,6 +66,51 @@ ISSUED_OPS_PER_COMPRESSION = 575.5
 PEAK_LANE_OPS = 256 * 128 * CLOCK_HZ
 
 
+def roofline_block(kernel, kernel_pmk_s, pmk_per_launch, kernel_ms, traffic_pmk, traffic_src, algo_bytes_per_pmk,
+                   peak_costs=None):
+    """The bench line's roofline object.  Headline (`achieved` / `peak` / `frac`): the guide's integer-VALU peak
+    (MI355X_MICROARCH.md: 256 CU x 128 int32 lane-ops/clk x 2.4 GHz = 78.64 T lane-ops/s) against SURVEY.md 8(d)'s
+    ideal 617 ops per SHA-1 compression x 16,388 compressions per PMK, so frac = PMKs per launch x 16,388 x 617 /
+    mean launch duration / 78.64e12.  Beside it: the same kernel against the issue-cost model measured on gfx950
+    (rotates and 3-input adds issue at half rate), and the most the guide basis can show under
+    that model."""
+    comp_s = kernel_pmk_s * COMPRESSIONS_PER_PMK
+    ops_s = comp_s * SURVEY_OPS_PER_COMPRESSION
+    return {
+        "bound": "valu",
+        "kernel": kernel,
+        "achieved": round(ops_s / 1e12, 3),
+        "peak": round(PEAK_LANE_OPS / 1e12, 3),
+        "unit": f"T int32 lane-ops/s ({SURVEY_OPS_PER_COMPRESSION} ops per SHA-1 compression x "
+                f"{COMPRESSIONS_PER_PMK} compressions per PMK)",
+        "frac": round(ops_s / PEAK_LANE_OPS, 4),
+        "peak_basis": "MI355X_MICROARCH.md: 256 CU x 128 int32 lane-ops/clk x 2.4 GHz = 78.64 T lane-ops/s; "
+                      f"SURVEY.md 8(d): {SURVEY_OPS_PER_COMPRESSION} ideal VALU ops per SHA-1 compression",
+        "roofline_pmk_per_s": round(PEAK_LANE_OPS / SURVEY_OPS_PER_COMPRESSION / COMPRESSIONS_PER_PMK, 1),
+        "traffic": round(traffic_pmk * pmk_per_launch) if traffic_pmk else None,
+        "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE of this workload, "
+                        + (traffic_src or "not measured") + ")",
+        "algorithmic_bytes": round(algo_bytes_per_pmk * pmk_per_launch),
+        "hbm_gbs": round(traffic_pmk * pmk_per_launch / (kernel_ms * 1e-3) / 1e9, 3) if traffic_pmk else None,
+        "kernel_ms": round(kernel_ms, 3),
+        "pmk_per_launch": pmk_per_launch,
+        "kernel_pmk_per_s": round(kernel_pmk_s, 1),
+        # the most the guide basis can show on gfx950: the cheapest compression under the measured issue costs
+        "frac_attainable_on_gfx950": round(PEAK_COMPRESSIONS * SURVEY_OPS_PER_COMPRESSION / PEAK_LANE_OPS, 4),
+        "frac_issue_cost_model": round(comp_s / PEAK_COMPRESSIONS, 4),
+        "issue_cost_model": {
+            "achieved": round(comp_s / 1e9, 3), "peak": round(PEAK_COMPRESSIONS / 1e9, 3),
+            "unit": "G SHA-1 compressions/s",
+            "roofline_pmk_per_s": round(PEAK_COMPRESSIONS / COMPRESSIONS_PER_PMK, 1),
+            "basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x 64 lanes / {C_MIN_CYCLES} SIMD-cycles per compression "
+                     "(measured gfx950 issue costs: full rate 2, half rate 4 SIMD-cycles per wave64 instruction; "
+                     "tools/cmin.py, " + (peak_costs or "profiles/r01/valu_issue_costs.json") + ")"},
+        "frac_nominal_ops": round(comp_s * ISSUED_OPS_PER_COMPRESSION / PEAK_LANE_OPS, 4),
+        "frac_nominal_ops_basis": f"{ISSUED_OPS_PER_COMPRESSION} VALU issued per compression (PMC) / "
+                                  "78.64 T int32 lane-ops/s",
+    }
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -514,7 +559,6 @@ def main():
     per_launch = list(counts) if w.groups > 1 else [c / w.groups for c in counts]
     pmk_per_launch = sum(per_launch) / len(per_launch)
     kernel_pmk_s = sum(per_launch) / (sum(kms) * 1e-3)
-    achieved = kernel_pmk_s * COMPRESSIONS_PER_PMK
     traffic_pmk = TRAFFIC_BYTES_PER_PMK.get(args.workload)
     if rank == 0:
         value = total / elapsed
@@ -536,38 +580,10 @@ def main():
             "data": "synthetic",
             "config": dict({"workload": w.description, "batch_per_step": w.B,
                             "parallelism": f"keyspace shards x{world}, no collective on the data path"}, **w.extra),
-            "roofline": {
-                "bound": "valu",
-                "kernel": "k_pbkdf2" if w.groups == 1 else "k_pbkdf2_mg + k_verify (per dwpa_scan_run)",
-                "achieved": round(achieved / 1e9, 3),
-                "peak": round(PEAK_COMPRESSIONS / 1e9, 3),
-                "unit": "G SHA-1 compressions/s",
-                "frac": round(achieved / PEAK_COMPRESSIONS, 4),
-                "traffic": round(traffic_pmk * pmk_per_launch) if traffic_pmk else None,
-                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE of this workload, "
-                                + TRAFFIC_SOURCE.get(args.workload, "not measured") + ")",
-                "algorithmic_bytes": round(w.algo_bytes_per_pmk * pmk_per_launch),
-                "hbm_gbs": round(traffic_pmk * pmk_per_launch / (kernel_ms * 1e-3) / 1e9, 3) if traffic_pmk else None,
-                "kernel_ms": round(kernel_ms, 3),
-                "pmk_per_launch": pmk_per_launch,
-                "kernel_pmk_per_s": round(kernel_pmk_s, 1),
-                "roofline_pmk_per_s": round(PEAK_COMPRESSIONS / COMPRESSIONS_PER_PMK, 1),
-                "peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz x 64 lanes / {C_MIN_CYCLES} SIMD-cycles per "
-                              "compression (measured gfx950 issue costs, tools/cmin.py; "
-                              + (args.peak_costs or "profiles/r01/valu_issue_costs.json") + ")",
-                # the same kernel against the guide's all-full-rate VALU peak (256 CU x 128 lane-ops/clk x 2.4 GHz)
-                "frac_guide_valu_peak": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * SURVEY_OPS_PER_COMPRESSION
-                                              / PEAK_LANE_OPS, 4),
-                "frac_guide_valu_peak_basis": f"{SURVEY_OPS_PER_COMPRESSION} ops per compression (SURVEY.md 8(d) "
-                                              "ideal count) / 78.64 T int32 lane-ops/s",
-                # the most that basis can show on gfx950: the issue-cost peak (rotates and add3 at half rate)
-                "frac_guide_valu_peak_attainable": round(PEAK_COMPRESSIONS * SURVEY_OPS_PER_COMPRESSION
-                                                         / PEAK_LANE_OPS, 4),
-                "frac_nominal_ops": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * ISSUED_OPS_PER_COMPRESSION
-                                          / PEAK_LANE_OPS, 4),
-                "frac_nominal_ops_basis": f"{ISSUED_OPS_PER_COMPRESSION} VALU issued per compression (PMC) / "
-                                          "78.64 T int32 lane-ops/s",
-            },
+            "roofline": roofline_block("k_pbkdf2_gfx950_q" if w.groups == 1 else
+                                       "k_pbkdf2_mg + k_verify (per dwpa_scan_run)", kernel_pmk_s, pmk_per_launch,
+                                       kernel_ms, traffic_pmk, TRAFFIC_SOURCE.get(args.workload),
+                                       w.algo_bytes_per_pmk, args.peak_costs),
             "cpu_baseline": cpu,
             "hits_verified": verified,
             "pbkdf2_kernel": "k_pbkdf2 (hipcc schedule)" if os.environ.get("DWPA_PBKDF2_PLAIN", "0") not in ("", "0")
@@ -705,17 +721,8 @@ def main_strong(args, world, rank, local):
             "speedup": round(args.t1_s / t_exhaust, 4) if args.t1_s else None,
             "speedup_basis": f"S(G) = T1 / TG with T1 = {args.t1_s} s (--t1-s)" if args.t1_s else None,
             "shards": shards,
-            "roofline": {
-                "bound": "valu", "kernel": "k_pbkdf2 (rank 0)",
-                "achieved": round(kernel_pmk_s * COMPRESSIONS_PER_PMK / 1e9, 3),
-                "peak": round(PEAK_COMPRESSIONS / 1e9, 3), "unit": "G SHA-1 compressions/s",
-                "frac": round(kernel_pmk_s * COMPRESSIONS_PER_PMK / PEAK_COMPRESSIONS, 4),
-                "traffic": round(traffic_pmk * pmk_per_launch), "algorithmic_bytes": round(ALGO_BYTES_PER_PMK * pmk_per_launch),
-                "traffic_unit": "HBM bytes per launch (" + TRAFFIC_SOURCE["c4"] + ")",
-                "kernel_ms": round(kernel_ms, 3), "pmk_per_launch": pmk_per_launch,
-                "kernel_pmk_per_s": round(kernel_pmk_s, 1),
-                "frac_guide_valu_peak": round(kernel_pmk_s * COMPRESSIONS_PER_PMK * SURVEY_OPS_PER_COMPRESSION
-                                              / PEAK_LANE_OPS, 4)},
+            "roofline": roofline_block("k_pbkdf2_gfx950_q (rank 0)", kernel_pmk_s, pmk_per_launch, kernel_ms,
+                                       traffic_pmk, TRAFFIC_SOURCE["c4"], ALGO_BYTES_PER_PMK, args.peak_costs),
             "cpu_baseline": cpu, "hits_verified": verified,
             "hits_checked": "the planted PSK 73019412 with its PMK, once per timed pass, on the rank holding it; "
                             "no other hit on any rank"})
@@ -1114,24 +1121,35 @@ def main_files_rules(args, world, rank, local):
 def cpu_baseline_jobs(jobs, seconds):
     """The PHP path for the same jobs: check_key_m22000 per job on the OpenSSL restatement (oracle/), as PHP-FPM
     runs requests: one job per worker process at a time, min(16, affinity) single-threaded processes (oracle/
-    php_pool.py), over a bounded prefix of the job list; plus one process alone (one PHP request after another)."""
+    php_pool.py; the box's CPU share per GPU), over a bounded prefix of the job list; the same with one process per
+    physical core of the host (`all_host`); plus one process alone (one PHP request after another)."""
     from oracle.php_pool import PhpPool, _job_pmks
     hc = host_cpu()
     P = hc["threads_all"]
     if len(jobs) == 1:
         line, keys, pmk, nc = jobs[0]
         return cpu_baseline(line, lambda m: keys[-m:], seconds, "keys (ending at the true PSK)", nc=nc)
-    pool = PhpPool(P)
-    try:
-        done, nkeys, dt = pool.job_pmks(jobs, seconds)
-    finally:
-        pool.close()
+
+    def run_pool(p, budget):
+        pool = PhpPool(p)
+        try:
+            return pool.job_pmks(jobs, budget)
+        finally:
+            pool.close()
+    done, nkeys, dt = run_pool(P, seconds)
     done1, nkeys1 = 0, 0
     t1 = time.perf_counter()
     while done1 < len(jobs) and time.perf_counter() - t1 < seconds / 3:
         nkeys1 += _job_pmks(jobs[done1])
         done1 += 1
     dt1 = time.perf_counter() - t1
+    all_host = None
+    PA = hc["all_host_processes"]
+    if PA > P:
+        doneA, nkeysA, dtA = run_pool(PA, seconds / 2)
+        all_host = {"value": round(nkeysA / dtA, 1), "unit": "PMK/s", "cores": PA, "processes": PA,
+                    "sample": f"first {doneA} jobs ({nkeysA} PMKs derived), one job per free worker, {dtA:.1f} s",
+                    "scaling_vs_one_process": round(nkeysA / dtA / (nkeys1 / dt1), 2)}
     return dict({"value": round(nkeys / dt, 1), "unit": "PMK/s", "cores": P, "kind": "port",
                  "workers": f"{P} single-threaded worker processes (PHP-FPM model, oracle/php_pool.py)",
                  "sample": f"first {done} jobs ({nkeys} PMKs derived: a job stops at its first matching key), "
@@ -1139,14 +1157,16 @@ def cpu_baseline_jobs(jobs, seconds):
                  "scaling_vs_one_process": round(nkeys / dt / (nkeys1 / dt1), 2),
                  "one_thread": {"value": round(nkeys1 / dt1, 1), "unit": "PMK/s", "cores": 1,
                                 "sample": f"first {done1} jobs ({nkeys1} PMKs derived) in one process (one PHP "
-                                          f"request after another), {dt1:.1f} s"}},
+                                          f"request after another), {dt1:.1f} s"},
+                 "all_host": all_host},
                 **hc)
 
 
 def host_cpu():
     """CPU model and counts of the host the baseline runs on.  threads_all = min(16, affinity): a GPU box gives one
     GPU a 16-core share, and its nproc reports the whole machine.  physical_cores_affinity counts distinct cores of
-    the affinity set (SMT siblings once)."""
+    the affinity set (SMT siblings once); all_host_processes = that count, the whole-host PHP-FPM pool (one worker
+    per physical core).  cgroup_cpu_max is the container's CPU quota (cgroup v2 cpu.max), if any."""
     from oracle.php_pool import physical_cores
     model = "unknown"
     try:
@@ -1154,46 +1174,69 @@ def host_cpu():
             model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), model)
     except OSError:
         pass
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota = f.read().strip()
+    except OSError:
+        pass
     cpus = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else set(range(os.cpu_count() or 1))
+    phys = physical_cores(cpus)
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(cpus),
-            "physical_cores_affinity": physical_cores(cpus), "threads_all": max(1, min(16, len(cpus)))}
+            "physical_cores_affinity": phys, "threads_all": max(1, min(16, len(cpus))),
+            "all_host_processes": max(1, min(len(cpus), phys)), "cgroup_cpu_max": quota}
 
 
 def cpu_baseline(line, keys_fn, seconds, what, nc=NC):
     """The PHP CPU path: check_key_m22000(line, [key]) once per key (one PHP request per key, as put_work does,
     common.php:902), restated in C on OpenSSL (oracle/; PKCS5_PBKDF2_HMAC is the call openssl_pbkdf2 makes,
     common.php:178-180,246-248).  Timed as PHP-FPM serves requests -- min(16, affinity) single-threaded worker
-    processes (oracle/php_pool.py) -- and in one process (one PHP request), over bounded samples of the workload's
-    own candidates that end at the planted PSK, which both runs must find.  PHP nonce window nc=8 (21 attempts
-    per EAPOL key) unless the leg's jobs carry their own."""
+    processes (oracle/php_pool.py; the box's CPU share per GPU), and one worker per physical core of the whole host
+    (`all_host`, the node comparison) -- and in one process (one PHP request), over bounded samples of the
+    workload's own candidates that end at the planted PSK, which every run must find.  PHP nonce window nc=8 (21
+    attempts per EAPOL key) unless the leg's jobs carry their own."""
     from oracle import oracle as O
     from oracle.php_pool import PhpPool
     hc = host_cpu()
     P = hc["threads_all"]
-    pool = PhpPool(P)
-    try:
-        probe = keys_fn(64 * P)
-        pool.check_keys(line, probe, nc)  # first checks in each worker (OpenSSL's method caches, clocks)
-        _, dtp = pool.check_keys(line, probe, nc)
-        rate = len(probe) / dtp
-        m = int(max(len(probe), min(400_000, rate * seconds)))
-        sample = keys_fn(m)
-        idx, dt = pool.check_keys(line, sample, nc)
-    finally:
-        pool.close()
+
+    def run_pool(p, budget):
+        pool = PhpPool(p)
+        try:
+            probe = keys_fn(64 * p)
+            pool.check_keys(line, probe, nc)  # first checks in each worker (OpenSSL's method caches, clocks)
+            _, dtp = pool.check_keys(line, probe, nc)
+            rate = len(probe) / dtp
+            m = int(max(len(probe), min(400_000 * max(1, p // 16), rate * budget)))
+            sample = keys_fn(m)
+            idx, dt = pool.check_keys(line, sample, nc)
+        finally:
+            pool.close()
+        return rate, sample, idx, dt
+    rate, sample, idx, dt = run_pool(P, seconds)
+    m = len(sample)
     one = keys_fn(int(max(16, min(m, rate / P * seconds / 3))))
     t1 = time.perf_counter()
     idx1, _ = O.c_check_many(line, one, nc, 1)
     dt1 = time.perf_counter() - t1
+    all_host, found_all = None, True
+    PA = hc["all_host_processes"]
+    if PA > P:
+        _, sA, idxA, dtA = run_pool(PA, seconds / 2)
+        found_all = idxA == len(sA) - 1
+        all_host = {"value": round(len(sA) / dtA, 1), "unit": "PMK/s", "cores": PA, "processes": PA,
+                    "sample": f"{len(sA)} {what} ending at the planted PSK, one check per key, {dtA:.1f} s",
+                    "scaling_vs_one_process": round(len(sA) / dtA / (len(one) / dt1), 2)}
     return dict({"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": P, "kind": "port",
                  "workers": f"{P} single-threaded worker processes (PHP-FPM model, oracle/php_pool.py)",
                  "sample": f"{len(sample)} {what} ending at the planted PSK, check_key_m22000(line, [key], False, "
                            f"{nc}) per key, {dt:.1f} s",
-                 "found_planted": idx == len(sample) - 1 and idx1 == len(one) - 1,
+                 "found_planted": idx == len(sample) - 1 and idx1 == len(one) - 1 and found_all,
                  "scaling_vs_one_process": round(len(sample) / dt / (len(one) / dt1), 2),
                  "one_thread": {"value": round(len(one) / dt1, 1), "unit": "PMK/s", "cores": 1,
                                 "sample": f"the last {len(one)} of them in one process (one PHP request), "
-                                          f"{dt1:.1f} s"}},
+                                          f"{dt1:.1f} s"},
+                 "all_host": all_host},
                 **hc)
 
 

@@ -36,3 +36,9 @@ for l in open('$O/clock_idle.jsonl'):
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread \
     -k "rules or rule_family" > $O/pytest_rules.log 2>&1
 rc=$?; tail -3 $O/pytest_rules.log; guard $rc
+# the bench line's new roofline object and the whole-host CPU baseline
+timeout -k 10 400 python3 bench.py --steps 3 --warmup 1 > $O/bench_short.json 2> $O/bench_short.err
+guard $?
+python3 -c "
+import json; d=json.load(open('$O/bench_short.json')); r=d['roofline']; c=d['cpu_baseline']
+print(d['value'], r['frac'], r['frac_issue_cost_model'], r['frac_attainable_on_gfx950'], c['value'], c['one_thread']['value'], c['all_host'])"
