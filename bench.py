@@ -905,13 +905,57 @@ def main_latency(args, world, rank, local):
                          "dwpa_check_batch vs 202 check_key_m22000 calls", "keys": 202,
                  "gpu_ms_per_call": round(gpu_ms, 3), "cpu_1core_ms_per_call": round(cpu_ms, 3),
                  "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp})
+    # Caller-PMK checks (no PBKDF2: pure verify work), each once per sibling net of a crack:
+    #   zero-PMK     check_key_m22000($struct, [''], $zpmk)                        common.php:592 (default nc=128)
+    #   PMK reuse    check_key_m22000($struct, [$pass], $pmk, (|nc| << 1) + 1)      common.php:606 (nc up to 131)
+    #   propagation  check_key_m22000($struct, [''], $pmk, |nc| * 2 + 128)          common.php:919 (nc up to 258)
+    # A sibling is usually not the same network, so the miss (all 1 + 4 * ((nc >> 1) + 1) attempts run) is the
+    # common case; the hit rows plant the correction near the middle of the window.
+    zpmk = bytes(32)
+    for site, nc, key, use_true, hit in (("zero-PMK (common.php:592)", 128, b"", False, False),
+                                         ("PMK reuse (common.php:606)", 131, None, True, True),
+                                         ("PMK propagation, hit (common.php:919)", 258, b"", True, True),
+                                         ("PMK propagation, miss (common.php:919)", 258, b"", False, False)):
+        for kind in ("pmkid", "eapol-kv2", "eapol-kv3"):
+            psk = S.fast_psk(rng)
+            e2, a2, s2, an2, sn2 = S.random_net(rng, essid_len=10)
+            kv = {"eapol-kv2": 2, "eapol-kv3": 3}.get(kind)
+            line = (S.pmkid_line(psk, e2, a2, s2) if kv is None else
+                    S.eapol_line(psk, e2, a2, s2, an2, sn2, kv, 37 if hit else 0, "LE", rng=rng))
+            pmk = S.pmk(psk, e2) if use_true else (zpmk if site.startswith("zero") else S.pmk(S.fast_psk(rng), e2))
+            keys = [psk if key is None else key]
+            gpu_ms, got = timed(lambda: dwpa_amd.check_key_m22000(line, keys, pmk, nc), reps)
+            cpu_ms, exp = timed(lambda: O.c_check_key_m22000(line, keys, pmk, nc), reps)
+            rows.append({"call": f"{site}, {kind}, caller PMK, nc={nc}, {'hit' if hit else 'miss'}", "keys": 1,
+                         "caller_pmk": True, "nc": nc, "hit": bool(got),
+                         "gpu_ms_per_call": round(gpu_ms, 3), "cpu_1core_ms_per_call": round(cpu_ms, 3),
+                         "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp and bool(got) == hit})
+    # one crack's propagation over 16 sibling nets as a single dwpa_check_batch (the batched snippet of INTEGRATION.md)
+    jobs = []
+    for i in range(16):
+        psk = S.fast_psk(rng)
+        e2, a2, s2, an2, sn2 = S.random_net(rng, essid_len=10)
+        line = (S.pmkid_line(psk, e2, a2, s2) if i % 4 == 0 else
+                S.eapol_line(psk, e2, a2, s2, an2, sn2, 2 + (i % 2), (i % 5) - 2, "BE", rng=rng))
+        jobs.append((line, [b""], S.pmk(psk if i % 3 else S.fast_psk(rng), e2), 258))
+    batch = dwpa_amd.BatchJobs(jobs)
+    gpu_ms, _ = timed(lambda: batch.run(), reps)
+    got = batch.results()
+    t0 = time.perf_counter()
+    exp = [O.c_check_key_m22000(*j) for j in jobs]
+    cpu_ms = (time.perf_counter() - t0) * 1e3
+    rows.append({"call": "PMK propagation to 16 sibling nets (PMKID + EAPOL keyver 2/3, nc=258) in one "
+                         "dwpa_check_batch vs 16 check_key_m22000 calls", "keys": 16, "caller_pmk": True, "nc": 258,
+                 "gpu_ms_per_call": round(gpu_ms, 3), "cpu_1core_ms_per_call": round(cpu_ms, 3),
+                 "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp})
     ok = all(r["same_result"] for r in rows)
     if rank == 0:
         emit({"metric": "ms per server check call (latency), m22000", "value": rows[0]["gpu_ms_per_call"],
                           "unit": "ms", "n_gpus": world, "steps": reps, "warmup": 1, "higher_is_better": False,
                           "dtype": "u32", "data": "synthetic",
                           "config": {"workload": "C1 latency: FFI calls of 1/16/202 keys (put_work, common.php:902,"
-                                                 "937) beside one CPU core", "parallelism": "none"},
+                                                 "937) and caller-PMK checks (common.php:592,606,919) beside one "
+                                                 "CPU core", "parallelism": "none"},
                           "rows": rows, "cpu_model": host_cpu()["cpu_model"], "hits_verified": ok})
     if rank == 0 and not ok:
         sys.exit(3)

@@ -98,10 +98,20 @@ __global__ __launch_bounds__(256) void k_pbkdf2(const uint32_t* __restrict__ mid
     pbkdf2_body(mid, cap, base, count, counter, salt, nsalt, pmk);
 }
 
+// Lanes [live, count) of a padded launch (lone_pad below) repeat slot live-1's derivation and store nothing.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_ms(
     const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
-    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk) {
-    pbkdf2_body_ms(mid, cap, count, pool, sref, pmk);
+    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, uint32_t live) {
+    const uint32_t blk = blockIdx.y;
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= count) return;
+    const uint32_t ss = min(s, live - 1);
+    uint32_t hi[5], ho[5], t[5];
+    load_mid(mid, cap, ss, hi, ho);
+    const uint32_t* e = pool + sref[ss];
+    const uint32_t nsalt = e[0];
+    pbkdf2_lane<false>(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
+    if (s < live) store_block(pmk, cap, s, blk, t);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_mg(const uint32_t* __restrict__ mid, uint32_t cap,
@@ -676,10 +686,28 @@ hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base,
     return hipGetLastError();
 }
 
+// Lone-wave derives are rounded up to whole waves of live lanes (the extra lanes repeat the last key and store
+// nothing).  On gfx950 a wave whose EXEC mask is partial runs a dependent VALU chain 18 % slower alone on its SIMD
+// and 39 % slower with 8 such waves on the chip, at the same shader clock (tools/clock_idle.hip,
+// profiles/r04/small_call/clock_lanes.jsonl); a one-key server call took 9.6-11.8 ms against 8.3 ms for 202 keys.
+// Padded, it takes 8.4 ms.  DWPA_LONE_PAD = 0 (off) / 64 (default: whole waves) / 256 (whole workgroups) for A/B.
+static uint32_t lone_pad() {
+    static const uint32_t pad = [] {
+        const char* e = getenv("DWPA_LONE_PAD");
+        const int v = e ? atoi(e) : 64;
+        return (uint32_t)(v == 64 || v == 256 ? v : 0);
+    }();
+    return pad;
+}
+
 hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                   const uint32_t* sref, uint32_t* pmk, hipStream_t s) {
+    count = min(count, cap);
     if (count == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pbkdf2_ms, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, count, pool, sref, pmk);
+    const uint32_t pad = lone_pad();
+    const uint32_t launch = pad ? (count + pad - 1) / pad * pad : count;
+    hipLaunchKernelGGL(k_pbkdf2_ms, dim3(cdiv(launch, 256), 2), dim3(256), 0, s, mid, cap, launch, pool, sref, pmk,
+                       count);
     return hipGetLastError();
 }
 

@@ -239,8 +239,9 @@ def test_crack_files_every_rule_family(tmp_path):
     planted, lines = {}, []
     for k, (name, rule) in enumerate(family.items()):
         wi = 700 if name in ("title", "toggle_sep", "reject", "reject_eq") else 100 + 37 * k
+        while not 8 <= len(R.apply(R.parse(rule), base[wi]) or b"") <= 63:  # the first word the rule keeps
+            wi += 1
         psk = R.apply(R.parse(rule), base[wi])
-        assert psk is not None and 8 <= len(psk) <= 63, (name, base[wi], psk)
         ap = bytes([2, 0, 0, 0, 0, k])
         planted[ap.hex()] = psk
         lines.append(S.pmkid_line(psk, essid, ap, sta))

@@ -22,7 +22,8 @@
     } while (0)
 
 __global__ __launch_bounds__(64) void k_chain(unsigned long long* stamps, unsigned iters, unsigned seed,
-                                              unsigned* sink) {
+                                              unsigned* sink, unsigned lanes) {
+    if (threadIdx.x >= lanes) return;  // partial EXEC: only `lanes` lanes of the wave run the chain
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     unsigned a = seed + threadIdx.x, b = a * 7u + 1u;
     for (unsigned i = 0; i < iters; i++) {
@@ -58,19 +59,23 @@ int main(int argc, char** argv) {
     // calibrate: iterations for ~6 ms at a warm clock (dependent full-rate op: ~4-8 cycles each at 1 wave per SIMD)
     unsigned iters = 1000;
     for (int c = 0; c < 6; c++) {
-        hipLaunchKernelGGL(k_chain, dim3(1), dim3(64), 0, 0, d_st, iters, 1u, d_sink);
+        hipLaunchKernelGGL(k_chain, dim3(1), dim3(64), 0, 0, d_st, iters, 1u, d_sink, 64u);
         CHK(hipDeviceSynchronize());
         CHK(hipMemcpy(h, d_st, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         const double ms = h[1] / 1e5;
         iters = (unsigned)(iters * 6.0 / (ms > 0.01 ? ms : 0.01));
     }
     fprintf(stderr, "iters %u\n", iters);
+    const unsigned lane_modes[] = {64, 16, 2, 1};
+    const bool lanes_only = getenv("CLOCK_LANES") != nullptr;  // only the partial-EXEC sweep (1 and 8 waves, no gap)
     for (double gap : gaps)
         for (int w : waves)
+            for (unsigned lanes : lane_modes)
             for (int r = 0; r < reps; r++) {
+                if (lanes_only ? (gap > 0 || w > 8) : lanes != 64) continue;
                 if (gap > 0) usleep((useconds_t)(gap * 1e6));
                 const double t0 = now_s();
-                hipLaunchKernelGGL(k_chain, dim3(w), dim3(64), 0, 0, d_st, iters, (unsigned)r, d_sink);
+                hipLaunchKernelGGL(k_chain, dim3(w), dim3(64), 0, 0, d_st, iters, (unsigned)r, d_sink, lanes);
                 CHK(hipDeviceSynchronize());
                 const double wall = now_s() - t0;
                 CHK(hipMemcpy(h, d_st, 4 * w * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -83,9 +88,9 @@ int main(int argc, char** argv) {
                     const double ms = h[4 * i + 1] / 1e5;
                     ms_max = ms > ms_max ? ms : ms_max;
                 }
-                printf("{\"gap_s\": %.3f, \"waves\": %d, \"rep\": %d, \"clock_mhz_mean\": %.1f, \"clock_mhz_min\": %.1f, "
+                printf("{\"gap_s\": %.3f, \"waves\": %d, \"lanes\": %u, \"rep\": %d, \"clock_mhz_mean\": %.1f, \"clock_mhz_min\": %.1f, "
                        "\"clock_mhz_max\": %.1f, \"kernel_ms\": %.3f, \"wall_ms\": %.3f}\n",
-                       gap, w, r, mhz_sum / w, mhz_min, mhz_max, ms_max, wall * 1e3);
+                       gap, w, lanes, r, mhz_sum / w, mhz_min, mhz_max, ms_max, wall * 1e3);
                 fflush(stdout);
             }
     return 0;
