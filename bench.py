@@ -1187,13 +1187,12 @@ def cpu_baseline_jobs(jobs, seconds):
         nkeys1 += _job_pmks(jobs[done1])
         done1 += 1
     dt1 = time.perf_counter() - t1
-    all_host = None
-    PA = hc["all_host_processes"]
-    if PA > P:
+    def measure_all(PA):
         doneA, nkeysA, dtA = run_pool(PA, seconds / 2)
-        all_host = {"value": round(nkeysA / dtA, 1), "unit": "PMK/s", "cores": PA, "processes": PA,
-                    "sample": f"first {doneA} jobs ({nkeysA} PMKs derived), one job per free worker, {dtA:.1f} s",
-                    "scaling_vs_one_process": round(nkeysA / dtA / (nkeys1 / dt1), 2)}
+        return {"value": round(nkeysA / dtA, 1), "unit": "PMK/s",
+                "sample": f"first {doneA} jobs ({nkeysA} PMKs derived), one job per free worker, {dtA:.1f} s",
+                "scaling_vs_one_process": round(nkeysA / dtA / (nkeys1 / dt1), 2)}
+    all_host = all_host_row(hc, P, measure_all, nkeys1 / dt1, nkeys / dt)
     return dict({"value": round(nkeys / dt, 1), "unit": "PMK/s", "cores": P, "kind": "port",
                  "workers": f"{P} single-threaded worker processes (PHP-FPM model, oracle/php_pool.py)",
                  "sample": f"first {done} jobs ({nkeys} PMKs derived: a job stops at its first matching key), "
@@ -1224,11 +1223,36 @@ def host_cpu():
             quota = f.read().strip()
     except OSError:
         pass
+    quota_cpus = None
+    if quota and quota.split()[0] != "max":
+        q, per = quota.split()[:2]
+        quota_cpus = int(q) / int(per)
     cpus = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else set(range(os.cpu_count() or 1))
     phys = physical_cores(cpus)
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(cpus),
             "physical_cores_affinity": phys, "threads_all": max(1, min(16, len(cpus))),
-            "all_host_processes": max(1, min(len(cpus), phys)), "cgroup_cpu_max": quota}
+            "all_host_processes": max(1, min(len(cpus), phys)), "cgroup_cpu_max": quota, "cgroup_cpus": quota_cpus}
+
+
+def all_host_row(hc, P, measure, one_rate, pool_rate):
+    """cpu_baseline.all_host: the PHP-FPM pool of the whole host (one single-threaded worker per physical core),
+    measured when the process may use that many CPUs.  Under a cgroup CPU quota smaller than that (the GPU box
+    gives a job 16 CPUs: cpu.max 1600000 100000) 128 workers would only share 16 CPUs, so the row is then the
+    extrapolation one-process rate x physical cores x the measured pool's per-process efficiency, marked as such."""
+    PA = hc["all_host_processes"]
+    if PA <= P:
+        return None
+    quota = hc.get("cgroup_cpus")
+    if quota is None or quota >= PA:
+        row = measure(PA)
+        row.update({"cores": PA, "processes": PA, "kind": "measured"})
+        return row
+    eff = pool_rate / (P * one_rate)
+    return {"value": round(one_rate * PA * eff, 1), "unit": "PMK/s", "cores": PA, "processes": PA,
+            "kind": "extrapolated",
+            "basis": f"one process {one_rate:.1f} PMK/s x {PA} physical cores x {eff:.3f} (the {P}-process pool's "
+                     f"per-process efficiency); not measurable here: cgroup cpu.max {hc['cgroup_cpu_max']} = "
+                     f"{quota:g} CPUs for this job"}
 
 
 def cpu_baseline(line, keys_fn, seconds, what, nc=NC):
@@ -1263,19 +1287,20 @@ def cpu_baseline(line, keys_fn, seconds, what, nc=NC):
     t1 = time.perf_counter()
     idx1, _ = O.c_check_many(line, one, nc, 1)
     dt1 = time.perf_counter() - t1
-    all_host, found_all = None, True
-    PA = hc["all_host_processes"]
-    if PA > P:
+    found_all = [True]
+
+    def measure_all(PA):
         _, sA, idxA, dtA = run_pool(PA, seconds / 2)
-        found_all = idxA == len(sA) - 1
-        all_host = {"value": round(len(sA) / dtA, 1), "unit": "PMK/s", "cores": PA, "processes": PA,
-                    "sample": f"{len(sA)} {what} ending at the planted PSK, one check per key, {dtA:.1f} s",
-                    "scaling_vs_one_process": round(len(sA) / dtA / (len(one) / dt1), 2)}
+        found_all[0] = idxA == len(sA) - 1
+        return {"value": round(len(sA) / dtA, 1), "unit": "PMK/s",
+                "sample": f"{len(sA)} {what} ending at the planted PSK, one check per key, {dtA:.1f} s",
+                "scaling_vs_one_process": round(len(sA) / dtA / (len(one) / dt1), 2)}
+    all_host = all_host_row(hc, P, measure_all, len(one) / dt1, len(sample) / dt)
     return dict({"value": round(len(sample) / dt, 1), "unit": "PMK/s", "cores": P, "kind": "port",
                  "workers": f"{P} single-threaded worker processes (PHP-FPM model, oracle/php_pool.py)",
                  "sample": f"{len(sample)} {what} ending at the planted PSK, check_key_m22000(line, [key], False, "
                            f"{nc}) per key, {dt:.1f} s",
-                 "found_planted": idx == len(sample) - 1 and idx1 == len(one) - 1 and found_all,
+                 "found_planted": idx == len(sample) - 1 and idx1 == len(one) - 1 and found_all[0],
                  "scaling_vs_one_process": round(len(sample) / dt / (len(one) / dt1), 2),
                  "one_thread": {"value": round(len(one) / dt1, 1), "unit": "PMK/s", "cores": 1,
                                 "sample": f"the last {len(one)} of them in one process (one PHP request), "
