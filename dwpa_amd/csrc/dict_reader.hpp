@@ -2,6 +2,7 @@
 // wordlists, one candidate per line, $HEX[...] for non-printable words, maint.php:55-60).  Header-only so that
 // tools/inflate_bench.cpp measures exactly the reader the library runs.
 #pragma once
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <fcntl.h>
@@ -246,7 +247,13 @@ class BlockInflater {
             if (eof) {
                 int zerr = Z_OK;
                 gzerror(gz, &zerr);
-                damaged = zerr == Z_BUF_ERROR || why != nullptr;  // truncated: gzread delivered what it could
+                damaged = zerr == Z_BUF_ERROR;  // truncated: gzread delivered what it could
+                // Only zlib's own verdict marks a file damaged (help_crack deletes and re-downloads those).  Our
+                // decoder rejecting a stream that zlib reads to its end cleanly is a decoder divergence: report it,
+                // keep the file.
+                if (!damaged && why)
+                    fprintf(stderr, "[dwpa] gzip decoder rejected a stream zlib reads cleanly (%s); zlib's output used\n",
+                            why);
             }
             b.file_end = eof || damaged;
             b.damaged = damaged;
@@ -417,17 +424,32 @@ class DictCache {
     size_t hits() const { return hits_.load(); }
 
   private:
-    // Budget: DWPA_DICT_CACHE_MB, else min(4 GiB, a quarter of the memory available when the library first reads
-    // a dictionary) -- a volunteer's help_crack process keeps this much host RAM between work units at most.
+    // Budget: DWPA_DICT_CACHE_MB, else min(4 GiB, max(512 MiB, a quarter of MemAvailable when the library first
+    // reads a dictionary)) -- a volunteer's help_crack process keeps this much host RAM between work units at most.
+    // MemAvailable (/proc/meminfo) counts the reclaimable page cache; MemFree (_SC_AVPHYS_PAGES) does not, and on a
+    // long-running host with a warm cache it can be a small fraction of what is really available.
     DictCache() {
         const char* e = getenv("DWPA_DICT_CACHE_MB");
         if (e && *e) {
             budget_ = (size_t)atoll(e) << 20;
         } else {
-            const long pages = sysconf(_SC_AVPHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
-            const size_t avail = pages > 0 && psz > 0 ? (size_t)pages * (size_t)psz : 0;
-            budget_ = std::min<size_t>((size_t)4096 << 20, avail / 4);
+            size_t avail = mem_available();
+            if (!avail) {
+                const long pages = sysconf(_SC_AVPHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+                avail = pages > 0 && psz > 0 ? (size_t)pages * (size_t)psz : 0;
+            }
+            budget_ = std::min<size_t>((size_t)4096 << 20, std::max<size_t>((size_t)512 << 20, avail / 4));
         }
+    }
+    static size_t mem_available() {
+        FILE* f = fopen("/proc/meminfo", "r");
+        if (!f) return 0;
+        char line[256];
+        unsigned long long kb = 0;
+        while (fgets(line, sizeof line, f))
+            if (sscanf(line, "MemAvailable: %llu kB", &kb) == 1) break;
+        fclose(f);
+        return (size_t)kb << 10;
     }
     struct Entry {
         std::shared_ptr<const Chunks> chunks;

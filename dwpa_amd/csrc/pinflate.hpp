@@ -14,14 +14,18 @@
 //      32 KiB, checks every member's CRC-32 and ISIZE over the joined output, and hands the bytes on.
 // A chunk whose end does not land exactly on the next chunk's boundary (a false find) or any decode error stops the
 // parallel decode: the caller continues from the bytes delivered with zlib's gzread (dict_reader.hpp), which also
-// decides what a damaged stream yields.  The input is memory-mapped over a zero-filled anonymous region, so every
-// decoder can read GzipDecoder::PAD zero bytes past the end.
+// decides what a damaged stream yields.  The input is read (pread, by a loader thread running ahead of the workers)
+// into a zero-filled anonymous region, so every decoder can read GzipDecoder::PAD zero bytes past the end.  It is
+// not memory-mapped: another help_crack in the same directory may truncate and rewrite a dictionary while it is read
+// (cracked.txt.gz is re-downloaded every 100 work units), and a mapped page past the new end of file raises SIGBUS.
+// A short read leaves zeros, which fail the decode and hand the file to zlib (a damaged-file outcome, not a crash).
 #pragma once
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -49,7 +53,8 @@ class ParallelGunzip {
     // because the stream is damaged.
     static bool false_boundary(const char* err) {
         return err && (!strcmp(err, "deflate block boundary mismatch") ||
-                       !strcmp(err, "stream ended before the chunk boundary") || !strcmp(err, "mmap failed"));
+                       !strcmp(err, "stream ended before the chunk boundary") || !strcmp(err, "mmap failed") ||
+                       !strcmp(err, "short read"));
     }
     struct Stats {
         size_t chunks = 0;     // compressed chunks
@@ -85,26 +90,51 @@ class ParallelGunzip {
         : n_(n), chunk_(std::max<size_t>(chunk, 1u << 16)), nthreads_(std::max(1u, threads)) {
         const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
         maplen_ = (n + GzipDecoder::PAD + 16 + pg - 1) / pg * pg + pg;
-        void* area = mmap(nullptr, maplen_, PROT_READ, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        void* area = mmap(nullptr, maplen_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (area == MAP_FAILED) return;
-        if (n && mmap(area, n, PROT_READ, MAP_PRIVATE | MAP_FIXED, fd, 0) == MAP_FAILED) {
-            munmap(area, maplen_);
-            return;
-        }
         data_ = (const uint8_t*)area;
-        madvise(area, n, MADV_SEQUENTIAL);
         nchunks_ = (n + chunk_ - 1) / chunk_;
         jobs_.resize(nchunks_);
+        loader_ = std::thread([this, fd, area] { load(fd, (uint8_t*)area); });
         for (unsigned t = 0; t < nthreads_; t++) pool_.emplace_back([this] { worker(); });
     }
     ~ParallelGunzip() {
+        quit_flag_.store(true, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> lk(mu_);
             quit_ = true;
         }
         cv_.notify_all();
         for (auto& t : pool_) t.join();
+        if (loader_.joinable()) loader_.join();
         if (data_) munmap((void*)data_, maplen_);
+    }
+
+    // The loader: the file in order, LOAD_STEP bytes per pread, publishing how far it got.
+    static constexpr size_t LOAD_STEP = 4u << 20;
+    void load(int fd, uint8_t* area) {
+        size_t pos = 0;
+        while (pos < n_ && !quit_flag_.load(std::memory_order_relaxed)) {
+            const ssize_t r = pread(fd, area + pos, std::min(LOAD_STEP, n_ - pos), (off_t)pos);
+            if (r <= 0) {  // truncated (or unreadable) under us: the rest stays zero and fails the decode
+                short_.store(true, std::memory_order_relaxed);
+                break;
+            }
+            pos += (size_t)r;
+            std::lock_guard<std::mutex> lk(load_mu_);
+            loaded_.store(pos, std::memory_order_release);
+            load_cv_.notify_all();
+        }
+        std::lock_guard<std::mutex> lk(load_mu_);
+        loaded_.store(n_, std::memory_order_release);  // done (or given up): nothing more to wait for
+        load_cv_.notify_all();
+    }
+    // Wait until bytes [0, min(end, n)) are loaded.
+    void need(uint64_t end) {
+        end = std::min<uint64_t>(end, n_);
+        if (loaded_.load(std::memory_order_acquire) >= end) return;
+        std::unique_lock<std::mutex> lk(load_mu_);
+        load_cv_.wait(lk, [&] { return loaded_.load(std::memory_order_acquire) >= end; });
     }
 
     void submit(std::function<void()> f) {
@@ -133,7 +163,8 @@ class ParallelGunzip {
     }
 
     // first dynamic-block boundary in chunk j's bytes (NONE if there is none)
-    uint64_t find(size_t j) const {
+    uint64_t find(size_t j) {
+        need((uint64_t)(j + 3) * chunk_);  // the chunk, and blocks probed from its end into the next ones
         const uint64_t b = (uint64_t)j * chunk_ * 8, e = (uint64_t)std::min(n_, (j + 1) * chunk_) * 8;
         GzipDecoder dec(data_, n_, true);
         std::vector<uint16_t> scratch;
@@ -147,6 +178,7 @@ class ParallelGunzip {
 
     // chunk j from bit `start` (0 = the file's gzip header) to bit `stop` (NONE = the end of the stream)
     void decode(size_t j, uint64_t start, uint64_t stop) {
+        need(stop == NONE ? n_ : stop / 8 + 2 * chunk_);
         Job& J = jobs_[j];
         GzipDecoder dec(data_, n_, true);
         bool bytes = false;
@@ -331,10 +363,12 @@ class ParallelGunzip {
             J.pieces.clear();
             cur++;
         }
+        if (!stop && !*err && short_.load()) *err = "short read";  // the file shrank while it was read
         if (!stop && !*err && tp != pending.size()) *err = "member without its trailer";
         if (!stop && !*err && pending.empty()) *err = "truncated gzip stream";
         if (!stop && !*err && pending.back().end != delivered) *err = "truncated gzip stream";
-        // drain: drop the queued tasks and let the running ones finish before the jobs go away
+        // drain: drop the queued tasks and let the running ones finish before the jobs go away; stop the loader
+        quit_flag_.store(true, std::memory_order_relaxed);
         {
             std::unique_lock<std::mutex> lk(mu_);
             tasks_.clear();
@@ -348,6 +382,11 @@ class ParallelGunzip {
     unsigned nthreads_;
     std::vector<Job> jobs_;
     std::vector<std::thread> pool_;
+    std::thread loader_;
+    std::mutex load_mu_;
+    std::condition_variable load_cv_;
+    std::atomic<size_t> loaded_{0};
+    std::atomic<bool> short_{false}, quit_flag_{false};
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     std::deque<std::function<void()>> tasks_;

@@ -158,9 +158,12 @@ int dwpa_crack_files(const char *hash_file, const char *const *dicts, size_t ndi
                      int nonce_error_corrections, const char *out_file, const dwpa_config *cfg);
 /* dwpa_crack_files plus one outcome per dictionary (dict_status[ndicts], nullable):
  *   DWPA_DICT_OK       read to its end (or not needed: every line cracked first)
- *   DWPA_DICT_DAMAGED  corrupt or truncated gzip stream: scanned up to the damage, exactly the bytes zlib's gzread
- *                      delivers (hashcat reads wordlists through gzread), and the call still returns 0/1; the file
- *                      should be fetched again (help_crack.py:530-534 only downloads a missing file)
+ *   DWPA_DICT_DAMAGED  corrupt or truncated gzip stream, by zlib's own verdict: scanned up to the damage, and the
+ *                      call still returns 0/1 (hashcat reads wordlists through gzread and does the same).  For a
+ *                      truncated stream the words are exactly those of the bytes gzread delivers; for a corrupt body
+ *                      or CRC they are at least those (the parallel decoder may deliver the bytes before the failing
+ *                      check, and how much gzread drops depends on its buffer and read sizes).  The file should be
+ *                      fetched again (help_crack.py:530-534 only downloads a missing file)
  *   DWPA_E_IO          cannot be opened or read: the call returns DWPA_RC_ERROR (before any device work when the
  *                      file cannot be opened, as hashcat refuses to start) */
 #define DWPA_DICT_OK 0
