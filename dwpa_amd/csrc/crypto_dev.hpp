@@ -488,6 +488,29 @@ __device__ __forceinline__ uint32_t aes4_subword_v1(const uint32_t* te, uint32_t
     const uint32_t lo = __builtin_amdgcn_perm(aes_v1_ld<KC>(te, wc, cw), aes_v1_ld<KD>(te, wd, cw), 0x00000501u);
     return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
 }
+#elif DWPA_KV3_AES == 3
+// A/B variant (round 4): Te0 AND Te1 = rotr(Te0, 8), 16 copies each, in the same 32 KiB and the same 128-byte entry
+// stride as layout 1: entry x of Te0 copy c at word 32 x + c, of Te1 copy c at word 32 x + 16 + c; lane l reads copy
+// l % 16.  Te2 / Te3 are Te0 / Te1 rotated by 16, so a column is Te0[a] ^ Te1[b] ^ rotr(Te0[c] ^ Te1[d], 16): one
+// rotate instead of three.  Lanes l and l + 16 share a copy, so reads are 2-way bank conflicts.
+constexpr uint32_t AES_SLICES = 32;                     // words per entry
+constexpr uint32_t AES_LDS_WORDS = 256 * AES_SLICES;    // 32 KiB
+template <int K>
+__device__ __forceinline__ uint32_t aes_v1_off(uint32_t s, uint32_t cw) {
+    const uint32_t t = K == 3 ? s >> 17 : K == 2 ? s >> 9 : K == 1 ? s >> 1 : s << 7;
+    return __builtin_amdgcn_bitop3_b32(t, 0x7f80u, cw, 0xea);
+}
+template <int K>
+__device__ __forceinline__ uint32_t aes_v1_ld(const uint32_t* te, uint32_t s, uint32_t cw) {
+    return *(const uint32_t*)((const char*)te + aes_v1_off<K>(s, cw));
+}
+template <int KA, int KB, int KC, int KD>
+__device__ __forceinline__ uint32_t aes4_subword_v1(const uint32_t* te, uint32_t cw, uint32_t wa, uint32_t wb,
+                                                    uint32_t wc, uint32_t wd) {
+    const uint32_t hi = __builtin_amdgcn_perm(aes_v1_ld<KA>(te, wa, cw), aes_v1_ld<KB>(te, wb, cw), 0x06020000u);
+    const uint32_t lo = __builtin_amdgcn_perm(aes_v1_ld<KC>(te, wc, cw), aes_v1_ld<KD>(te, wd, cw), 0x00000501u);
+    return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
+}
 #elif DWPA_KV3_AES == 2
 // A/B variant: Te0 AND Te2 = rotr(Te0, 16), 32 copies each, entry x of copy c at byte (x << 8) | (c << 2) (Te2 at
 // +128): one v_perm builds a lookup's whole address from the state byte and the lane's copy offset, and
@@ -521,6 +544,8 @@ __device__ __forceinline__ uint32_t aes4_subword(const uint32_t* te4, uint32_t a
 __device__ __forceinline__ uint32_t aes_lds_word(uint32_t k) {
 #if DWPA_KV3_AES == 1
     return AES_TABLES.te0[k >> 5];
+#elif DWPA_KV3_AES == 3
+    return rotr(AES_TABLES.te0[k >> 5], (k & 16) >> 1);  // words 32x + c: Te0[x]; 32x + 16 + c: Te1[x]
 #elif DWPA_KV3_AES == 2
     return rotr(AES_TABLES.te0[k >> 6], (k & 32) >> 1);  // words 64x + c: Te0[x]; 64x + 32 + c: Te2[x]
 #else
@@ -557,6 +582,37 @@ __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uin
     s[1] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s1, s2, s3, s0) ^ k1;
     s[2] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s2, s3, s0, s1) ^ k2;
     s[3] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s3, s0, s1, s2) ^ k3;
+}
+#elif DWPA_KV3_AES == 3
+__device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uint32_t key[4], uint32_t s[4]) {
+    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
+    const uint32_t c0 = (threadIdx.x & 15u) << 2, c1 = c0 + 64u;  // the lane's Te0 / Te1 copy
+    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
+    uint32_t s0 = s[0] ^ k0, s1 = s[1] ^ k1, s2 = s[2] ^ k2, s3 = s[3] ^ k3;
+#define T0(w, k) aes_v1_ld<k>(te, w, c0)
+#define T1(w, k) aes_v1_ld<k>(te, w, c1)
+#pragma unroll
+    for (int r = 1; r < 10; r++) {
+        k0 ^= aes4_subword_v1<2, 1, 0, 3>(te, c0, k3, k3, k3, k3) ^ (RCON[r - 1] << 24);
+        k1 ^= k0;
+        k2 ^= k1;
+        k3 ^= k2;
+        const uint32_t t0 = xor3(T0(s0, 3), T1(s1, 2), k0) ^ rotr(T0(s2, 1) ^ T1(s3, 0), 16);
+        const uint32_t t1 = xor3(T0(s1, 3), T1(s2, 2), k1) ^ rotr(T0(s3, 1) ^ T1(s0, 0), 16);
+        const uint32_t t2 = xor3(T0(s2, 3), T1(s3, 2), k2) ^ rotr(T0(s0, 1) ^ T1(s1, 0), 16);
+        const uint32_t t3 = xor3(T0(s3, 3), T1(s0, 2), k3) ^ rotr(T0(s1, 1) ^ T1(s2, 0), 16);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+#undef T0
+#undef T1
+    k0 ^= aes4_subword_v1<2, 1, 0, 3>(te, c0, k3, k3, k3, k3) ^ (RCON[9] << 24);
+    k1 ^= k0;
+    k2 ^= k1;
+    k3 ^= k2;
+    s[0] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s0, s1, s2, s3) ^ k0;
+    s[1] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s1, s2, s3, s0) ^ k1;
+    s[2] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s2, s3, s0, s1) ^ k2;
+    s[3] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s3, s0, s1, s2) ^ k3;
 }
 #elif DWPA_KV3_AES == 2
 __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uint32_t key[4], uint32_t s[4]) {

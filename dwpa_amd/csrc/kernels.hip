@@ -418,8 +418,8 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
 template <uint32_t VC>
 __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     if constexpr ((VC & VC_KV3) != 0) {
-#if DWPA_KV3_AES == 1
-        // four copies of one entry per 16-byte store (words 4j..4j+3 all hold Te0[4j >> 5])
+#if DWPA_KV3_AES == 1 || DWPA_KV3_AES == 3
+        // four copies of one entry per 16-byte store (words 4j..4j+3 all hold the same table's entry 4j >> 5)
         for (uint32_t j = threadIdx.x; j < AES_LDS_WORDS / 4; j += blockDim.x) {
             const uint32_t v = aes_lds_word(4 * j);
             reinterpret_cast<uint4*>(te)[j] = make_uint4(v, v, v, v);
