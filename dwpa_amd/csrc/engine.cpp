@@ -204,6 +204,7 @@ struct Device {
     DevBuf lines, atts, pool, segs, segs_tail, salt;
     DevBuf koff, klen, kbytes, uslot;  // check path: the call's key bytes by slot, unique key -> its first slot
     DevBuf keys, keys_tail;        // check path: per-key EapolKey scratch of the attempt-parallel verify
+    DevBuf first_hit;              // check path: per line (= job), the smallest slot with a hit so far (~0u: none)
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
     SlotTable slots;               // check path: the call's slots (capacity kept between calls)
     CheckScratch cs;               // check path: host-phase scratch
@@ -688,6 +689,15 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
     return 0;
 }
 
+// DWPA_FIRST_KEY_EXIT=0 verifies every key of a job even after an earlier key matched (A/B of the early exit).
+static bool first_key_exit_knob() {
+    static const bool on = [] {
+        const char* e = getenv("DWPA_FIRST_KEY_EXIT");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 // d.stream waits for everything queued on d.tail so far.
 static int join_tail(Device& d) {
     HIPCHK(hipEventRecord(d.tail_done, d.tail));
@@ -724,6 +734,23 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
         }
         i = j;
     }
+    // attempt-parallel buckets in rank order: every job's first 64 keys, then every job's next 64, ... .  The check
+    // wants only the first key in input order with a hit (common.php:170-189,238-306), so a wave whose keys all come
+    // after a key already found for its job exits at once (k_verify_att, first_hit); with a job's segments a whole
+    // pass over the other jobs apart, the hit of an early segment is known before its later segments are dispatched.
+    // Segments keep their 64 keys (natt waves each, no partial wave but the job's last).
+    if (first_key_exit_knob())
+        for (int k = 4; k < 8; k++) {
+            std::vector<SegDev>& v = bucket[k];
+            if (v.size() < 2) continue;
+            std::vector<std::pair<uint32_t, uint32_t>> key(v.size());  // (rank within its line, position)
+            std::unordered_map<uint32_t, uint32_t> rank;
+            for (size_t i = 0; i < v.size(); i++) key[i] = {rank[v[i].line]++, (uint32_t)i};
+            std::sort(key.begin(), key.end());
+            std::vector<SegDev> w(v.size());
+            for (size_t i = 0; i < v.size(); i++) w[i] = v[key[i].second];
+            v.swap(w);
+        }
     // attempt-parallel buckets: pad = the segment's first wave in its launch (ceil(count * natt / 64) waves each)
     uint32_t nwaves[8] = {0};
     for (int k = 4; k < 8; k++)
@@ -778,7 +805,8 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
             HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, sg,
                                      nb, nwaves[k], (uint32_t*)keybuf.p + koff[k], (uint32_t)bucket[k].size() * 64,
                                      (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p,
-                                     (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc, vsk));
+                                     (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap,
+                                     first_key_exit_knob() ? (uint32_t*)d.first_hit.p : nullptr, vc, vsk));
     }
     if (fan) {
         HIPCHK(hipEventRecord(d.vs_done, d.side));
@@ -995,6 +1023,10 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     std::vector<uint32_t> job_line(njobs, 0);
     std::vector<HitDev> hits;
     const size_t chunk = default_batch();
+    // first-key early exit of the attempt-parallel verify (queue_verify): one word per line, reset before the first
+    // kernel of the call; the tail stream's kernels wait for this stream's prep event, queued after it
+    RCHK(d.first_hit.ensure(std::max<size_t>(njobs, 1) * 4));
+    HIPCHK(hipMemsetAsync(d.first_hit.p, 0xff, njobs * 4, d.stream));
     for (size_t b = 0; b < nslots; b += chunk) {
         const size_t e = std::min(nslots, b + chunk);
         // the ESSID runs of [b, e) are the groups' slot ranges clipped to it
@@ -1451,6 +1483,7 @@ void dwpa_shutdown(void) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
         for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->keys, &d->keys_tail, &d->salt,
+                          &d->first_hit,
                           &d->koff, &d->klen, &d->kbytes, &d->uslot, &d->upmk, &d->sref, &d->src, &d->cpmk,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();

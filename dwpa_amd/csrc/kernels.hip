@@ -598,10 +598,11 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                     const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool,
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
-                                                    uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
+                                                    uint32_t* __restrict__ hitcnt, uint32_t hitcap,
+                                                    uint32_t* __restrict__ first_hit) {
     check_prio_vc<VC>();
     __shared__ __attribute__((aligned(16))) uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 4];
-    const uint32_t* te = aes_table_lds<VC>(te_lds);
+    const uint32_t* te = aes_table_lds<VC>(te_lds);  // (every wave of the block helps fill the table first)
 #if DWPA_KV3_RK_LDS
     __shared__ uint4 rk_lds[(VC & VC_KV3) ? 10 * vc_block(VC) : 1];
     uint4* rk = rk_lds + threadIdx.x;
@@ -621,6 +622,12 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     const uint32_t segi = lo;
     const SegDev sg = segs[segi];
     const LineDev L = lines[sg.line];
+    // first-key early exit: every key of this wave comes after a key of the same job that already matched
+    if (first_hit) {
+        const uint32_t f = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(first_hit + sg.line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (sg.slot + (gw - sg.pad) * 64 / L.natt > f) return;
+    }
     const uint32_t item = (gw - sg.pad) * 64 + lane;
     const uint32_t k = item / L.natt, a = item - k * L.natt;
     const bool active = k < sg.count;
@@ -646,6 +653,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     uint32_t mic[4];
     eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic, rk);
     const bool found = active && mic_match(L, mic);
+    if (found && first_hit) __hip_atomic_fetch_min(first_hit + sg.line, slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     report_hits(found, lane, cand, sg.line, a, pmk + slot, cap, hits, hitcnt, hitcap);
 }
 
@@ -780,14 +788,14 @@ uint32_t eapol_key_words(uint32_t vc) { return (vc & VC_KV3) ? 16u : 10u; }
 hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
                              uint32_t nsegs, uint32_t nwaves, uint32_t* keys, uint32_t kstride, const LineDev* lines,
                              const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt,
-                             uint32_t hitcap, uint32_t vc, hipStream_t s) {
+                             uint32_t hitcap, uint32_t* first_hit, uint32_t vc, hipStream_t s) {
     if (nsegs == 0 || nwaves == 0) return hipSuccess;
     if (kstride < nsegs * 64) return hipErrorInvalidValue;
 #define DWPA_LAUNCH_VERIFY_ATT(V)                                                                                 \
     hipLaunchKernelGGL(k_eapol_keys<V>, dim3(cdiv((uint64_t)nsegs * 64, 256)), dim3(256), 0, s, pmk, cap, segs,   \
                        nsegs, lines, pool, keys, kstride);                                                         \
     hipLaunchKernelGGL(k_verify_att<V>, dim3(cdiv(nwaves, vc_block(V) / 64)), dim3(vc_block(V)), 0, s, pmk, cap, \
-                       ids, segs, nsegs, nwaves, keys, kstride, lines, pool, atts, hits, hitcnt, hitcap)
+                       ids, segs, nsegs, nwaves, keys, kstride, lines, pool, atts, hits, hitcnt, hitcap, first_hit)
     DWPA_VC_DISPATCH(vc & ~VC_PMKID, DWPA_LAUNCH_VERIFY_ATT)
 #undef DWPA_LAUNCH_VERIFY_ATT
     return hipGetLastError();

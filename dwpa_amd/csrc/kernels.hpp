@@ -34,10 +34,12 @@ hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t co
 // segs[i].pad = first wave of segment i (ceil(count * natt / 64) waves each, nwaves in all); keys = scratch of
 // eapol_key_words(vc) x kstride words, kstride >= 64 * nsegs
 uint32_t eapol_key_words(uint32_t vc);
+// first_hit (nullable): per line, the smallest slot with a hit so far (~0u: none); waves whose keys all come after
+// it exit at once, and hits lower it (the check wants only the first key in input order)
 hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
                              uint32_t nsegs, uint32_t nwaves, uint32_t* keys, uint32_t kstride, const LineDev* lines,
                              const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt,
-                             uint32_t hitcap, uint32_t vc, hipStream_t s);
+                             uint32_t hitcap, uint32_t* first_hit, uint32_t vc, hipStream_t s);
 // many ESSID groups x one batch per launch (cap % 64 == 0): gsalt[c] = {salt word offset, nsalt} of chunk group c,
 // PMK word k of (c, slot) at pmk[k * pstride + c * cap + slot]
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,

@@ -1,15 +1,19 @@
-# round 4, call d: keyver-3 AES layout A/B: 1 = lane-sliced Te0 x32 (default), 3 = Te0 + Te1 x16
-# (one rotate per column instead of three, 2-way bank conflicts).  Per library: kv3 parity tests, C5 with one and two
-# callers, one PMC pass (SQ_INSTS_VALU, LDS bank conflicts) over C5.
+# round 4, call d: C5's post-head phase.
+#   * first-key early exit of the attempt-parallel verify (DWPA_FIRST_KEY_EXIT, default on) against off;
+#   * keyver-3 AES layout: 1 = lane-sliced Te0 x32 (default), 3 = Te0 + Te1 x16 (one rotate per column instead of
+#     three, 2-way bank conflicts).
+# Per library: check-path parity tests, C5 with one and two callers, one PMC pass (SQ_INSTS_VALU, LDS bank
+# conflicts) over C5.
 cd $GRAFT_REPO_ROOT
 O=${O:-gpurun_out/r04d}
 mkdir -p $O
 export TMPDIR=/tmp
 guard() { case $1 in 0) ;; 124|134|137|139) echo "stop: rc $1" >&2; exit $1;; *) echo "fail: rc $1" >&2; exit 1;; esac; }
-for lib in aes3 aes1; do
-  L=$PWD/ab/$lib.so
+for lib in aes1 aes1_noexit aes3; do
+  L=$PWD/ab/${lib%_noexit}.so
+  if [ "$lib" = aes1_noexit ]; then export DWPA_FIRST_KEY_EXIT=0; else export DWPA_FIRST_KEY_EXIT=1; fi
   DWPA_LIB=$L timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py \
-      -k "golden or c5 or random_batch or nc_windows" -x -q --timeout 200 --timeout-method thread > $O/pytest_$lib.txt 2>&1
+      -k "golden or c5 or random_batch or nc_windows or batch" -x -q --timeout 200 --timeout-method thread > $O/pytest_$lib.txt 2>&1
   rc=$?; echo "$lib pytest rc=$rc $(tail -1 $O/pytest_$lib.txt)"; guard $rc
   for k in 1 2; do
     DWPA_LIB=$L timeout -k 10 150 python3 bench.py --workload c5 --callers $k --steps 20 --warmup 3 --no-cpu-baseline \
