@@ -207,3 +207,19 @@ function check_keys_m22000_gpu_batch($jobs)
     }
     return $res;
 }
+
+/* Routing by call shape (INTEGRATION.md §2, round-4 latencies in profiles/r04/c1lat.json): a one-key check and a
+ * caller-PMK check of a PMKID line stay in PHP (one PBKDF2 on one core, 1.1 ms, against 8.5 ms for the GPU's single
+ * PBKDF2 chain; one HMAC, 4 us, against a GPU call's ~0.08 ms); a check of several keys and a caller-PMK check of an
+ * EAPOL line (up to 521 PRF + MIC attempts, 2-12x faster on the GPU) go to the library.  Needs
+ * check_key_m22000_php, the reference's function renamed; without it everything goes to the library. */
+function check_key_m22000_routed($hashline, $keys, $pmk = False, $nc = 128)
+{
+    if (function_exists('check_key_m22000_php')) {
+        $pmkid = strncmp($hashline, 'WPA*01*', 7) === 0;
+        if ($pmk ? $pmkid : count($keys) < 2) {
+            return check_key_m22000_php($hashline, $keys, $pmk, $nc);
+        }
+    }
+    return check_key_m22000_gpu($hashline, $keys, $pmk, $nc);
+}

@@ -105,3 +105,14 @@ def test_pmk_is_never_padded_or_truncated():
     assert "str_pad" not in pmk and "substr" not in pmk
     ok = _function(src, "pmk_ok")
     assert "return !$pmk || strlen((string) $pmk) == 32;" in ok
+
+
+def test_routed_check_follows_the_latency_table():
+    """check_key_m22000_routed (profiles/r04/c1lat.json): one-key checks and PMKID caller-PMK
+    checks go to the PHP function when it exists; everything else to the library."""
+    src = _src()
+    body = src[src.index("function check_key_m22000_routed"):]
+    assert "function_exists('check_key_m22000_php')" in body
+    assert "strncmp($hashline, 'WPA*01*', 7) === 0" in body
+    assert "$pmk ? $pmkid : count($keys) < 2" in body
+    assert body.index("return check_key_m22000_php(") < body.index("return check_key_m22000_gpu(")
