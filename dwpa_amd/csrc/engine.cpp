@@ -698,6 +698,16 @@ static bool first_key_exit_knob() {
     return on;
 }
 
+// Keys per attempt-parallel segment (DWPA_ATT_SEG_KEYS, 1..64, default 16) when the first-key early exit is on.
+static uint32_t att_seg_keys() {
+    static const uint32_t k = [] {
+        const char* e = getenv("DWPA_ATT_SEG_KEYS");
+        const int v = e ? atoi(e) : 16;
+        return (uint32_t)std::min(64, std::max(1, v));
+    }();
+    return k;
+}
+
 // d.stream waits for everything queued on d.tail so far.
 static int join_tail(Device& d) {
     HIPCHK(hipEventRecord(d.tail_done, d.tail));
@@ -719,13 +729,17 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
     // runs while the PBKDF2 tail holds some SIMDs ends only with the tail, so fewer launches in a row end sooner.
     std::vector<SegDev> bucket[8];
     auto bucket_vc = [](int k) { return k == 5 ? (uint32_t)(VC_KV1 | VC_KV2) : 1u << (k & 3); };
+    const uint32_t att_seg = first_key_exit_knob() ? att_seg_keys() : 64;
     for (uint32_t i = 0; i < n;) {
         uint32_t j = i;
         const uint32_t job = T.job[b + i];
-        while (j < n && T.job[b + j] == job && j - i < 64) j++;
         const uint32_t li = job_line[job];
         const LineDev& L = tb.lines[li];
         const bool att = L.kind == LINE_EAPOL && L.natt >= ATT_PARALLEL_MIN;
+        // attempt-parallel segments are cut shorter: the early exit below skips whole segments dispatched after a
+        // job's hit, so the finer the cut, the fewer keys past the hit are verified
+        const uint32_t segmax = att ? att_seg : 64;
+        while (j < n && T.job[b + j] == job && j - i < segmax) j++;
         // the key-parallel kernel reads every attempt's KW blocks (built for lines under ATT_PARALLEL_MIN)
         if (L.kind == LINE_EAPOL && !att && tb.atts[L.list_off].kw_off == NO_KW) return DWPA_E_ARG;
         if (!tb.never[li]) {
@@ -738,7 +752,8 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
     // wants only the first key in input order with a hit (common.php:170-189,238-306), so a wave whose keys all come
     // after a key already found for its job exits at once (k_verify_att, first_hit); with a job's segments a whole
     // pass over the other jobs apart, the hit of an early segment is known before its later segments are dispatched.
-    // Segments keep their 64 keys (natt waves each, no partial wave but the job's last).
+    // A segment of S keys spans S * natt / 64 waves (at nc = 128, 261 attempts: 65.25 waves for S = 16, one partial
+    // wave per segment).
     if (first_key_exit_knob())
         for (int k = 4; k < 8; k++) {
             std::vector<SegDev>& v = bucket[k];
