@@ -60,3 +60,22 @@ def invalid_rules():
 
 def all_rules():
     return single_function_rules() + memory_rules() + combo_rules()
+
+
+def fuzz_rules(n: int = 3000, seed: int = 17):
+    """Random rule strings over the rule alphabet: function letters, position characters, arbitrary argument bytes
+    and spaces, 1-12 characters -- valid and invalid lines alike (seeded)."""
+    rng = random.Random(seed)
+    ops = ":lucCtrdf{}[]kKqEM46QTpDzZ'yYLR+-.,<>_$^@e!/()io=%3sxO*X"
+    args = "0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZabcz-$ @\x80\xff"
+    out = []
+    for _ in range(n):
+        m = rng.randint(1, 12)
+        out.append("".join(rng.choice(ops) if rng.random() < 0.45 else rng.choice(args) for _ in range(m)))
+    return [r for r in out if not r.startswith("#") and r.strip("\r\n")]
+
+
+def fuzz_words(seed: int = 19):
+    rng = random.Random(seed)
+    return [bytes(rng.randrange(256) if rng.random() < 0.1 else rng.choice(b"abcdEFGH0123-$ @z") for _ in
+                  range(rng.choice([1, 2, 3, 5, 8, 12, 35, 36, 63, 100, 255, 256]))) for _ in range(12)]

@@ -218,6 +218,20 @@ def test_rules_language_gpu_vs_oracle(group):
     assert not bad, bad[:8]
 
 
+def test_rules_fuzz_gpu_vs_oracle():
+    """Random rule strings over the whole alphabet (tests/rule_corpus.py fuzz_rules): the GPU expands exactly the
+    rules the oracle parses, in order, and every candidate equals the oracle's."""
+    from tests import rule_corpus as C
+    rules = C.fuzz_rules()
+    words = C.fuzz_words()
+    parsed = [r for r in rules if R.parse(r) is not None]
+    got = dwpa_amd.rules_expand("\n".join(rules).encode("latin-1"), words)
+    exp = R.expand(parsed, words)
+    assert len(got[0]) == len(parsed)
+    bad = [(parsed[j], w[:12], len(w)) for i, w in enumerate(words) for j in range(len(parsed)) if got[i][j] != exp[i][j]]
+    assert not bad, bad[:8]
+
+
 def test_crack_files_every_rule_family(tmp_path):
     """A work unit whose server rule file (-S -r, help_crack.py:931-933) uses every family of the language beyond
     bestWPA.rule's ops -- insert/overwrite/extract/omit, swaps and byte arithmetic, block duplication, title case and

@@ -82,3 +82,24 @@ def test_documented_examples():
     for rule, w, exp in ex:
         assert R.apply(R.parse(rule), w) == exp, rule
         assert dwpa_amd.m22000.rules_apply_host(rule.encode(), 0, w) == exp, rule
+
+
+def test_fuzz_parse_and_apply_vs_oracle():
+    """Random rule strings (valid and invalid) over the whole alphabet: the library parses exactly the lines the
+    oracle parses, and the host interpreter equals the oracle on every parsed one."""
+    rules = C.fuzz_rules()
+    words = C.fuzz_words()
+    lib_parsed = [dwpa_amd.rules_count(r.encode("latin-1"))[1] == 1 for r in rules]
+    orc_parsed = [R.parse(r) is not None for r in rules]
+    assert lib_parsed == orc_parsed, [r for r, a, b in zip(rules, lib_parsed, orc_parsed) if a != b][:10]
+    assert 0.05 < sum(orc_parsed) / len(rules) < 0.95  # both kinds are exercised
+    bad = []
+    for r, ok in zip(rules, orc_parsed):
+        if not ok:
+            continue
+        ops = R.parse(r)
+        for w in words:
+            got = dwpa_amd.m22000.rules_apply_host(r.encode("latin-1"), 0, w)
+            if got != R.apply(ops, w):
+                bad.append((r, w[:12], len(w)))
+    assert not bad, bad[:10]
