@@ -20,9 +20,10 @@ Rules (comma-separated, applied in the loop body only):
   nop1            use s_nop 1 instead of s_nop 0
   split_add3      rewrite every v_add3_u32 as two v_add_u32_e32 (same adds, mod 2^32; 4-cycle op -> two 2-cycle
                   ops), applied before the nop rules (A/B: fewer half-rate ops in the stream)
-  sched=D[:alt]   list-schedule the loop body again (VGPR/SGPR/SCC dependences kept, registers unchanged) so that an
-                  instruction issues at least D VALU slots after the producers of its operands where the dependences
-                  allow; `alt` also prefers alternating 2-/4-cycle ops.  Applied before the nop rules (A/B)
+  sched=D[:alt|:group]  list-schedule the loop body again (VGPR/SGPR/SCC dependences kept, registers unchanged) so
+                  that an instruction issues at least D VALU slots after the producers of its operands where the
+                  dependences allow; `alt` also prefers alternating 2-/4-cycle ops, `group` runs of one rate (fewer
+                  2 <-> 4-cycle transitions, for lone waves).  Applied before the nop rules (A/B)
   none            copy through
 """
 import re
@@ -101,7 +102,7 @@ def _defs_uses(line):
     raise ValueError(f"unexpected instruction in the loop body: {line!r}")
 
 
-def reschedule(body, dmin, alt):
+def reschedule(body, dmin, alt, group=False):
     """Greedy list schedule of a straight-line loop body (see the sched rule)."""
     ins = []
     for l in body:
@@ -147,7 +148,8 @@ def reschedule(body, dmin, alt):
         def key(i):
             dist = min((len(order) - pos[j] for j in raw[i]), default=dmin)
             half = ins[i][1].replace("_e32", "").replace("_e64", "") in HALF
-            return (min(dist, dmin), alt and prev_half is not None and half != prev_half, cp[i], -i)
+            return (min(dist, dmin), alt and prev_half is not None and half != prev_half,
+                    group and prev_half is not None and half == prev_half, cp[i], -i)
         i = max(ready, key=key)
         ready.discard(i)
         pos[i] = len(order)
@@ -167,7 +169,7 @@ def nopify(lines, kernel, rules):
     for r in rules:
         if r.startswith("sched="):
             arg = r.split("=", 1)[1].split(":")
-            body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:])
+            body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:], "group" in arg[1:])
             lines = lines[:h + 1] + body + lines[e:]
             e = h + 1 + len(body)
     if "split_add3" in rules:
