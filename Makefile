@@ -58,7 +58,7 @@ clean:
 .PHONY: all oracle clean asm
 
 tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
-       tools/bin/inflate_check tools/bin/item_queue_check
+       tools/bin/inflate_check tools/bin/item_queue_check tools/bin/rules_fuzz_asan tools/bin/clock_idle
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -91,3 +91,13 @@ tools/bin/item_queue_check: tools/item_queue_check.cpp $(SRC)/dict_reader.hpp $(
                             $(SRC)/m22000_host.cpp $(SRC)/m22000_host.hpp
 	@mkdir -p tools/bin
 	g++ -O2 -std=c++17 -Wall -Iinclude -I$(SRC) -o $@ tools/item_queue_check.cpp $(SRC)/m22000_host.cpp -lz -lpthread
+
+# host fuzz of the rule engine under AddressSanitizer + UBSan (host code only: -fsanitize after -Xarch_host)
+tools/bin/rules_fuzz_asan: tools/rules_fuzz.cpp $(SRC)/rules.cpp $(SRC)/rules.hpp $(SRC)/rules_apply.hpp
+	@mkdir -p tools/bin
+	$(HIPCC) -O1 -g -std=c++17 -Iinclude -I$(SRC) -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+	    -o $@ tools/rules_fuzz.cpp $(SRC)/rules.cpp
+
+tools/bin/clock_idle: tools/clock_idle.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<

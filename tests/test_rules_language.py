@@ -103,3 +103,20 @@ def test_fuzz_parse_and_apply_vs_oracle():
             if got != R.apply(ops, w):
                 bad.append((r, w[:12], len(w)))
     assert not bad, bad[:10]
+
+
+def test_interpreter_under_address_sanitizer():
+    """tools/bin/rules_fuzz_asan (make tools): random rule lines (well-formed with out-of-range arguments, and
+    garbage) applied to words of 0..300 bytes by the interpreter the GPU runs, compiled for the host with
+    AddressSanitizer + UBSan, with the GPU's exact 256 + 4-byte buffers: no out-of-bounds access, no candidate
+    longer than 256 bytes."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "bin", "rules_fuzz_asan")
+    if not os.path.exists(exe):
+        pytest.skip("tools/bin/rules_fuzz_asan not built (make tools)")
+    r = subprocess.run([exe, "40000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+    st = json.loads(r.stdout.strip().splitlines()[-1])
+    assert st["rules_parsed"] > 20000 and st["candidates"] > 20000 and st["rejected"] > 20000
