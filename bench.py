@@ -143,13 +143,14 @@ def parse():
                          "SIMDs, so the verify runs starved beside it -- and blurs the per-kernel events; default 1")
     ap.add_argument("--rule-words", type=int, default=1_000_000,
                     help="c3files: base words of the gz dictionary the WPA rule set is applied to")
-    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files", "c3files", "c1lat"], default="c2",
+    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files", "c3files", "c1lat", "expand"],
+                    default="c2",
                     help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs; "
                          "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
                          "dwpa_crack_files from a gz dictionary on disk (the help_crack client path); c3files = "
                          "the client's rule pass: a gz dictionary x the WPA rule set through dwpa_crack_files; "
-                         "c1lat = "
-                         "server call latency at 1/16/202 keys per call beside one CPU core")
+                         "c1lat = server call latency at 1/16/202 keys per call beside one CPU core; expand = "
+                         "help_crack's `hashcat --stdout -r` wordlist expansion (dwpa_rules_expand_file)")
     ap.add_argument("--rules-set", choices=["wpa", "server"], default="wpa",
                     help="c3files: the rules file -- wpa (148 rules of bestWPA.rule's ops) or server (those plus 67 "
                          "lines of the rest of hashcat's rule language: title case, inserts, memory, reject ...)")
@@ -478,6 +479,8 @@ def main():
         return main_files_rules(args, world, rank, local)
     if args.workload == "c1lat":
         return main_latency(args, world, rank, local)
+    if args.workload == "expand":
+        return main_expand(args, world, rank, local)
     if args.scaling == "strong":
         return main_strong(args, world, rank, local)
     if world > 1:
@@ -1173,6 +1176,68 @@ def main_files_rules(args, world, rank, local):
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0 and not cracked:
+        sys.exit(3)
+
+
+def main_expand(args, world, rank, local):
+    """help_crack's wordlist expansion `hashcat --stdout -r bestWPA.rule source.txt -o cracked.txt.gz`
+    (help_crack.py:508, every 100th run over the site's cracked.txt + rkg.txt; :575 for prdict) through
+    dwpa_rules_expand_file: --rule-words synthetic words (6..16 printable bytes) x the WPA rule set (148 rules),
+    plain-text output like hashcat's.  A step = one expansion of the whole source; value = candidates written per
+    second (the output rate; a candidate is not a PMK here).  The count is checked against the rule set's
+    per-length counts and the first candidates against the library's in-memory expansion."""
+    import tempfile
+    import numpy as np
+    import dwpa_amd
+    from dwpa_amd.rulesets import wpa_rules
+    n = max(2000, args.rule_words)
+    rules = wpa_rules()
+    rules_text = "\n".join(rules)
+    rng = np.random.default_rng(9)
+    lens = rng.integers(6, 17, n).astype(np.int64)
+    ends = np.cumsum(lens + 1)
+    text = rng.integers(0x21, 0x7F, int(ends[-1]), dtype=np.uint8)
+    text[text == ord("$")] = ord("%")
+    text[ends - 1] = 0x0A
+    reps = [bytes(b"abcdefghijklmnop"[:L]) for L in range(6, 17)]
+    per_len = {L: sum(1 for c in r if c is not None)
+               for L, r in zip(range(6, 17), dwpa_amd.rules_expand(rules_text, reps, device=local))}
+    expected = int(sum(int(c) * per_len[L] for L, c in enumerate(np.bincount(lens, minlength=17)) if L >= 6))
+    tmp = tempfile.mkdtemp(prefix="dwpa_expand_")
+    spath, rpath, opath = (os.path.join(tmp, x) for x in ("source.txt", "bestWPA.rule", "cracked.txt.gz"))
+    with open(spath, "wb") as f:
+        f.write(text.tobytes())
+    with open(rpath, "w") as f:
+        f.write(rules_text + "\n")
+    first = [text[int(ends[i - 1]) if i else 0:int(ends[i]) - 1].tobytes() for i in range(8)]
+    del text
+    times, ok = [], True
+    for rep in range(args.warmup + args.steps):
+        t0 = time.perf_counter()
+        words, cands = dwpa_amd.m22000.rules_expand_file(rpath, [spath], opath, 0, local)
+        el = time.perf_counter() - t0
+        if rep >= args.warmup:
+            times.append(el)
+        ok &= words == n and cands == expected
+    out_bytes = os.path.getsize(opath)
+    with open(opath, "rb") as f:
+        head = f.read(1 << 16).split(b"\n")
+    exp_head = [c for row in dwpa_amd.rules_expand(rules_text, first, device=local) for c in row if c is not None]
+    ok &= head[:len(exp_head)] == exp_head
+    for x in (spath, rpath, opath):
+        os.remove(x)
+    os.rmdir(tmp)
+    el = sum(times) / len(times)
+    if rank == 0:
+        emit({"metric": "candidates/s written, hashcat --stdout -r replacement (wordlist expansion)",
+              "value": round(expected / el, 1), "unit": "candidates/s", "n_gpus": world, "steps": args.steps,
+              "warmup": args.warmup, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+              "config": {"workload": f"expandcracked: {n}-word source x {len(rules)} WPA rules -> plain-text wordlist "
+                                     "(dwpa_rules_expand_file)", "rule_words": n, "rules": len(rules),
+                         "candidates": expected, "output_bytes": out_bytes, "parallelism": f"replicas x{world}"},
+              "roofline": None, "cpu_baseline": None, "hits_verified": bool(ok)})
+    if rank == 0 and not ok:
         sys.exit(3)
 
 

@@ -87,6 +87,9 @@ SIGNATURES = {
                             ctypes.c_int),
     "dwpa_rules_expand": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(Bytes), ctypes.c_size_t, _P, _P,
                            ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "dwpa_rules_expand_file": ([ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t,
+                                ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "dwpa_rules_count": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "dwpa_rules_apply_host": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, _P,

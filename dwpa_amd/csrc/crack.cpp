@@ -427,9 +427,170 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     return sh.ncracked == sh.valid ? DWPA_RC_CRACKED : DWPA_RC_EXHAUSTED;
 }
 
+// One candidate as hashcat's --stdout writes it: $HEX[..] when a byte is outside 0x20..0x7e or the candidate itself
+// starts with "$HEX[" (a ':' needs no escaping here: there is no separator), else as it is.
+static void stdout_plain(const uint8_t* p, size_t n, std::string& out) {
+    bool hex = n >= 5 && memcmp(p, "$HEX[", 5) == 0;
+    for (size_t i = 0; i < n && !hex; i++) hex = p[i] < 0x20 || p[i] > 0x7e;
+    if (!hex) {
+        out.append((const char*)p, n);
+    } else {
+        static const char* H = "0123456789abcdef";
+        out.append("$HEX[");
+        for (size_t i = 0; i < n; i++) {
+            out.push_back(H[p[i] >> 4]);
+            out.push_back(H[p[i] & 15]);
+        }
+        out.push_back(']');
+    }
+    out.push_back('\n');
+}
+
+// `hashcat --stdout -r rules_file sources... -o out_path` (help_crack.py:508 expandcracked, :575 prdict): the words
+// of the sources (plain or gzip, one per line, $HEX[] decoded, as hashcat reads wordlists) x every rule, expanded on
+// the GPU in sub-batches of ~1M candidates (256-byte slots, k_rules_expand), packed on the host in word-major order,
+// rejected candidates skipped, written as hashcat writes plains.  The device part of each sub-batch overlaps the
+// host's packing and writing of the previous one (two slot sets, two streams).
+static int rules_expand_file_impl(int device, const char* rules_file, const char* const* sources, size_t nsources,
+                                  const char* out_path, int gzip_level, uint64_t* words_out, uint64_t* cands_out) {
+    if (!rules_file || !out_path || (!sources && nsources)) return DWPA_E_ARG;
+    for (size_t i = 0; i < nsources; i++) {
+        FILE* f = sources[i] ? fopen(sources[i], "rb") : nullptr;
+        if (!f) return DWPA_E_IO;
+        fclose(f);
+    }
+    RuleSet rs;
+    int rc = rs.load_file(rules_file);
+    if (rc < 0) return rc;
+    if ((rc = engine_init()) < 0) return rc;
+    if (hipSetDevice(device) != hipSuccess) return DWPA_E_NODEV;
+    FILE* fo = nullptr;
+    gzFile gz = nullptr;
+    if (gzip_level > 0) {
+        char mode[8];
+        snprintf(mode, sizeof mode, "wb%d", std::min(9, gzip_level));
+        gz = gzopen(out_path, mode);
+        if (!gz) return DWPA_E_IO;
+        gzbuffer(gz, 1 << 20);
+    } else if (!(fo = fopen(out_path, "wb"))) {
+        return DWPA_E_IO;
+    }
+    DevRules dr;
+    rc = rules_upload(device, rs, &dr);
+    const size_t nr = rs.size();
+    const size_t wpb = std::max<size_t>(1, (1u << 20) / nr);  // words per sub-batch: ~1M candidate slots
+    const size_t ncap = wpb * nr;
+    struct Set {
+        DevBuf off, bytes, out, len;
+        uint8_t* h_out = nullptr;
+        uint32_t* h_len = nullptr;
+        hipStream_t s = nullptr;
+        hipEvent_t done = nullptr, up = nullptr;  // expansion copied back / inputs uploaded
+        std::vector<uint64_t> hoff;
+        size_t words = 0, base = 0;  // words of the sub-batch, first word's index in the chunk
+        bool busy = false;
+    } set[2];
+    for (Set& S : set) {
+        if (rc < 0) break;
+        if (S.out.ensure(ncap * 256) || S.len.ensure(ncap * 4) || S.off.ensure((wpb + 1) * 8) ||
+            hipHostMalloc((void**)&S.h_out, ncap * 256) != hipSuccess ||
+            hipHostMalloc((void**)&S.h_len, ncap * 4) != hipSuccess)
+            rc = DWPA_E_NOMEM;
+        else if (hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&S.up, hipEventDisableTiming) != hipSuccess)
+            rc = DWPA_E_HIP;
+    }
+    uint64_t words = 0, cands = 0;
+    std::string text;
+    auto drain = [&](Set& S) -> int {  // wait for S's expansion, pack and write it
+        if (!S.busy) return 0;
+        S.busy = false;
+        if (hipEventSynchronize(S.done) != hipSuccess) return DWPA_E_HIP;
+        text.clear();
+        for (size_t c = 0; c < S.words * nr; c++) {
+            const uint32_t n = S.h_len[c];
+            if (n == 0xFFFFFFFFu) continue;  // rejected (input word, or a reject / memory function)
+            stdout_plain(S.h_out + c * 256, n, text);
+            cands++;
+        }
+        const size_t put = gz ? (size_t)gzwrite(gz, text.data(), (unsigned)text.size())
+                              : fwrite(text.data(), 1, text.size(), fo);
+        return put == text.size() ? 0 : DWPA_E_IO;
+    };
+    if (rc >= 0) {
+        std::vector<std::string> paths(sources, sources + nsources);
+        DictReader reader(paths);
+        Chunk c;
+        bool err = false;
+        int cur = 0;
+        auto uploads_done = [&]() {  // the chunk's bytes may change only when no upload still reads them
+            for (Set& S : set)
+                if (S.busy && hipEventSynchronize(S.up) != hipSuccess) return false;
+            return true;
+        };
+        while (rc >= 0 && uploads_done() && reader.next(c, 16 * wpb, 64u << 20, err)) {
+            for (size_t b = 0; b < c.words() && rc >= 0; b += wpb) {
+                Set& S = set[cur];
+                if ((rc = drain(S)) < 0) break;  // its previous sub-batch, two sub-batches ago
+                const size_t e = std::min(c.words(), b + wpb);
+                S.words = e - b;
+                S.hoff.resize(S.words + 1);
+                for (size_t i = b; i <= e; i++) S.hoff[i - b] = c.off[i] - c.off[b];
+                const size_t nbytes = c.off[e] - c.off[b];
+                if (S.bytes.n < nbytes + 16 && S.bytes.ensure(nbytes + 16 + (nbytes >> 1))) { rc = DWPA_E_NOMEM; break; }
+                if (hipMemcpyAsync(S.off.p, S.hoff.data(), S.hoff.size() * 8, hipMemcpyHostToDevice, S.s) != hipSuccess ||
+                    (nbytes && hipMemcpyAsync(S.bytes.p, c.bytes.data() + c.off[b], nbytes, hipMemcpyHostToDevice,
+                                              S.s) != hipSuccess) ||
+                    hipEventRecord(S.up, S.s) != hipSuccess ||
+                    launch_rules_expand((const uint64_t*)S.off.p, (const uint8_t*)S.bytes.p, (uint32_t)S.words,
+                                        (const uint32_t*)dr.offs, (const uint32_t*)dr.code, (uint32_t)nr,
+                                        (uint8_t*)S.out.p, (uint32_t*)S.len.p, S.s) != hipSuccess ||
+                    hipMemcpyAsync(S.h_len, S.len.p, S.words * nr * 4, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+                    hipMemcpyAsync(S.h_out, S.out.p, S.words * nr * 256, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+                    hipEventRecord(S.done, S.s) != hipSuccess) {
+                    rc = DWPA_E_HIP;
+                    break;
+                }
+                S.busy = true;  // S.hoff is rewritten only after drain(S); the chunk only after uploads_done()
+                words += S.words;
+                cur ^= 1;
+                if ((rc = drain(set[cur])) < 0) break;
+            }
+        }
+        if (err && rc >= 0) rc = DWPA_E_IO;
+        for (Set& S : set)
+            if (rc >= 0) rc = drain(S);
+    }
+    for (Set& S : set) {
+        if (S.s) (void)hipStreamSynchronize(S.s);
+        S.off.release();
+        S.bytes.release();
+        S.out.release();
+        S.len.release();
+        if (S.h_out) (void)hipHostFree(S.h_out);
+        if (S.h_len) (void)hipHostFree(S.h_len);
+        if (S.done) (void)hipEventDestroy(S.done);
+        if (S.up) (void)hipEventDestroy(S.up);
+        if (S.s) (void)hipStreamDestroy(S.s);
+    }
+    rules_release(&dr);
+    if (gz && gzclose(gz) != Z_OK && rc >= 0) rc = DWPA_E_IO;
+    if (fo && fclose(fo) != 0 && rc >= 0) rc = DWPA_E_IO;
+    if (words_out) *words_out = words;
+    if (cands_out) *cands_out = cands;
+    return rc < 0 ? rc : 0;
+}
+
 }  // namespace dwpa
 
 extern "C" {
+
+int dwpa_rules_expand_file(int device, const char* rules_file, const char* const* sources, size_t nsources,
+                           const char* out_path, int gzip_level, uint64_t* words_out, uint64_t* cands_out) {
+    return dwpa::rules_expand_file_impl(device, rules_file, sources, nsources, out_path, gzip_level, words_out,
+                                        cands_out);
+}
 
 int dwpa_crack_files(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,
                      int nonce_error_corrections, const char* out_file, const dwpa_config* cfg) {

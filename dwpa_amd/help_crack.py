@@ -156,38 +156,13 @@ def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR
         sleepy()
 
 
-def expand_rules(rules_file: str, source: str, out_gz: str, chunk: int = 1 << 16) -> int:
-    """`hashcat --stdout -r rules_file source > out_gz` (help_crack.py:508) with the rules applied on the GPU.
-    Rejected words are skipped like hashcat does; returns the number of candidates written."""
-    with open(rules_file, "rb") as f:
-        rules_text = f.read()
-    present, parsed, _ = M.rules_count(rules_text)
-    if parsed < present:  # hashcat: "Skipping invalid or unsupported rule in file ... on line ...: ..."
-        for no, line in enumerate(rules_text.split(b"\n"), 1):
-            line = line.rstrip(b"\r")
-            if line and not line.startswith(b"#") and M.rules_count(line)[1] == 0:
-                print(f"Skipping invalid or unsupported rule in file {rules_file} on line {no}: "
-                      f"{line.decode('latin-1')}", file=sys.stderr)
-    if parsed == 0:
-        raise L.DwpaError(L.DWPA_E_RULE, f"{rules_file}: no valid rules left")  # hashcat refuses to start
-    written = 0
-    opener = gzip.open if source.endswith(".gz") else open
-    with opener(source, "rb") as src, gzip.open(out_gz, "wb") as dst:
-        batch = []
-
-        def flush():
-            nonlocal written
-            for row in M.rules_expand(rules_text, batch):
-                for cand in row:
-                    if cand is not None:
-                        dst.write(cand + b"\n")
-                        written += 1
-            batch.clear()
-
-        for line in src:
-            batch.append(line.rstrip(b"\r\n"))
-            if len(batch) >= chunk:
-                flush()
-        if batch:
-            flush()
-    return written
+def expand_rules(rules_file: str, source: str, out_path: str, gzip_level: int = 0, device: int = 0) -> int:
+    """`hashcat --stdout -r rules_file source -o out_path` (help_crack.py:508 expandcracked, :575 prdict) with the
+    rules applied on the GPU and the candidates packed and written by the library (dwpa_rules_expand_file): one per
+    line, word-major, rejected candidates skipped, $HEX[] for non-printable ones.  Like hashcat, the output is plain
+    text whatever its name (help_crack names it cracked.txt.gz; the dictionary readers take plain and gzip alike);
+    gzip_level 1..9 compresses it.  Rule lines that do not parse are reported by the library on stderr ("skipping
+    invalid or unsupported rule in <file> on line <n>"), and a file without a valid rule raises, as hashcat refuses
+    to start.  Returns the number of candidates written."""
+    _, cands = M.rules_expand_file(rules_file, [source], out_path, gzip_level, device)
+    return cands

@@ -171,6 +171,16 @@ def rules_apply_host(rules_text, rule_index: int, word):
     return None if n.value == 0xFFFFFFFF else out.raw[:n.value]
 
 
+def rules_expand_file(rules_file, sources, out_path, gzip_level: int = 0, device: int = 0):
+    """`hashcat --stdout -r rules_file sources -o out_path` on the GPU: returns (words read, candidates written)."""
+    src = [_b(x) for x in sources]
+    arr = (ctypes.c_char_p * max(1, len(src)))(*src)
+    w, c = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    L.check(L.load().dwpa_rules_expand_file(device, _b(rules_file), arr, len(src), _b(out_path), int(gzip_level),
+                                            ctypes.byref(w), ctypes.byref(c)), "rules_expand_file")
+    return w.value, c.value
+
+
 def rules_expand(rules_text, words, device: int = 0):
     """GPU rule application (hashcat --stdout -r): returns [[candidate or None (rejected)] per rule] per word."""
     rt = _b(rules_text)

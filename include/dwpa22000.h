@@ -195,6 +195,14 @@ int dwpa_crack_last_stats(dwpa_crack_stats *out);
  * Rule lines that do not parse are skipped with a stderr message each (out != NULL). */
 int dwpa_rules_expand(int device, const char *rules_text, size_t rules_len, const dwpa_bytes *words, size_t nwords,
                       uint8_t *out, uint32_t *out_len, uint32_t *nrules_out);
+/* `hashcat --stdout -r rules_file sources... -o out_path` (help_crack.py:508 expandcracked, :575 prdict): every word of
+ * the sources (plain or gzip, one per line, $HEX[] decoded) x every rule of rules_file, expanded on `device`, written
+ * to out_path one candidate per line in word-major order, rejected candidates skipped, as hashcat writes plains
+ * ($HEX[..] when a byte is outside 0x20..0x7e); gzip_level 0 = plain text (what hashcat writes), 1..9 = gzip.
+ * Counts the words read and the candidates written.  Returns 0 or a negative code (DWPA_E_IO: a source cannot be
+ * opened or the output cannot be written; DWPA_E_RULE: no valid rule). */
+int dwpa_rules_expand_file(int device, const char *rules_file, const char *const *sources, size_t nsources,
+                           const char *out_path, int gzip_level, uint64_t *words_out, uint64_t *cands_out);
 /* Host only: rule `rule_index` (0-based among the rules that parse) applied to one word by the same interpreter the
  * GPU runs, compiled for the host; *out_len = 0xFFFFFFFF when rejected.  out holds 256 bytes. */
 int dwpa_rules_apply_host(const char *rules_text, size_t rules_len, uint32_t rule_index, const uint8_t *word,

@@ -505,23 +505,40 @@ def test_help_crack_truncated_dictionary_no_livelock(tmp_path):
     assert open(conf["key_file"], "rb").read().count(b"\n") == 1
 
 
-def test_help_crack_expand_rules_file(tmp_path):
-    """`hashcat --stdout -r bestWPA.rule source.txt` (help_crack.py:508) via the GPU rule engine: the gz output
-    equals the rule oracle's expansion with rejected candidates skipped (parity with hashcat itself unpinned)."""
+def _stdout_plain(c: bytes) -> bytes:
+    """hashcat's --stdout form of a candidate: $HEX[..] for bytes outside 0x20..0x7e or a literal $HEX[ prefix."""
+    if c.startswith(b"$HEX[") or any(b < 0x20 or b > 0x7E for b in c):
+        return b"$HEX[" + c.hex().encode() + b"]"
+    return c
+
+
+@pytest.mark.parametrize("gzip_level", [0, 1])
+def test_help_crack_expand_rules_file(tmp_path, gzip_level):
+    """`hashcat --stdout -r bestWPA.rule source.txt -o cracked.txt.gz` (help_crack.py:508) via the GPU rule engine
+    and the library's packing (dwpa_rules_expand_file): the output equals the rule oracle's expansion in word-major
+    order with rejected candidates skipped and non-printable candidates as $HEX[] -- over 20k words x 148 rules
+    (3M candidates: several sub-batches, both slot sets), $HEX[] source words decoded, a 300-byte word rejected.
+    Plain text (what hashcat writes) and gzip.  Parity with hashcat itself unpinned."""
     from dwpa_amd.help_crack import expand_rules
     rng = random.Random(32)
-    words = [S.random_psk(rng, 1, 20) for _ in range(500)] + [b"x" * 300]
+    words = [S.random_psk(rng, 1, 20) for _ in range(20000)] + [b"x" * 300]
+    words[7] = b"\x00\xffAb"
     rules = wpa_rules()
     src = tmp_path / "source.txt"
-    src.write_bytes(b"\n".join(words) + b"\n")
+    src.write_bytes(b"\n".join(b"$HEX[" + w.hex().encode() + b"]" if any(b < 0x20 or b > 0x7E for b in w) else w
+                                for w in words) + b"\n")
     rf = tmp_path / "bestWPA.rule"
     rf.write_text("\n".join(rules) + "\n")
     out = tmp_path / "cracked.txt.gz"
-    n = expand_rules(str(rf), str(src), str(out), chunk=128)
-    exp = [c for row in R.expand(rules, words) for c in row if c is not None]
-    with gzip.open(out, "rb") as f:
-        got = f.read().split(b"\n")[:-1]
-    assert n == len(exp) and got == exp
+    n = expand_rules(str(rf), str(src), str(out), gzip_level=gzip_level)
+    exp = [_stdout_plain(c) for row in R.expand(rules, words) for c in row if c is not None]
+    raw = out.read_bytes()
+    if gzip_level:
+        raw = gzip.decompress(raw)
+    got = raw.split(b"\n")[:-1]
+    assert n == len(exp) and len(got) == len(exp)
+    assert got == exp
+    assert any(g.startswith(b"$HEX[00ff") for g in got)
 
 
 def test_crack_files_several_dictionaries(tmp_path):
