@@ -58,7 +58,8 @@ clean:
 .PHONY: all oracle clean asm
 
 tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
-       tools/bin/inflate_check tools/bin/item_queue_check tools/bin/rules_fuzz_asan tools/bin/clock_idle
+       tools/bin/inflate_check tools/bin/item_queue_check tools/bin/rules_fuzz_asan tools/bin/clock_idle \
+       tools/bin/inflate_check_tsan
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -101,3 +102,8 @@ tools/bin/rules_fuzz_asan: tools/rules_fuzz.cpp $(SRC)/rules.cpp $(SRC)/rules.hp
 tools/bin/clock_idle: tools/clock_idle.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+# the parallel inflate (loader thread + workers + the reader) under ThreadSanitizer
+tools/bin/inflate_check_tsan: tools/inflate_check.cpp $(SRC)/inflate.hpp $(SRC)/pinflate.hpp
+	@mkdir -p tools/bin
+	g++ -O1 -g -std=c++17 -Wall -I$(SRC) -fsanitize=thread -o $@ tools/inflate_check.cpp -lz -lpthread
