@@ -514,6 +514,14 @@ static uint32_t head_pmks(uint32_t nu) {
     return nu / unit * unit;
 }
 
+// T's key bytes and their offsets/lengths (every slot of the call) up d.stream.
+static int upload_slot_keys(Device& d, const SlotTable& T) {
+    RCHK(upload_span(d.koff, Span<uint64_t>{T.koff, T.n}, d.stream));
+    RCHK(upload_span(d.klen, Span<uint32_t>{T.klen, T.n}, d.stream));
+    RCHK(upload_span(d.kbytes, Span<uint8_t>{T.kbytes, T.nbytes + 16}, d.stream));
+    return 0;
+}
+
 // Derive the PMKs of slots [b, e) of T into batch.pmk (slot order) and their key ordinals into batch.ids.  Unique
 // (ESSID, key) pairs are derived once, all ESSIDs in one PBKDF2 launch (server batches fan one key out to every
 // net of an ESSID, common.php:879-902); each slot then gathers its PMK from them or from the caller's $pmk
@@ -637,11 +645,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
                 st.split = i;
                 break;
             }
-    if (upload_keys) {
-        RCHK(upload_span(d.koff, Span<uint64_t>{T.koff, T.n}, s));
-        RCHK(upload_span(d.klen, Span<uint32_t>{T.klen, T.n}, s));
-        RCHK(upload_span(d.kbytes, Span<uint8_t>{T.kbytes, T.nbytes + 16}, s));
-    }
+    if (upload_keys) RCHK(upload_slot_keys(d, T));
     if (nu) {
         RCHK(upload_span(d.uslot, st.uslot, s));
         RCHK(upload_span(d.salt, st.spool, s));
@@ -1024,6 +1028,8 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
             }
         }
     });
+    // the key bytes go up now, while the host deduplicates (derive_slots): the first kernel waits for them
+    RCHK(upload_slot_keys(d, T));
     tr.mark("slots");
 
     // The first chunk's PBKDF2 is queued before the line tables exist: the host builds them while the GPU derives.
@@ -1054,7 +1060,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         }
         runs.push_back((uint32_t)(e - b));
         DeriveStage st;
-        RCHK(derive_slots(d, T, b, e, cs.job_pmk, runs, run_essid, b == 0, st));
+        RCHK(derive_slots(d, T, b, e, cs.job_pmk, runs, run_essid, false, st));
         if (b == 0) {
             for (uint32_t j : cs.order) job_line[j] = tb.add_line(cs.parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
             tr.mark("tables (overlapped)");

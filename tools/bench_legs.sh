@@ -6,7 +6,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/legs}
 mkdir -p $OUT
-LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm c3files"}
+LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm c3files c3files_server expand"}
 for leg in $LEGS; do
   case $leg in
     peak)    OUT=$OUT/peak tools/regen_peak.sh > /dev/null ;;
@@ -26,6 +26,10 @@ for leg in $LEGS; do
                > $OUT/c2files_warm.json 2> $OUT/c2files_warm.err ;;
     c3files) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --steps 2 --warmup 0 \
                > $OUT/c3files.json 2> $OUT/c3files.err ;;
+    c3files_server) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --rules-set server --steps 2 \
+               --warmup 0 > $OUT/c3files_server.json 2> $OUT/c3files_server.err ;;
+    expand)  timeout -k 10 300 python3 bench.py --workload expand --rule-words 5000000 --steps 2 --warmup 1 \
+               > $OUT/expand.json 2> $OUT/expand.err ;;
     *) echo "unknown leg $leg" >&2; exit 2 ;;
   esac
   echo "leg $leg done" >&2
