@@ -1,6 +1,7 @@
 # round 4, call k: the round's full measurement on one box, in two parts (one call each, PART=1|2):
 #   1: GPU suite, smoke, then the in-memory bench legs (tools/bench_legs.sh)
-#   2: the file legs (gz dictionaries, rules, expansion) and a rocprofv3 kernel-trace summary of the default bench
+#   2: the file legs (gz dictionaries, rules, expansion), a rocprofv3 kernel-trace summary of the default bench, and
+#      the C5 test with every one of its 1,010 jobs prefix-checked against the oracle (DWPA_FULL_ORACLE=1)
 cd $GRAFT_REPO_ROOT
 O=${O:-gpurun_out/r04k}
 mkdir -p $O
@@ -19,5 +20,9 @@ else
   guard $?
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
   guard $?
+  DWPA_FULL_ORACLE=1 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_configs.py -m gpu -k c5_mixed -x -v -s --timeout 380 \
+    --timeout-method thread > $O/c5_full_oracle_pytest.txt 2>&1
+  guard $?
+  grep -h "DWPA_FULL_ORACLE\|passed\|failed" $O/c5_full_oracle_pytest.txt
 fi
 for f in $O/legs/*.json; do echo "$f $(python3 -c "import json;d=json.load(open('$f'));print(d.get('value'),d.get('unit'))" 2>/dev/null)"; done
