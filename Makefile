@@ -59,7 +59,7 @@ clean:
 
 tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
        tools/bin/inflate_check tools/bin/item_queue_check tools/bin/rules_fuzz_asan tools/bin/clock_idle \
-       tools/bin/inflate_check_tsan
+       tools/bin/inflate_check_tsan tools/bin/tail_placement
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -100,6 +100,10 @@ tools/bin/rules_fuzz_asan: tools/rules_fuzz.cpp $(SRC)/rules.cpp $(SRC)/rules.hp
 	    -o $@ tools/rules_fuzz.cpp $(SRC)/rules.cpp
 
 tools/bin/clock_idle: tools/clock_idle.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+tools/bin/tail_placement: tools/tail_placement.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 
