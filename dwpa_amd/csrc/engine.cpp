@@ -205,7 +205,6 @@ struct Device {
     DevBuf koff, klen, kbytes, uslot;  // check path: the call's key bytes by slot, unique key -> its first slot
     DevBuf keys, keys_tail;        // check path: per-key EapolKey scratch of the attempt-parallel verify
     DevBuf first_hit;              // check path: per line (= job), the smallest slot with a hit so far (~0u: none)
-    DevBuf tail_state;             // check path: U and T of every tail lane between tail pieces (DWPA_TAIL_PIECES)
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
     SlotTable slots;               // check path: the call's slots (capacity kept between calls)
     CheckScratch cs;               // check path: host-phase scratch
@@ -296,14 +295,6 @@ static int env_int(const char* name, int dflt, int lo, int hi) {
 static int check_prio_knob() { static const int v = env_int("DWPA_CHECK_PRIO", 0, 0, 3); return v; }
 static int kv3_prio_knob() { static const int v = env_int("DWPA_KV3_PRIO", 0, 0, 3); return v; }
 static int tail_prio_knob() { static const int v = env_int("DWPA_TAIL_PRIO", 2, 0, 3); return v; }
-// DWPA_TAIL_PIECES=P (2..64): the check path's PBKDF2 tail runs as P sequential launches of 4096/P iterations at
-// priority DWPA_TAIL_PIECE_PRIO (default 3) with the head's priorities shifted to 2..0; 0/1 = one tail launch beside
-// the head at priority 0 (k_pbkdf2_ms_tail).  Read on every derive (tests switch it within one process).
-static int tail_pieces_knob() {
-    const int p = env_int("DWPA_TAIL_PIECES", 0, 0, 64);
-    return p < 2 ? 0 : p;
-}
-static int tail_piece_prio_knob() { static const int v = env_int("DWPA_TAIL_PIECE_PRIO", 3, 0, 3); return v; }
 static bool head_fence_knob() { static const bool v = env_int("DWPA_HEAD_FENCE", 1, 0, 1) != 0; return v; }
 static bool verify_fanout_knob() { static const bool v = env_int("DWPA_VERIFY_FANOUT", 1, 0, 1) != 0; return v; }
 static bool verify_kv3_first_knob() { static const bool v = env_int("DWPA_VERIFY_KV3_FIRST", 0, 0, 1) != 0; return v; }
@@ -677,21 +668,13 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
         std::lock_guard<std::mutex> fl(f.mu);
         if (head_fence_knob() && f.last && f.last != d.head_end) HIPCHK(hipStreamWaitEvent(s, f.last, 0));
         uint32_t* head_flag = (uint32_t*)d.batch.counters.p + 3;  // zeroed with the counters above
-        const int pieces = nh < nu ? tail_pieces_knob() : 0;
         if (nh < nu) {  // the tail first, beside the head (priority 0 until the head has ended: pbkdf2_lane_tail)
             HIPCHK(hipEventRecord(d.prep_done, s));
             HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
-            if (pieces) {  // or in pieces, ahead of the head's waves (DWPA_TAIL_PIECES)
-                RCHK(d.tail_state.ensure((size_t)(nu - nh) * 2 * 10 * 4));
-                HIPCHK(launch_pbkdf2_ms_pieces(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh,
-                                               upmk + nh, (uint32_t*)d.tail_state.p, (uint32_t)pieces,
-                                               (uint32_t)tail_piece_prio_knob(), d.tail));
-            } else {
-                HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh,
-                                             upmk + nh, head_flag, (uint32_t)tail_prio_knob(), d.tail));
-            }
+            HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh,
+                                         head_flag, (uint32_t)tail_prio_knob(), d.tail));
         }
-        HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s, pieces ? 2 : 3));
+        HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
         if (nh < nu) HIPCHK(launch_set_flag(head_flag, s));
         HIPCHK(hipEventRecord(d.head_end, s));
         f.last = d.head_end;
@@ -1521,7 +1504,7 @@ void dwpa_shutdown(void) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
         for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->keys, &d->keys_tail, &d->salt,
-                          &d->first_hit, &d->tail_state,
+                          &d->first_hit,
                           &d->koff, &d->klen, &d->kbytes, &d->uslot, &d->upmk, &d->sref, &d->src, &d->cpmk,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();

@@ -137,48 +137,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     store_block(pmk, cap, s, blk, t);
 }
 
-// One piece of the check path's tail (DWPA_TAIL_PIECES, pbkdf2_u1 / pbkdf2_iterate): iterations [it0, it1) of every
-// tail lane at wave priority `prio`; U and T of lane (blk, s) carried in `state` (word k at k * 2 * count + lane).
-// The pieces run one after another on the tail stream, so every piece lands on the SIMDs that are free when it is
-// dispatched and the tail's work is spread over more SIMDs than one launch's waves hold.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_ms_piece(
-    const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
-    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, uint32_t* __restrict__ state, uint32_t it0,
-    uint32_t it1, uint32_t prio) {
-    set_wave_prio(prio);
-    const uint32_t blk = blockIdx.y;
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= min(count, cap)) return;
-    uint32_t hi[5], ho[5], u[5], t[5];
-    load_mid(mid, cap, s, hi, ho);
-    const size_t lane = (size_t)blk * count + s, stride = 2 * (size_t)count;
-    uint32_t it = it0;
-    if (it0 == 0) {
-        const uint32_t* e = pool + sref[s];
-        const uint32_t nsalt = e[0];
-        pbkdf2_u1(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, u);
-#pragma unroll
-        for (int k = 0; k < 5; k++) t[k] = u[k];
-        it = 1;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            u[k] = state[k * stride + lane];
-            t[k] = state[(5 + k) * stride + lane];
-        }
-    }
-    pbkdf2_iterate(hi, ho, u, t, it, it1);
-    if (it1 >= 4096) {
-        store_block(pmk, cap, s, blk, t);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            state[k * stride + lane] = u[k];
-            state[(5 + k) * stride + lane] = t[k];
-        }
-    }
-}
-
 // Sets the tail's head-done flag (agent scope: the tail's waves poll it from every XCD).
 __global__ void k_set_flag(uint32_t* __restrict__ flag) {
     if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -782,18 +740,6 @@ hipError_t launch_pbkdf2_ms_tail(const uint32_t* mid, uint32_t cap, uint32_t cou
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pbkdf2_ms_tail, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, count, pool, sref, pmk,
                        flag, prio);
-    return hipGetLastError();
-}
-
-hipError_t launch_pbkdf2_ms_pieces(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                                   const uint32_t* sref, uint32_t* pmk, uint32_t* state, uint32_t pieces,
-                                   uint32_t prio, hipStream_t s) {
-    if (count == 0) return hipSuccess;
-    for (uint32_t p = 0; p < pieces; p++) {
-        const uint32_t it0 = 4096u * p / pieces, it1 = 4096u * (p + 1) / pieces;
-        hipLaunchKernelGGL(k_pbkdf2_ms_piece, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, count, pool, sref,
-                           pmk, state, it0, it1, prio);
-    }
     return hipGetLastError();
 }
 

@@ -26,9 +26,8 @@ const char* pbkdf2_variant();
 // PMKs that give every SIMD of the current device one PBKDF2 wave (two output-block lanes per PMK); 0 on error
 uint32_t pbkdf2_wave_unit();
 // many ESSIDs per launch: slot s uses the salt entry pool + sref[s] = {nsalt, [2][nsalt][16] words}
-// prio_top 2: a one-round launch's progress-ordered priorities run 2, 1, 0 instead of 3, 2, 1 (k_pbkdf2_gfx950_ms_p2)
 hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                            const uint32_t* sref, uint32_t* pmk, hipStream_t s, int prio_top = 3);
+                            const uint32_t* sref, uint32_t* pmk, hipStream_t s);
 hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                   const uint32_t* sref, uint32_t* pmk, hipStream_t s);
 // attempt-parallel verification of EAPOL lists with >= ATT_PARALLEL_MIN attempts: lane = (key, attempt) item,
@@ -54,10 +53,6 @@ hipError_t launch_pbkdf2_mg_plain(const uint32_t* mid, uint32_t cap, const uint3
 hipError_t launch_pbkdf2_ms_tail(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                  const uint32_t* sref, uint32_t* pmk, const uint32_t* flag, uint32_t prio,
                                  hipStream_t s);
-// The same tail in `pieces` sequential launches at wave priority `prio` (state: 10 words per lane, 2 * count lanes).
-hipError_t launch_pbkdf2_ms_pieces(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                                   const uint32_t* sref, uint32_t* pmk, uint32_t* state, uint32_t pieces,
-                                   uint32_t prio, hipStream_t s);
 hipError_t launch_set_flag(uint32_t* flag, hipStream_t s);
 // Wave priority (0..3) of the check path's post-derive kernels (PMK gather, EAPOL key states, verifies) on the
 // current device; the hit copy-out always runs at 3.

@@ -22,18 +22,7 @@ namespace dwpa {
 // starts at priority 3 and drops to 2 at iteration 3584 and to 1 at 3968, so waves that are behind get the issue
 // slots and the waves of a SIMD reach the end together (spread <= ~128 iterations instead of up to a whole wave).
 // Priority 0 stays free for work that should only take the slots these waves leave (the check path's tail).
-// TOP = 2 shifts the three levels to 2, 1, 0, which leaves priority 3 to work that should run ahead of every head
-// wave (the check path's tail cut into pieces, DWPA_TAIL_PIECES).
-__device__ __forceinline__ void set_prio_imm(int p) {
-    switch (p) {  // s_setprio takes an immediate; p is a compile-time constant at every call site
-    case 0: __builtin_amdgcn_s_setprio(0); break;
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    case 2: __builtin_amdgcn_s_setprio(2); break;
-    default: __builtin_amdgcn_s_setprio(3); break;
-    }
-}
-
-template <bool PRIO = false, int TOP = 3>
+template <bool PRIO = false>
 __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
                                             uint32_t nsalt, uint32_t t[5]) {
     uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
@@ -58,13 +47,13 @@ __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t
             for (int k = 0; k < 5; k++) t[k] ^= u[k];
         }
     } else {
-        set_prio_imm(TOP);
+        __builtin_amdgcn_s_setprio(3);
         int it = 1;
 #pragma unroll 1
         for (int phase = 0; phase < 3; phase++) {
             const int end = phase == 0 ? 3584 : phase == 1 ? 3968 : 4096;
-            if (phase == 1) set_prio_imm(TOP - 1);
-            else if (phase == 2) set_prio_imm(TOP - 2);
+            if (phase == 1) __builtin_amdgcn_s_setprio(2);
+            else if (phase == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll 1
             for (; it < end; it++) {
                 sha1_84(MI, u, x);
@@ -121,35 +110,6 @@ __device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uin
     }
 #pragma unroll 1
     for (; it < 4096; it++) {
-        sha1_84(MI, u, x);
-        sha1_84(MO, x, u);
-#pragma unroll
-        for (int k = 0; k < 5; k++) t[k] ^= u[k];
-    }
-}
-
-// The check path's tail cut into sequential pieces (DWPA_TAIL_PIECES): one piece runs iterations [it0, it1) of a
-// lane's output block, carrying U and T between pieces.  pbkdf2_u1 is the lane's first iteration (the salt blocks
-// and U_1 = T); pbkdf2_iterate the loop body of pbkdf2_lane over [it, end).
-__device__ __forceinline__ void pbkdf2_u1(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
-                                          uint32_t nsalt, uint32_t u[5]) {
-    uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
-    for (uint32_t b = 0; b < nsalt; b++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) m[j] = sb[b * 16 + j];
-        sha1_compress(st, m);
-    }
-    sha1_84(sha1_mid(ho), st, u);
-}
-
-__device__ __forceinline__ void pbkdf2_iterate(const uint32_t hi[5], const uint32_t ho[5], uint32_t u[5],
-                                               uint32_t t[5], uint32_t it, uint32_t end) {
-    const Sha1Mid MI = sha1_mid(hi);
-    const Sha1Mid MO = sha1_mid(ho);
-    uint32_t x[5];
-#pragma unroll 1
-    for (; it < end; it++) {
         sha1_84(MI, u, x);
         sha1_84(MO, x, u);
 #pragma unroll
@@ -224,7 +184,7 @@ __device__ __forceinline__ void pbkdf2_body_queue(const uint32_t* __restrict__ m
 // Many ESSIDs in one launch (server batches, common.php:902): slot s derives with the salt entry at
 // pool + sref[s] = {nsalt, [2 blocks][nsalt][16] words}.  Only the U_1 blocks differ per lane; the 4096 loop is
 // the same code as pbkdf2_body's.
-template <bool PRIO = false, int TOP = 3>
+template <bool PRIO = false>
 __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
                                                const uint32_t* __restrict__ pool,
                                                const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk) {
@@ -235,7 +195,7 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
     load_mid(mid, cap, s, hi, ho);
     const uint32_t* e = pool + sref[s];
     const uint32_t nsalt = e[0];
-    pbkdf2_lane<PRIO, TOP>(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
+    pbkdf2_lane<PRIO>(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
     store_block(pmk, cap, s, blk, t);
 }
 

@@ -45,13 +45,6 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     dwpa::pbkdf2_body_ms<true>(mid, cap, count, pool, sref, pmk);
 }
 
-// The check path's head when its tail runs in pieces at priority 3 (DWPA_TAIL_PIECES): levels 2, 1, 0.
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_ms_p2(
-    const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
-    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk) {
-    dwpa::pbkdf2_body_ms<true, 2>(mid, cap, count, pool, sref, pmk);
-}
-
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_mg_p(
     const uint32_t* __restrict__ mid, uint32_t cap, const uint32_t* __restrict__ counter, uint32_t ngroups,
     const uint32_t* __restrict__ salt, const uint32_t* __restrict__ gsalt, uint32_t* __restrict__ pmk,

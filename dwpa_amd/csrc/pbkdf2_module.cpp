@@ -20,7 +20,6 @@ extern const size_t pbkdf2_gfx950_hsaco_size;
 struct Fns {
     hipFunction_t one, ms, mg;  // k_pbkdf2_gfx950 (one ESSID), _ms (per-slot salt), _mg (ESSID groups x batch)
     hipFunction_t one_p, ms_p, mg_p;  // the same with progress-ordered wave priority (pbkdf2_dev.hpp PRIO)
-    hipFunction_t ms_p2;              // ms_p with the priority levels 2, 1, 0 (the check path's tail in pieces)
     hipFunction_t one_q, mg_q;        // the one-ESSID and group kernels as work queues (pbkdf2_dev.hpp *_queue)
     uint64_t level_lanes;       // lanes that give every SIMD of the device one wave: CUs x 4 SIMDs x 64
 };
@@ -81,7 +80,6 @@ static hipError_t tuned_functions(Fns* fn) {
     if ((e = hipModuleGetFunction(&fn->one_p, mod, "k_pbkdf2_gfx950_p")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->ms_p, mod, "k_pbkdf2_gfx950_ms_p")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->mg_p, mod, "k_pbkdf2_gfx950_mg_p")) != hipSuccess) return e;
-    if ((e = hipModuleGetFunction(&fn->ms_p2, mod, "k_pbkdf2_gfx950_ms_p2")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->one_q, mod, "k_pbkdf2_gfx950_q")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->mg_q, mod, "k_pbkdf2_gfx950_mg_q")) != hipSuccess) return e;
     int cus = 0;
@@ -134,7 +132,7 @@ hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint3
 }
 
 hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                            const uint32_t* sref, uint32_t* pmk, hipStream_t s, int prio_top) {
+                            const uint32_t* sref, uint32_t* pmk, hipStream_t s) {
     if (count == 0) return hipSuccess;
     if (use_plain()) return launch_pbkdf2_ms_plain(mid, cap, count, pool, sref, pmk, s);
     Fns fn;
@@ -143,8 +141,8 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
     if (lone_waves(fn, std::min(count, cap))) return launch_pbkdf2_ms_plain(mid, cap, count, pool, sref, pmk, s);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk};
     const uint32_t wg = wg_size();
-    const hipFunction_t f = !use_prio(fn, std::min(count, cap)) ? fn.ms : prio_top == 2 ? fn.ms_p2 : fn.ms_p;
-    return hipModuleLaunchKernel(f, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args, nullptr);
+    return hipModuleLaunchKernel(use_prio(fn, std::min(count, cap)) ? fn.ms_p : fn.ms, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args,
+                                 nullptr);
 }
 
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,

@@ -18,7 +18,7 @@ if [ "${PART:-1}" = 1 ]; then
 else
   LEGS="c2files c2files_warm c3files c3files_server expand" OUT=$O/legs timeout -k 10 700 bash tools/bench_legs.sh
   guard $?
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof_bench.err
   guard $?
   DWPA_FULL_ORACLE=1 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_configs.py -m gpu -k c5_mixed -x -v -s --timeout 380 \
     --timeout-method thread > $O/c5_full_oracle_pytest.txt 2>&1
