@@ -109,6 +109,37 @@ def test_random_batch_vs_oracle():
     assert sum(1 for e in exp if e) > 60
 
 
+def test_binary_essids_and_keys_vs_oracle():
+    """ESSIDs and PSKs of arbitrary bytes: NUL, 0x80-0xff, the hashline's own separators '*' and ':' (the ESSID field
+    is hex, so hex2bin hands PHP any byte string, common.php:165,233), ESSIDs of 1..64 bytes sharing a batch, keys of
+    0..80 bytes with embedded NULs (strings, not C strings, on both sides of the FFI) and $HEX[] forms of them."""
+    rng = random.Random(4242)
+    jobs = []
+    for i in range(120):
+        essid = bytes(rng.choice([0, 0x2a, 0x3a, 0xff, 0x80, rng.randrange(256)]) for _ in range(rng.choice(
+            [1, 2, 13, 31, 32, 33, 47, 64])))
+        ap, sta = rng.randbytes(6), rng.randbytes(6)
+        psk = bytes(rng.choice([0, 0xff, 0x3a, rng.randrange(256)]) for _ in range(rng.choice([0, 1, 8, 31, 63, 64, 80])))
+        kind = rng.choice(["pmkid", 1, 2, 3])
+        if kind == "pmkid":
+            line = S.pmkid_line(psk, essid, ap, sta)
+        else:
+            line = S.eapol_line(psk, essid, ap, sta, rng.randbytes(32), rng.randbytes(32), kind, rng.randint(-5, 5),
+                                rng.choice(["LE", "BE"]), rng=rng)
+        keys = [bytes(rng.randrange(256) for _ in range(rng.randint(0, 20))) for _ in range(rng.randint(0, 6))]
+        form = psk if i % 3 else b"$HEX[" + psk.hex().encode() + b"]"
+        if rng.random() < 0.85:
+            keys.insert(rng.randint(0, len(keys)), form)
+        jobs.append((line, keys, False, rng.choice([0, 8, 128])))
+    exp = _oracle_many(jobs)
+    got = dwpa_amd.check_batch(jobs)
+    mism = [(i, g, e) for i, (g, e) in enumerate(zip(got, exp)) if g != e]
+    assert not mism, mism[:3]
+    for i in range(0, len(jobs), 7):
+        assert dwpa_amd.check_key_m22000(*jobs[i]) == exp[i]
+    assert sum(1 for e in exp if e) > 70
+
+
 def test_mutated_lines_vs_oracle():
     """Parse semantics by mutation (tests/mutate.py): 1,500 valid PMKID/keyver 1/2/3 lines with one or two random
     mutations each (type field spellings, dropped/inserted/replaced characters, upper-case fields, odd or short or
