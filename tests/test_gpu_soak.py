@@ -39,10 +39,8 @@ def _calls(seed):
     rng = random.Random(seed)
     nets = [S.random_net(rng) for _ in range(6)]
     seq = []
-    for r in range(24):
-        shape = rng.choice(["one", "one", "batch", "batch", "mid"] + (["big"] if r in (5, 17) else []))
-        if r in (5, 17):
-            shape = "big"
+    for r in range(16):
+        shape = "big" if r in (3, 11) else rng.choice(["one", "one", "batch", "batch", "mid"])
         if shape == "one":
             seq.append(("one", [_job(rng, nets, rng.randint(0, 20), rng.choice([0, 8, 128]),
                                      caller=rng.random() < 0.3)]))
