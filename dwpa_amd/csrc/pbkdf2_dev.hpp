@@ -117,6 +117,34 @@ __device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uin
     }
 }
 
+// The first iteration of a lane's output block (the salt blocks and U_1) and the PBKDF2 loop over [it, end), for
+// kernels that cut the 4096 iterations into pieces (pbkdf2_body_ms_chunked).
+__device__ __forceinline__ void pbkdf2_u1(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
+                                          uint32_t nsalt, uint32_t u[5]) {
+    uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
+    for (uint32_t b = 0; b < nsalt; b++) {
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) m[j] = sb[b * 16 + j];
+        sha1_compress(st, m);
+    }
+    sha1_84(sha1_mid(ho), st, u);
+}
+
+__device__ __forceinline__ void pbkdf2_iterate(const uint32_t hi[5], const uint32_t ho[5], uint32_t u[5],
+                                               uint32_t t[5], uint32_t it, uint32_t end) {
+    const Sha1Mid MI = sha1_mid(hi);
+    const Sha1Mid MO = sha1_mid(ho);
+    uint32_t x[5];
+#pragma unroll 1
+    for (; it < end; it++) {
+        sha1_84(MI, u, x);
+        sha1_84(MO, x, u);
+#pragma unroll
+        for (int k = 0; k < 5; k++) t[k] ^= u[k];
+    }
+}
+
 __device__ __forceinline__ void load_mid(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t s, uint32_t hi[5],
                                          uint32_t ho[5]) {
 #pragma unroll
@@ -197,6 +225,85 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
     const uint32_t nsalt = e[0];
     pbkdf2_lane<PRIO>(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
     store_block(pmk, cap, s, blk, t);
+}
+
+// The check path's derive as a work queue of iteration chunks (DWPA_CHECK_CHUNKS).  A one-round launch of nu unique
+// PMKs at k.f waves per SIMD leaves the SIMDs that hold a (k+1)-th wave k+1 wave times of work, whatever the
+// schedule ("Where a C5 call goes now").  Here a chain = (64 slots, output block) is cut into
+// nchunks pieces of 4096 / nchunks iterations, U and T carried in `state` between pieces, and the resident waves take
+// (chunk, chain) items chunk-major from one counter: a chain moves from wave to wave (and SIMD to SIMD) at chunk
+// boundaries, so the work of the last 0.f waves spreads over every SIMD instead of landing on a few.
+//   ctl[0] = item counter, ctl[1] = error flag (a dependency wait ran out), ctl[16 + c] = chunks of chain c done.
+// An item (k, c) with k > 0 waits for (k - 1, c), which has a smaller item number, so it was taken earlier by a wave
+// that is running: every wait ends.  The wait is bounded anyway (spin limit -> ctl[1] = 1, the host fails the call).
+// Chunk k's state is published with an agent-scope release (the next chunk may run on another XCD) and read after
+// an agent-scope acquire.
+__device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
+                                                       const uint32_t* __restrict__ pool,
+                                                       const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk,
+                                                       uint32_t* __restrict__ state, uint32_t* __restrict__ ctl,
+                                                       uint32_t nchunks) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t n = min(count, cap);
+    const uint32_t nchains = 2u * ((n + 63u) / 64u);
+    const uint32_t nitems = nchains * nchunks;
+    const size_t S = (size_t)nchains * 64u;  // state word stride
+    uint32_t* done = ctl + 16;
+#pragma unroll 1
+    for (;;) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(ctl, 1u);
+        item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
+        if (item >= nitems) break;
+        const uint32_t k = item / nchains, c = item - k * nchains;
+        if (k) {
+            uint32_t spins = 0;
+            while (__builtin_amdgcn_readfirstlane(
+                       __hip_atomic_load(done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < k) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 24)) {  // ~seconds: never expected; fail the call instead of hanging the GPU
+                    if (lane == 0) __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        const uint32_t blk = c & 1u;
+        const uint32_t s = (c >> 1) * 64u + lane;
+        const size_t si = (size_t)c * 64u + lane;
+        if (s < n) {
+            uint32_t hi[5], ho[5], u[5], t[5];
+            load_mid(mid, cap, s, hi, ho);
+            uint32_t it = 4096u * k / nchunks;
+            const uint32_t end = 4096u * (k + 1) / nchunks;
+            if (k == 0) {
+                const uint32_t* e = pool + sref[s];
+                const uint32_t nsalt = e[0];
+                pbkdf2_u1(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, u);
+#pragma unroll
+                for (int w = 0; w < 5; w++) t[w] = u[w];
+                it = 1;
+            } else {
+#pragma unroll
+                for (int w = 0; w < 5; w++) {
+                    u[w] = state[w * S + si];
+                    t[w] = state[(5 + w) * S + si];
+                }
+            }
+            pbkdf2_iterate(hi, ho, u, t, it, end);
+            if (k + 1 == nchunks) {
+                store_block(pmk, cap, s, blk, t);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 5; w++) {
+                    state[w * S + si] = u[w];
+                    state[(5 + w) * S + si] = t[w];
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) __hip_atomic_store(done + c, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // Many ESSID groups x one candidate batch in one launch (scan work units with many ESSIDs):
