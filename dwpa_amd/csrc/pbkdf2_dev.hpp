@@ -236,6 +236,7 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
 //   ctl[0] = item counter, ctl[1] = error flag (a dependency wait ran out), ctl[16 + c] = chunks of chain c done.
 // An item (k, c) with k > 0 waits for (k - 1, c), which has a smaller item number, so it was taken earlier by a wave
 // that is running: every wait ends.  The wait is bounded anyway (spin limit -> ctl[1] = 1, the host fails the call).
+// The done words are written and polled with atomic read-modify-writes only.
 // Chunk k's state is published with an agent-scope release (the next chunk may run on another XCD) and read after
 // an agent-scope acquire.
 __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
@@ -257,12 +258,25 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
         if (item >= nitems) break;
         const uint32_t k = item / nchains, c = item - k * nchains;
         if (k) {
+            // polled with an atomic read-modify-write: a plain (even agent-scope) load of a line this XCD's L2 already
+            // holds kept returning that copy (measured: the waits ran out), while the RMW is performed where every
+            // XCD sees the same word
             uint32_t spins = 0;
-            while (__builtin_amdgcn_readfirstlane(
-                       __hip_atomic_load(done + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < k) {
+            for (;;) {
+                // compare-and-swap k -> k: succeeds once chunk k - 1 is done (the word only grows, to k at most
+                // before this item runs); a load-like RMW (add 0, or 0) is turned back into a plain load by the
+                // compiler
+                uint32_t v = 0;
+                if (lane == 0) {
+                    uint32_t expect = k;
+                    __hip_atomic_compare_exchange_strong(done + c, &expect, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    v = expect;  // k on success, else the current count
+                }
+                if (__builtin_amdgcn_readfirstlane(__shfl(v, 0)) >= k) break;
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24)) {  // ~seconds: never expected; fail the call instead of hanging the GPU
-                    if (lane == 0) __hip_atomic_store(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (++spins > (1u << 20)) {  // never expected: fail the call instead of spinning on
+                    if (lane == 0) __hip_atomic_fetch_or(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
@@ -302,7 +316,7 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) __hip_atomic_store(done + c, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_fetch_max(done + c, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
