@@ -235,7 +235,8 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
 // boundaries, so the work of the last 0.f waves spreads over every SIMD instead of landing on a few.
 //   ctl[0] = item counter, ctl[1] = error flag (a dependency wait ran out), ctl[16 + c] = chunks of chain c done.
 // An item (k, c) with k > 0 waits for (k - 1, c), which has a smaller item number, so it was taken earlier by a wave
-// that is running: every wait ends.  The wait is bounded anyway (spin limit -> ctl[1] = 1, the host fails the call).
+// that is running: every wait ends.  The wait is bounded anyway (1 s -> ctl[1] = 1, the host fails the call).  With
+// fewer resident waves than chains, (k - 1, c) was taken about one chunk time before (k, c), so waits are rare.
 // The done words are written and polled with atomic read-modify-writes only.
 // Chunk k's state is published with an agent-scope release (the next chunk may run on another XCD) and read after
 // an agent-scope acquire.
@@ -261,7 +262,7 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
             // polled with an atomic read-modify-write: a plain (even agent-scope) load of a line this XCD's L2 already
             // holds kept returning that copy (measured: the waits ran out), while the RMW is performed where every
             // XCD sees the same word
-            uint32_t spins = 0;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
             for (;;) {
                 // compare-and-swap k -> k: succeeds once chunk k - 1 is done (the word only grows, to k at most
                 // before this item runs); a load-like RMW (add 0, or 0) is turned back into a plain load by the
@@ -274,8 +275,9 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
                     v = expect;  // k on success, else the current count
                 }
                 if (__builtin_amdgcn_readfirstlane(__shfl(v, 0)) >= k) break;
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 20)) {  // never expected: fail the call instead of spinning on
+                __builtin_amdgcn_s_sleep(16);  // ~1k cycles between polls: thousands of polling waves would
+                                               // otherwise crowd the device-scope atomics the producers need
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: fail the call, never spin on
                     if (lane == 0) __hip_atomic_fetch_or(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }

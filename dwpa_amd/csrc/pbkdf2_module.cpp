@@ -148,7 +148,7 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
 }
 
 // k_pbkdf2_gfx950_ms_c over `count` unique PMKs: chains = 2 x ceil(count / 64) (64 slots x output block), each
-// cut into `nchunks` pieces; the grid holds min(chains, 8 per SIMD) waves, every one of them resident at once.
+// cut into `nchunks` pieces; the grid holds min(7/8 of the chains, 8 per SIMD) waves, all resident at once.
 // ctl needs 16 + chains words and state 10 x 64 x chains words; ctl is zeroed here, on the launch's stream.
 uint32_t pbkdf2_chunk_chains(uint32_t count) { return 2u * ((count + 63u) / 64u); }
 
@@ -162,7 +162,8 @@ hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t 
     if (e != hipSuccess) return e;
     const uint32_t chains = pbkdf2_chunk_chains(std::min(count, cap));
     if ((e = hipMemsetAsync(ctl, 0, (16 + (size_t)chains) * 4, s)) != hipSuccess) return e;
-    const uint64_t waves = std::min<uint64_t>(chains, 8 * fn.level_lanes / 64);
+    // fewer waves than chains (7/8): item (k, c) is taken about one chunk time after (k - 1, c), so it rarely waits
+    const uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>(chains - chains / 8, 8 * fn.level_lanes / 64));
     const uint32_t blocks = (uint32_t)((waves + 3) / 4);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk,
                     (void*)&state, (void*)&ctl, (void*)&nchunks};
