@@ -259,26 +259,21 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
         if (item >= nitems) break;
         const uint32_t k = item / nchains, c = item - k * nchains;
         if (k) {
-            // polled with an atomic read-modify-write: a plain (even agent-scope) load of a line this XCD's L2 already
-            // holds kept returning that copy (measured: the waits ran out), while the RMW is performed where every
-            // XCD sees the same word
+            // Polled with an atomic read-modify-write: a plain (even agent-scope) load of a line this XCD's L2 already
+            // holds may keep returning that copy, while the RMW is performed where every XCD sees the same word.  A
+            // compare-and-swap k -> k succeeds once chunk k - 1 is done (the word only grows, to k at most before
+            // this item runs); load-like RMWs (add 0, or 0) are turned back into plain loads by the compiler.  Every
+            // lane polls (same address): a lane-0-only atomic inside this loop and at the end of the item loop made
+            // the compiler split the item loop by lanes, and lane 0 stopped taking items.
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
             for (;;) {
-                // compare-and-swap k -> k: succeeds once chunk k - 1 is done (the word only grows, to k at most
-                // before this item runs); a load-like RMW (add 0, or 0) is turned back into a plain load by the
-                // compiler
-                uint32_t v = 0;
-                if (lane == 0) {
-                    uint32_t expect = k;
-                    __hip_atomic_compare_exchange_strong(done + c, &expect, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    v = expect;  // k on success, else the current count
-                }
-                if (__builtin_amdgcn_readfirstlane(__shfl(v, 0)) >= k) break;
-                __builtin_amdgcn_s_sleep(16);  // ~1k cycles between polls: thousands of polling waves would
-                                               // otherwise crowd the device-scope atomics the producers need
+                uint32_t expect = k;
+                __hip_atomic_compare_exchange_strong(done + c, &expect, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane(expect) >= k) break;
+                __builtin_amdgcn_s_sleep(16);  // ~1k cycles between polls
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: fail the call, never spin on
-                    if (lane == 0) __hip_atomic_fetch_or(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_or(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
@@ -318,7 +313,7 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) __hip_atomic_fetch_max(done + c, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(done + c, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every lane, same word
     }
 }
 
