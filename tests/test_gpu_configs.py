@@ -80,7 +80,7 @@ def test_c5_mixed_batch_full_size():
         print(f"DWPA_FULL_ORACLE: {len(sel)} jobs prefix-checked, {len(jobs)} exact, 0 mismatches")
 
 
-@pytest.mark.parametrize("chunks", ["0"])
+@pytest.mark.parametrize("chunks", ["0", "16", "7"])
 def test_batch_head_tail_split(chunks, monkeypatch):
     """A derive of >= 4 waves per SIMD of unique (ESSID, key) pairs is split: the head (whole waves per SIMD) and
     the tail (the remainder, on the second stream, overlapping the head's verify).  Hits are planted in head slots,
