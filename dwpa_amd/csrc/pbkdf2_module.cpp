@@ -162,8 +162,12 @@ hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t 
     if (e != hipSuccess) return e;
     const uint32_t chains = pbkdf2_chunk_chains(std::min(count, cap));
     if ((e = hipMemsetAsync(ctl, 0, (16 + (size_t)chains) * 4, s)) != hipSuccess) return e;
-    // fewer waves than chains (7/8): item (k, c) is taken about one chunk time after (k - 1, c), so it rarely waits
-    const uint64_t waves = std::max<uint64_t>(1, std::min<uint64_t>(chains - chains / 8, 8 * fn.level_lanes / 64));
+    // fewer waves than chains (DWPA_CHUNK_WAVES sixteenths of them, default 14): item (k, c) is taken about
+    // 16 / DWPA_CHUNK_WAVES chunk times after (k - 1, c), so it rarely waits
+    const char* fe = getenv("DWPA_CHUNK_WAVES");
+    const int frac = fe && *fe ? std::max(1, std::min(16, atoi(fe))) : 14;
+    const uint64_t waves =
+        std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)chains * frac / 16, 8 * fn.level_lanes / 64));
     const uint32_t blocks = (uint32_t)((waves + 3) / 4);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk,
                     (void*)&state, (void*)&ctl, (void*)&nchunks};
