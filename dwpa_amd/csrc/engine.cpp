@@ -679,7 +679,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
         uint32_t* head_flag = (uint32_t*)d.batch.counters.p + 3;  // zeroed with the counters above
         if (chunked) {  // one launch, no tail (DWPA_CHECK_CHUNKS)
             const uint32_t chains = pbkdf2_chunk_chains(nu);
-            RCHK(d.chunk_ctl.ensure((16 + (size_t)chains) * 4));
+            RCHK(d.chunk_ctl.ensure(pbkdf2_chunk_ctl_words(nu) * 4));
             RCHK(d.chunk_state.ensure((size_t)chains * 640 * 4));
             HIPCHK(launch_pbkdf2_ms_chunked(mid, cap, nu, (const uint32_t*)d.salt.p, sref, upmk,
                                             (uint32_t*)d.chunk_state.p, (uint32_t*)d.chunk_ctl.p, nchunks, s));

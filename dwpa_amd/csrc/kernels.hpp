@@ -29,9 +29,10 @@ uint32_t pbkdf2_wave_unit();
 hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                             const uint32_t* sref, uint32_t* pmk, hipStream_t s);
 // the check path's derive as a work queue of iteration chunks (pbkdf2_dev.hpp pbkdf2_body_ms_chunked): ctl holds
-// 16 + pbkdf2_chunk_chains(count) words (ctl[1] != 0 after the launch: a dependency wait ran out), state
-// 640 x pbkdf2_chunk_chains(count) words
+// pbkdf2_chunk_ctl_words(count) words (ctl[1] != 0 after the launch: a queue wait ran out or an entry was bad),
+// state 640 x pbkdf2_chunk_chains(count) words
 uint32_t pbkdf2_chunk_chains(uint32_t count);
+size_t pbkdf2_chunk_ctl_words(uint32_t count);
 hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                     const uint32_t* sref, uint32_t* pmk, uint32_t* state, uint32_t* ctl,
                                     uint32_t nchunks, hipStream_t s);

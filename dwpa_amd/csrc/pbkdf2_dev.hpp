@@ -230,16 +230,18 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
 // The check path's derive as a work queue of iteration chunks (DWPA_CHECK_CHUNKS).  A one-round launch of nu unique
 // PMKs at k.f waves per SIMD leaves the SIMDs that hold a (k+1)-th wave k+1 wave times of work, whatever the
 // schedule ("Where a C5 call goes now").  Here a chain = (64 slots, output block) is cut into
-// nchunks pieces of 4096 / nchunks iterations, U and T carried in `state` between pieces, and the resident waves take
-// (chunk, chain) items chunk-major from one counter: a chain moves from wave to wave (and SIMD to SIMD) at chunk
-// boundaries, so the work of the last 0.f waves spreads over every SIMD instead of landing on a few.
-//   ctl[0] = item counter, ctl[1] = error flag (a dependency wait ran out), ctl[16 + c] = chunks of chain c done.
-// An item (k, c) with k > 0 waits for (k - 1, c), which has a smaller item number, so it was taken earlier by a wave
-// that is running: every wait ends.  The wait is bounded anyway (1 s -> ctl[1] = 1, the host fails the call).  With
-// fewer resident waves than chains, (k - 1, c) was taken about one chunk time before (k, c), so waits are rare.
-// The done words are written and polled with atomic read-modify-writes only.
-// Chunk k's state is published with an agent-scope release (the next chunk may run on another XCD) and read after
-// an agent-scope acquire.
+// nchunks pieces of 4096 / nchunks iterations, U and T carried in `state` between pieces, and the resident waves
+// (fewer than the chains) take pieces from a ready queue: a chain whose piece is done goes back to the queue's
+// tail, so it moves from wave to wave (and SIMD to SIMD) and the work of the last 0.f waves spreads over every SIMD.
+// Pops 0 .. chains-1 are the chains' first pieces; pop i >= chains takes push i - chains, a ring entry
+// {chain | next piece << 20} published with seq = push index + 1 (ring of Q = 2 x chains entries).  With fewer waves
+// than chains the entry a pop needs was pushed a piece time earlier, so pops rarely wait; every wait is for a push
+// of a chain some running wave holds, and it is bounded anyway (1 s -> ctl[1] = 1, the host fails the call).
+//   ctl[0] = pop counter, ctl[1] = error flag, ctl[2] = push counter, ctl[16 ..] = ring entries, then ring seqs.
+// The queue words are written and polled with atomic read-modify-writes (a plain load of a line this XCD's L2
+// already holds may keep returning that copy); state and entries are published with an agent-scope release and
+// read after an agent-scope acquire (a piece may run on another XCD than the one before).  Every lane takes part in
+// the polls and pushes: a lane-0-only atomic inside the item loop made the compiler split the loop by lanes.
 __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
                                                        const uint32_t* __restrict__ pool,
                                                        const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk,
@@ -249,28 +251,31 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
     const uint32_t n = min(count, cap);
     const uint32_t nchains = 2u * ((n + 63u) / 64u);
     const uint32_t nitems = nchains * nchunks;
+    const uint32_t Q = 2u * nchains;
     const size_t S = (size_t)nchains * 64u;  // state word stride
-    uint32_t* done = ctl + 16;
+    uint32_t* ring = ctl + 16;
+    uint32_t* seq = ring + Q;
 #pragma unroll 1
     for (;;) {
         uint32_t item = 0;
         if (lane == 0) item = atomicAdd(ctl, 1u);
         item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
         if (item >= nitems) break;
-        const uint32_t k = item / nchains, c = item - k * nchains;
-        if (k) {
-            // Polled with an atomic read-modify-write: a plain (even agent-scope) load of a line this XCD's L2 already
-            // holds may keep returning that copy, while the RMW is performed where every XCD sees the same word.  A
-            // compare-and-swap k -> k succeeds once chunk k - 1 is done (the word only grows, to k at most before
-            // this item runs); load-like RMWs (add 0, or 0) are turned back into plain loads by the compiler.  Every
-            // lane polls (same address): a lane-0-only atomic inside this loop and at the end of the item loop made
-            // the compiler split the item loop by lanes, and lane 0 stopped taking items.
+        uint32_t c = item, k = 0;
+        if (item >= nchains) {
+            const uint32_t j = item - nchains, slot = j % Q;
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
             for (;;) {
-                uint32_t expect = k;
-                __hip_atomic_compare_exchange_strong(done + c, &expect, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                // compare-and-swap 0 -> 0 reads the word atomically (it is never 0 once pushed); load-like RMWs
+                // (add 0, or 0) are turned back into plain loads by the compiler
+                uint32_t got = 0;
+                __hip_atomic_compare_exchange_strong(seq + slot, &got, 0u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_readfirstlane(expect) >= k) break;
+                got = __builtin_amdgcn_readfirstlane(got);
+                if (got >= j + 1u) {
+                    if (got != j + 1u) __hip_atomic_fetch_or(ctl + 1, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(16);  // ~1k cycles between polls
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: fail the call, never spin on
                     __hip_atomic_fetch_or(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -278,6 +283,13 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            const uint32_t e = __builtin_amdgcn_readfirstlane(ring[slot]);
+            c = e & 0xfffffu;
+            k = e >> 20;
+            if (c >= nchains || k >= nchunks) {  // never expected: a corrupt entry must not index out of bounds
+                __hip_atomic_fetch_or(ctl + 1, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
         }
         const uint32_t blk = c & 1u;
         const uint32_t s = (c >> 1) * 64u + lane;
@@ -312,8 +324,14 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
                 }
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_max(done + c, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every lane, same word
+        if (k + 1 < nchunks) {  // back to the queue: entry, release, then its seq
+            const uint32_t j = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(
+                ctl + 2, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            const uint32_t slot = j % Q;
+            ring[slot] = c | ((k + 1) << 20);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_fetch_max(seq + slot, j + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 

@@ -149,8 +149,10 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
 
 // k_pbkdf2_gfx950_ms_c over `count` unique PMKs: chains = 2 x ceil(count / 64) (64 slots x output block), each
 // cut into `nchunks` pieces; the grid holds min(7/8 of the chains, 8 per SIMD) waves, all resident at once.
-// ctl needs 16 + chains words and state 10 x 64 x chains words; ctl is zeroed here, on the launch's stream.
+// ctl needs pbkdf2_chunk_ctl_words(count) words (16 + a ring of 2 x chains entries and seqs) and state
+// 10 x 64 x chains words; ctl is zeroed here, on the launch's stream.
 uint32_t pbkdf2_chunk_chains(uint32_t count) { return 2u * ((count + 63u) / 64u); }
+size_t pbkdf2_chunk_ctl_words(uint32_t count) { return 16 + 4 * (size_t)pbkdf2_chunk_chains(count); }
 
 hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                     const uint32_t* sref, uint32_t* pmk, uint32_t* state, uint32_t* ctl,
@@ -161,7 +163,7 @@ hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t 
     hipError_t e = tuned_functions(&fn);
     if (e != hipSuccess) return e;
     const uint32_t chains = pbkdf2_chunk_chains(std::min(count, cap));
-    if ((e = hipMemsetAsync(ctl, 0, (16 + (size_t)chains) * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(ctl, 0, pbkdf2_chunk_ctl_words(std::min(count, cap)) * 4, s)) != hipSuccess) return e;
     // fewer waves than chains (DWPA_CHUNK_WAVES sixteenths of them, default 14): item (k, c) is taken about
     // 16 / DWPA_CHUNK_WAVES chunk times after (k - 1, c), so it rarely waits
     const char* fe = getenv("DWPA_CHUNK_WAVES");
