@@ -683,7 +683,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
             RCHK(d.chunk_state.ensure((size_t)chains * 640 * 4));
             HIPCHK(launch_pbkdf2_ms_chunked(mid, cap, nu, (const uint32_t*)d.salt.p, sref, upmk,
                                             (uint32_t*)d.chunk_state.p, (uint32_t*)d.chunk_ctl.p, nchunks, s));
-            d.chunk_err = (const uint32_t*)d.chunk_ctl.p + 1;
+            d.chunk_err = (const uint32_t*)d.chunk_ctl.p;
         } else {
             if (nh < nu) {  // the tail first, beside the head (priority 0 until the head has ended: pbkdf2_lane_tail)
                 HIPCHK(hipEventRecord(d.prep_done, s));

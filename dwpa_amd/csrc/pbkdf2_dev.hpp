@@ -232,16 +232,27 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
 // schedule ("Where a C5 call goes now").  Here a chain = (64 slots, output block) is cut into
 // nchunks pieces of 4096 / nchunks iterations, U and T carried in `state` between pieces, and the resident waves
 // (fewer than the chains) take pieces from a ready queue: a chain whose piece is done goes back to the queue's
-// tail, so it moves from wave to wave (and SIMD to SIMD) and the work of the last 0.f waves spreads over every SIMD.
-// Pops 0 .. chains-1 are the chains' first pieces; pop i >= chains takes push i - chains, a ring entry
-// {chain | next piece << 20} published with seq = push index + 1 (ring of Q = 2 x chains entries).  With fewer waves
-// than chains the entry a pop needs was pushed a piece time earlier, so pops rarely wait; every wait is for a push
-// of a chain some running wave holds, and it is bounded anyway (1 s -> ctl[1] = 1, the host fails the call).
-//   ctl[0] = pop counter, ctl[1] = error flag, ctl[2] = push counter, ctl[16 ..] = ring entries, then ring seqs.
-// The queue words are written and polled with atomic read-modify-writes (a plain load of a line this XCD's L2
-// already holds may keep returning that copy); state and entries are published with an agent-scope release and
-// read after an agent-scope acquire (a piece may run on another XCD than the one before).  Every lane takes part in
-// the polls and pushes: a lane-0-only atomic inside the item loop made the compiler split the loop by lanes.
+// tail, so it moves from wave to wave and SIMD to SIMD and the work of the last 0.f waves spreads over the XCD.
+//
+// One queue per XCD (chain c belongs to XCD c % 8, served by the waves running there): a chain's state then moves
+// only between CUs that share one L2, so a piece publishes it by waiting for its stores (s_waitcnt: they have reached
+// the L2, through the write-through L1) and the next piece reads it with agent-scope loads, which miss the L1.  An
+// agent-scope release/acquire instead writes back / invalidates the whole L2 per piece (measured: pieces of 64
+// iterations took the derive from 49 to 71 ms).  Queue words are written and read with atomic read-modify-writes
+// only (a plain load of a line the L2 already holds may keep returning that copy).  Every lane takes part in the
+// queue atomics: a lane-0-only atomic inside the item loop made the compiler split the loop by lanes.
+//
+// Per XCD x: pops 0 .. m_x - 1 are the first pieces of its m_x chains; pop i >= m_x takes push i - m_x, a ring entry
+// {chain | next piece << 20} (never 0) with seq = push index + 1.  Every wait is for a push of a chain that some
+// running wave holds, and it is bounded anyway (1 s -> error flag, the host fails the call).
+//   ctl[0] = error flags; ctl[16 + 2x] / [17 + 2x] = XCD x's pop / push counters; ctl[64 + x * 2Q ..] = its ring
+//   (Q entries, then Q seqs), Q = 2 * ceil(chains / 8) + 2.
+__device__ __forceinline__ uint32_t cas_read(uint32_t* p) {  // atomic read of a word (compare-and-swap 0 -> 0)
+    uint32_t got = 0;
+    __hip_atomic_compare_exchange_strong(p, &got, 0u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return got;
+}
+
 __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
                                                        const uint32_t* __restrict__ pool,
                                                        const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk,
@@ -250,46 +261,44 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t n = min(count, cap);
     const uint32_t nchains = 2u * ((n + 63u) / 64u);
-    const uint32_t nitems = nchains * nchunks;
-    const uint32_t Q = 2u * nchains;
+    const uint32_t Q = 2u * ((nchains + 7u) / 8u) + 2u;
     const size_t S = (size_t)nchains * 64u;  // state word stride
-    uint32_t* ring = ctl + 16;
+    const uint32_t x = (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u) % 8u;  // HW_REG_XCC_ID
+    const uint32_t mx = nchains > x ? (nchains - x + 7u) / 8u : 0u;
+    const uint32_t nitems = mx * nchunks;
+    uint32_t* pops = ctl + 16 + 2 * x;
+    uint32_t* pushes = pops + 1;
+    uint32_t* ring = ctl + 64 + (size_t)x * 2 * Q;
     uint32_t* seq = ring + Q;
 #pragma unroll 1
     for (;;) {
-        uint32_t item = 0;
-        if (lane == 0) item = atomicAdd(ctl, 1u);
-        item = __builtin_amdgcn_readfirstlane(__shfl(item, 0));
+        const uint32_t item = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_fetch_add(pops, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (item >= nitems) break;
-        uint32_t c = item, k = 0;
-        if (item >= nchains) {
-            const uint32_t j = item - nchains, slot = j % Q;
+        uint32_t c = x + 8u * item, k = 0;
+        if (item >= mx) {
+            const uint32_t j = item - mx, slot = j % Q;
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
             for (;;) {
-                // compare-and-swap 0 -> 0 reads the word atomically (it is never 0 once pushed); load-like RMWs
-                // (add 0, or 0) are turned back into plain loads by the compiler
-                uint32_t got = 0;
-                __hip_atomic_compare_exchange_strong(seq + slot, &got, 0u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-                got = __builtin_amdgcn_readfirstlane(got);
+                const uint32_t got = __builtin_amdgcn_readfirstlane(cas_read(seq + slot));
                 if (got >= j + 1u) {
-                    if (got != j + 1u) __hip_atomic_fetch_or(ctl + 1, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (got != j + 1u) __hip_atomic_fetch_or(ctl, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(16);  // ~1k cycles between polls
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: fail the call, never spin on
-                    __hip_atomic_fetch_or(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_fetch_or(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            const uint32_t e = __builtin_amdgcn_readfirstlane(ring[slot]);
+            const uint32_t e = __builtin_amdgcn_readfirstlane(cas_read(ring + slot));
             c = e & 0xfffffu;
             k = e >> 20;
-            if (c >= nchains || k >= nchunks) {  // never expected: a corrupt entry must not index out of bounds
-                __hip_atomic_fetch_or(ctl + 1, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c >= nchains || c % 8u != x || k == 0 || k >= nchunks) {  // never expected: no out-of-bounds use
+                __hip_atomic_fetch_or(ctl, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 continue;
             }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the state loads stay after the queue reads
         }
         const uint32_t blk = c & 1u;
         const uint32_t s = (c >> 1) * 64u + lane;
@@ -308,9 +317,9 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
                 it = 1;
             } else {
 #pragma unroll
-                for (int w = 0; w < 5; w++) {
-                    u[w] = state[w * S + si];
-                    t[w] = state[(5 + w) * S + si];
+                for (int w = 0; w < 5; w++) {  // L1-missing loads: the last piece may have run on another CU
+                    u[w] = __hip_atomic_load(state + w * S + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    t[w] = __hip_atomic_load(state + (5 + w) * S + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             pbkdf2_iterate(hi, ho, u, t, it, end);
@@ -324,12 +333,14 @@ __device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restric
                 }
             }
         }
-        if (k + 1 < nchunks) {  // back to the queue: entry, release, then its seq
-            const uint32_t j = __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(
-                ctl + 2, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (k + 1 < nchunks) {  // back to the queue: the state's stores complete, then the entry, then its seq
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint32_t j = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_fetch_add(pushes, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             const uint32_t slot = j % Q;
-            ring[slot] = c | ((k + 1) << 20);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            __hip_atomic_exchange(ring + slot, c | ((k + 1) << 20), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_waitcnt(0);
             __hip_atomic_fetch_max(seq + slot, j + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }

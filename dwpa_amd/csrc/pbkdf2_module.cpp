@@ -149,10 +149,13 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
 
 // k_pbkdf2_gfx950_ms_c over `count` unique PMKs: chains = 2 x ceil(count / 64) (64 slots x output block), each
 // cut into `nchunks` pieces; the grid holds min(7/8 of the chains, 8 per SIMD) waves, all resident at once.
-// ctl needs pbkdf2_chunk_ctl_words(count) words (16 + a ring of 2 x chains entries and seqs) and state
+// ctl needs pbkdf2_chunk_ctl_words(count) words (counters + one ring per XCD) and state
 // 10 x 64 x chains words; ctl is zeroed here, on the launch's stream.
 uint32_t pbkdf2_chunk_chains(uint32_t count) { return 2u * ((count + 63u) / 64u); }
-size_t pbkdf2_chunk_ctl_words(uint32_t count) { return 16 + 4 * (size_t)pbkdf2_chunk_chains(count); }
+size_t pbkdf2_chunk_ctl_words(uint32_t count) {
+    const size_t q = 2 * (((size_t)pbkdf2_chunk_chains(count) + 7) / 8) + 2;  // ring entries per XCD
+    return 64 + 8 * 2 * q;
+}
 
 hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                     const uint32_t* sref, uint32_t* pmk, uint32_t* state, uint32_t* ctl,
