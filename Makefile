@@ -27,7 +27,7 @@ build/pbkdf2/pbkdf2_gfx950.s: $(SRC)/pbkdf2_gfx950.hip $(SRC)/pbkdf2_dev.hpp $(S
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 --cuda-device-only -S $< -o $@
 
 build/pbkdf2/pbkdf2_issue.s: build/pbkdf2/pbkdf2_gfx950.s $(SRC)/gen/issue_pass.py
-	python3 $(SRC)/gen/issue_pass.py $< $@ k_pbkdf2_gfx950+k_pbkdf2_gfx950_ms+k_pbkdf2_gfx950_mg+k_pbkdf2_gfx950_p+k_pbkdf2_gfx950_ms_p+k_pbkdf2_gfx950_mg_p+k_pbkdf2_gfx950_q+k_pbkdf2_gfx950_mg_q+k_pbkdf2_gfx950_ms_c $(ISSUE_RULE)
+	python3 $(SRC)/gen/issue_pass.py $< $@ k_pbkdf2_gfx950+k_pbkdf2_gfx950_ms+k_pbkdf2_gfx950_mg+k_pbkdf2_gfx950_p+k_pbkdf2_gfx950_ms_p+k_pbkdf2_gfx950_mg_p+k_pbkdf2_gfx950_q+k_pbkdf2_gfx950_mg_q $(ISSUE_RULE)
 
 build/pbkdf2/pbkdf2_gfx950.hsaco: build/pbkdf2/pbkdf2_issue.s
 	$(LLVM)/clang -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c $< -o build/pbkdf2/pbkdf2_issue.o

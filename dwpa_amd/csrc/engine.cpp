@@ -205,8 +205,6 @@ struct Device {
     DevBuf koff, klen, kbytes, uslot;  // check path: the call's key bytes by slot, unique key -> its first slot
     DevBuf keys, keys_tail;        // check path: per-key EapolKey scratch of the attempt-parallel verify
     DevBuf first_hit;              // check path: per line (= job), the smallest slot with a hit so far (~0u: none)
-    DevBuf chunk_state, chunk_ctl;  // check path: the chunked derive's U/T state and its queue control words
-    const uint32_t* chunk_err = nullptr;  // the current derive's error word (chunked derive), else nullptr
     DevBuf upmk, sref, src, cpmk;  // run_slots: unique-pair PMKs, their salt refs, slot -> PMK source
     SlotTable slots;               // check path: the call's slots (capacity kept between calls)
     CheckScratch cs;               // check path: host-phase scratch
@@ -510,11 +508,6 @@ static bool check_split_enabled() {
 // (< one wave per SIMD, the latency-bound plain kernel, priority 0) is launched beside it on d.tail and takes only
 // the issue slots the head leaves, then finishes alone while the head's verify runs.  From 2 whole waves per SIMD
 // up (the head's PRIO kernel; below that both kernels are lone-wave plain kernels) the split pays.
-// DWPA_CHECK_CHUNKS=K (1..256, 0 = off): from 2 whole waves per SIMD of unique PMKs up, the check path derives them
-// in one work-queue launch of K-iteration-chunk items (k_pbkdf2_gfx950_ms_c, pbkdf2_dev.hpp) instead of the head/tail
-// split.  Read on every derive (tests switch it within one process).
-static uint32_t check_chunks_knob() { return (uint32_t)env_int("DWPA_CHECK_CHUNKS", 0, 0, 256); }
-
 static uint32_t head_pmks(uint32_t nu) {
     const uint32_t unit = pbkdf2_wave_unit();
     if (!check_split_enabled() || !unit || nu < 2 * unit) return nu;
@@ -644,9 +637,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
     RCHK(d.upmk.ensure((size_t)PMK_WORDS * d.batch.cap * 4));
     // head = unique PMKs [0, nh); unique ids are numbered in first-occurrence slot order, so slots [0, split) only
     // read head PMKs (or caller PMKs) and the slots after it wait for the tail
-    const uint32_t nchunks = check_chunks_knob();
-    const bool chunked = nchunks && pbkdf2_wave_unit() && nu >= 2 * pbkdf2_wave_unit();
-    const uint32_t nh = chunked ? nu : head_pmks(nu);
+    const uint32_t nh = head_pmks(nu);
     st.split = n;
     if (nh < nu)
         for (uint32_t i = 0; i < n; i++)
@@ -677,23 +668,14 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
         std::lock_guard<std::mutex> fl(f.mu);
         if (head_fence_knob() && f.last && f.last != d.head_end) HIPCHK(hipStreamWaitEvent(s, f.last, 0));
         uint32_t* head_flag = (uint32_t*)d.batch.counters.p + 3;  // zeroed with the counters above
-        if (chunked) {  // one launch, no tail (DWPA_CHECK_CHUNKS)
-            const uint32_t chains = pbkdf2_chunk_chains(nu);
-            RCHK(d.chunk_ctl.ensure(pbkdf2_chunk_ctl_words(nu) * 4));
-            RCHK(d.chunk_state.ensure((size_t)chains * 640 * 4));
-            HIPCHK(launch_pbkdf2_ms_chunked(mid, cap, nu, (const uint32_t*)d.salt.p, sref, upmk,
-                                            (uint32_t*)d.chunk_state.p, (uint32_t*)d.chunk_ctl.p, nchunks, s));
-            d.chunk_err = (const uint32_t*)d.chunk_ctl.p;
-        } else {
-            if (nh < nu) {  // the tail first, beside the head (priority 0 until the head has ended: pbkdf2_lane_tail)
-                HIPCHK(hipEventRecord(d.prep_done, s));
-                HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
-                HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh,
-                                             upmk + nh, head_flag, (uint32_t)tail_prio_knob(), d.tail));
-            }
-            HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
-            if (nh < nu) HIPCHK(launch_set_flag(head_flag, s));
+        if (nh < nu) {  // the tail first, beside the head (priority 0 until the head has ended: pbkdf2_lane_tail)
+            HIPCHK(hipEventRecord(d.prep_done, s));
+            HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
+            HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh,
+                                         head_flag, (uint32_t)tail_prio_knob(), d.tail));
         }
+        HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
+        if (nh < nu) HIPCHK(launch_set_flag(head_flag, s));
         HIPCHK(hipEventRecord(d.head_end, s));
         f.last = d.head_end;
     }
@@ -859,12 +841,9 @@ static int collect_hits(Device& d, std::vector<HitDev>& hits_out) {
     RCHK(join_tail(d));
     const uint32_t* hitcnt = (const uint32_t*)d.batch.counters.p + 1;
     RCHK(d.hits_host.ensure(16 + (size_t)d.batch.hitcap * sizeof(HitDev)));
-    HIPCHK(launch_hits_out(hitcnt, (const HitDev*)d.batch.hits.p, d.batch.hitcap, (uint32_t*)d.hits_host.dev,
-                           d.chunk_err, s));
+    HIPCHK(launch_hits_out(hitcnt, (const HitDev*)d.batch.hits.p, d.batch.hitcap, (uint32_t*)d.hits_host.dev, s));
     HIPCHK(hipStreamSynchronize(s));
     tr.mark("  device wait");
-    d.chunk_err = nullptr;
-    if (((volatile const uint32_t*)d.hits_host.p)[1]) return DWPA_E_HIP;  // the chunked derive's wait ran out
     const uint32_t nh = *(volatile const uint32_t*)d.hits_host.p;
     if (nh > d.batch.hitcap) return DWPA_E_OVERFLOW;
     size_t old = hits_out.size();
@@ -1168,12 +1147,7 @@ static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essi
         RCHK(join_tail(d));
         std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
         HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, d.stream));
-        uint32_t chunk_err = 0;
-        if (d.chunk_err)
-            HIPCHK(hipMemcpyAsync(&chunk_err, d.chunk_err, 4, hipMemcpyDeviceToHost, d.stream));
         HIPCHK(hipStreamSynchronize(d.stream));
-        d.chunk_err = nullptr;
-        if (chunk_err) return DWPA_E_HIP;  // the chunked derive's wait ran out
         for (size_t i = 0; i < e - b; i++) {
             uint32_t pw[8];
             for (int k = 0; k < 8; k++) pw[k] = w[(size_t)k * d.batch.cap + i];
@@ -1530,7 +1504,7 @@ void dwpa_shutdown(void) {
         (void)hipSetDevice(d->id);
         (void)hipDeviceSynchronize();
         for (DevBuf* b : {&d->lines, &d->atts, &d->pool, &d->segs, &d->segs_tail, &d->keys, &d->keys_tail, &d->salt,
-                          &d->first_hit, &d->chunk_state, &d->chunk_ctl,
+                          &d->first_hit,
                           &d->koff, &d->klen, &d->kbytes, &d->uslot, &d->upmk, &d->sref, &d->src, &d->cpmk,
                           &d->batch.mid, &d->batch.pmk, &d->batch.ids, &d->batch.hits, &d->batch.counters})
             b->release();

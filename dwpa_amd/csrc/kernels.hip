@@ -170,12 +170,12 @@ __global__ __launch_bounds__(256) void k_gather_pmk(const uint32_t* __restrict__
     }
 }
 
-// Hit count and hits -> host-mapped pinned memory (word 0 = count, word 1 = *err or 0, the min(count, hitcap) HitDev
-// records from byte 16): the check path reads its results without a device-to-host copy, whose runtime blit kernel would run at wave
+// Hit count and hits -> host-mapped pinned memory (word 0 = count, the min(count, hitcap) HitDev records from byte
+// 16): the check path reads its results without a device-to-host copy, whose runtime blit kernel would run at wave
 // priority 0 and starve beside another call's PBKDF2 head.
 __global__ __launch_bounds__(256) void k_hits_out(const uint32_t* __restrict__ hitcnt,
                                                   const HitDev* __restrict__ hits, uint32_t hitcap,
-                                                  uint32_t* __restrict__ out, const uint32_t* __restrict__ err) {
+                                                  uint32_t* __restrict__ out) {
     __builtin_amdgcn_s_setprio(3);
     const uint32_t n = min(*hitcnt, hitcap);
     constexpr uint32_t W = sizeof(HitDev) / 4;
@@ -183,10 +183,7 @@ __global__ __launch_bounds__(256) void k_hits_out(const uint32_t* __restrict__ h
     const uint32_t total = n * W;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
         out[4 + i] = src[i];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        out[0] = *hitcnt;
-        out[1] = err ? *err : 0u;  // word 1: a derive's error flag (the chunked PBKDF2's ctl[1])
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = *hitcnt;
 }
 
 // Caller-supplied PMK for one slot (check_key_m22000's $pmk argument, common.php:157,178).
@@ -730,10 +727,10 @@ hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t
 }
 
 hipError_t launch_hits_out(const uint32_t* hitcnt, const HitDev* hits, uint32_t hitcap, uint32_t* out,
-                           const uint32_t* err, hipStream_t s) {
+                           hipStream_t s) {
     const uint32_t blocks = cdiv((uint64_t)hitcap * (sizeof(HitDev) / 4), 256);
     hipLaunchKernelGGL(k_hits_out, dim3(blocks < 1 ? 1 : blocks > 64 ? 64 : blocks), dim3(256), 0, s, hitcnt, hits,
-                       hitcap, out, err);
+                       hitcap, out);
     return hipGetLastError();
 }
 

@@ -28,14 +28,6 @@ uint32_t pbkdf2_wave_unit();
 // many ESSIDs per launch: slot s uses the salt entry pool + sref[s] = {nsalt, [2][nsalt][16] words}
 hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                             const uint32_t* sref, uint32_t* pmk, hipStream_t s);
-// the check path's derive as a work queue of iteration chunks (pbkdf2_dev.hpp pbkdf2_body_ms_chunked): ctl holds
-// pbkdf2_chunk_ctl_words(count) words (ctl[1] != 0 after the launch: a queue wait ran out or an entry was bad),
-// state 640 x pbkdf2_chunk_chains(count) words
-uint32_t pbkdf2_chunk_chains(uint32_t count);
-size_t pbkdf2_chunk_ctl_words(uint32_t count);
-hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                                    const uint32_t* sref, uint32_t* pmk, uint32_t* state, uint32_t* ctl,
-                                    uint32_t nchunks, hipStream_t s);
 hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                   const uint32_t* sref, uint32_t* pmk, hipStream_t s);
 // attempt-parallel verification of EAPOL lists with >= ATT_PARALLEL_MIN attempts: lane = (key, attempt) item,
@@ -72,7 +64,7 @@ hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t
                              uint32_t n, uint32_t* pmk, uint32_t cap, hipStream_t s);
 // out: host-mapped, >= 16 + hitcap * sizeof(HitDev) bytes (word 0 = hit count, HitDev records from byte 16)
 hipError_t launch_hits_out(const uint32_t* hitcnt, const HitDev* hits, uint32_t hitcap, uint32_t* out,
-                           const uint32_t* err, hipStream_t s);
+                           hipStream_t s);
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s);
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,

@@ -117,34 +117,6 @@ __device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uin
     }
 }
 
-// The first iteration of a lane's output block (the salt blocks and U_1) and the PBKDF2 loop over [it, end), for
-// kernels that cut the 4096 iterations into pieces (pbkdf2_body_ms_chunked).
-__device__ __forceinline__ void pbkdf2_u1(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
-                                          uint32_t nsalt, uint32_t u[5]) {
-    uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
-    for (uint32_t b = 0; b < nsalt; b++) {
-        uint32_t m[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) m[j] = sb[b * 16 + j];
-        sha1_compress(st, m);
-    }
-    sha1_84(sha1_mid(ho), st, u);
-}
-
-__device__ __forceinline__ void pbkdf2_iterate(const uint32_t hi[5], const uint32_t ho[5], uint32_t u[5],
-                                               uint32_t t[5], uint32_t it, uint32_t end) {
-    const Sha1Mid MI = sha1_mid(hi);
-    const Sha1Mid MO = sha1_mid(ho);
-    uint32_t x[5];
-#pragma unroll 1
-    for (; it < end; it++) {
-        sha1_84(MI, u, x);
-        sha1_84(MO, x, u);
-#pragma unroll
-        for (int k = 0; k < 5; k++) t[k] ^= u[k];
-    }
-}
-
 __device__ __forceinline__ void load_mid(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t s, uint32_t hi[5],
                                          uint32_t ho[5]) {
 #pragma unroll
@@ -225,125 +197,6 @@ __device__ __forceinline__ void pbkdf2_body_ms(const uint32_t* __restrict__ mid,
     const uint32_t nsalt = e[0];
     pbkdf2_lane<PRIO>(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t);
     store_block(pmk, cap, s, blk, t);
-}
-
-// The check path's derive as a work queue of iteration chunks (DWPA_CHECK_CHUNKS).  A one-round launch of nu unique
-// PMKs at k.f waves per SIMD leaves the SIMDs that hold a (k+1)-th wave k+1 wave times of work, whatever the
-// schedule ("Where a C5 call goes now").  Here a chain = (64 slots, output block) is cut into
-// nchunks pieces of 4096 / nchunks iterations, U and T carried in `state` between pieces, and the resident waves
-// (fewer than the chains) take pieces from a ready queue: a chain whose piece is done goes back to the queue's
-// tail, so it moves from wave to wave and SIMD to SIMD and the work of the last 0.f waves spreads over the XCD.
-//
-// One queue per XCD (chain c belongs to XCD c % 8, served by the waves running there): a chain's state then moves
-// only between CUs that share one L2, so a piece publishes it by waiting for its stores (s_waitcnt: they have reached
-// the L2, through the write-through L1) and the next piece reads it with agent-scope loads, which miss the L1.  An
-// agent-scope release/acquire instead writes back / invalidates the whole L2 per piece (measured: pieces of 64
-// iterations took the derive from 49 to 71 ms).  Queue words are written and read with atomic read-modify-writes
-// only (a plain load of a line the L2 already holds may keep returning that copy).  Every lane takes part in the
-// queue atomics: a lane-0-only atomic inside the item loop made the compiler split the loop by lanes.
-//
-// Per XCD x: pops 0 .. m_x - 1 are the first pieces of its m_x chains; pop i >= m_x takes push i - m_x, a ring entry
-// {chain | next piece << 20} (never 0) with seq = push index + 1.  Every wait is for a push of a chain that some
-// running wave holds, and it is bounded anyway (1 s -> error flag, the host fails the call).
-//   ctl[0] = error flags; ctl[16 + 2x] / [17 + 2x] = XCD x's pop / push counters; ctl[64 + x * 2Q ..] = its ring
-//   (Q entries, then Q seqs), Q = 2 * ceil(chains / 8) + 2.
-__device__ __forceinline__ uint32_t cas_read(uint32_t* p) {  // atomic read of a word (compare-and-swap 0 -> 0)
-    uint32_t got = 0;
-    __hip_atomic_compare_exchange_strong(p, &got, 0u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return got;
-}
-
-__device__ __forceinline__ void pbkdf2_body_ms_chunked(const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count,
-                                                       const uint32_t* __restrict__ pool,
-                                                       const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk,
-                                                       uint32_t* __restrict__ state, uint32_t* __restrict__ ctl,
-                                                       uint32_t nchunks) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t n = min(count, cap);
-    const uint32_t nchains = 2u * ((n + 63u) / 64u);
-    const uint32_t Q = 2u * ((nchains + 7u) / 8u) + 2u;
-    const size_t S = (size_t)nchains * 64u;  // state word stride
-    const uint32_t x = (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u) % 8u;  // HW_REG_XCC_ID
-    const uint32_t mx = nchains > x ? (nchains - x + 7u) / 8u : 0u;
-    const uint32_t nitems = mx * nchunks;
-    uint32_t* pops = ctl + 16 + 2 * x;
-    uint32_t* pushes = pops + 1;
-    uint32_t* ring = ctl + 64 + (size_t)x * 2 * Q;
-    uint32_t* seq = ring + Q;
-#pragma unroll 1
-    for (;;) {
-        const uint32_t item = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_fetch_add(pops, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (item >= nitems) break;
-        uint32_t c = x + 8u * item, k = 0;
-        if (item >= mx) {
-            const uint32_t j = item - mx, slot = j % Q;
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-            for (;;) {
-                const uint32_t got = __builtin_amdgcn_readfirstlane(cas_read(seq + slot));
-                if (got >= j + 1u) {
-                    if (got != j + 1u) __hip_atomic_fetch_or(ctl, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(16);  // ~1k cycles between polls
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {  // 1 s: fail the call, never spin on
-                    __hip_atomic_fetch_or(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-            }
-            const uint32_t e = __builtin_amdgcn_readfirstlane(cas_read(ring + slot));
-            c = e & 0xfffffu;
-            k = e >> 20;
-            if (c >= nchains || c % 8u != x || k == 0 || k >= nchunks) {  // never expected: no out-of-bounds use
-                __hip_atomic_fetch_or(ctl, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                continue;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the state loads stay after the queue reads
-        }
-        const uint32_t blk = c & 1u;
-        const uint32_t s = (c >> 1) * 64u + lane;
-        const size_t si = (size_t)c * 64u + lane;
-        if (s < n) {
-            uint32_t hi[5], ho[5], u[5], t[5];
-            load_mid(mid, cap, s, hi, ho);
-            uint32_t it = 4096u * k / nchunks;
-            const uint32_t end = 4096u * (k + 1) / nchunks;
-            if (k == 0) {
-                const uint32_t* e = pool + sref[s];
-                const uint32_t nsalt = e[0];
-                pbkdf2_u1(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, u);
-#pragma unroll
-                for (int w = 0; w < 5; w++) t[w] = u[w];
-                it = 1;
-            } else {
-#pragma unroll
-                for (int w = 0; w < 5; w++) {  // L1-missing loads: the last piece may have run on another CU
-                    u[w] = __hip_atomic_load(state + w * S + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    t[w] = __hip_atomic_load(state + (5 + w) * S + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            pbkdf2_iterate(hi, ho, u, t, it, end);
-            if (k + 1 == nchunks) {
-                store_block(pmk, cap, s, blk, t);
-            } else {
-#pragma unroll
-                for (int w = 0; w < 5; w++) {
-                    state[w * S + si] = u[w];
-                    state[(5 + w) * S + si] = t[w];
-                }
-            }
-        }
-        if (k + 1 < nchunks) {  // back to the queue: the state's stores complete, then the entry, then its seq
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_s_waitcnt(0);
-            const uint32_t j = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_fetch_add(pushes, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            const uint32_t slot = j % Q;
-            __hip_atomic_exchange(ring + slot, c | ((k + 1) << 20), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_s_waitcnt(0);
-            __hip_atomic_fetch_max(seq + slot, j + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // Many ESSID groups x one candidate batch in one launch (scan work units with many ESSIDs):

@@ -52,14 +52,6 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     dwpa::pbkdf2_body_mg<true>(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride);
 }
 
-// The check path's derive as a work queue of iteration chunks (pbkdf2_dev.hpp pbkdf2_body_ms_chunked).
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_ms_c(
-    const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
-    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, uint32_t* __restrict__ state,
-    uint32_t* __restrict__ ctl, uint32_t nchunks) {
-    dwpa::pbkdf2_body_ms_chunked(mid, cap, count, pool, sref, pmk, state, ctl, nchunks);
-}
-
 // Work-queue variant of k_pbkdf2_gfx950 (pbkdf2_dev.hpp pbkdf2_body_queue): XCD-balanced multi-round launches.
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_gfx950_q(
     const uint32_t* __restrict__ mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* __restrict__ counter,

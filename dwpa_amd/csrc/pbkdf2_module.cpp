@@ -21,7 +21,6 @@ struct Fns {
     hipFunction_t one, ms, mg;  // k_pbkdf2_gfx950 (one ESSID), _ms (per-slot salt), _mg (ESSID groups x batch)
     hipFunction_t one_p, ms_p, mg_p;  // the same with progress-ordered wave priority (pbkdf2_dev.hpp PRIO)
     hipFunction_t one_q, mg_q;        // the one-ESSID and group kernels as work queues (pbkdf2_dev.hpp *_queue)
-    hipFunction_t ms_c;               // the check path's derive as a queue of iteration chunks (*_ms_chunked)
     uint64_t level_lanes;       // lanes that give every SIMD of the device one wave: CUs x 4 SIMDs x 64
 };
 static std::mutex g_mod_mu;
@@ -83,7 +82,6 @@ static hipError_t tuned_functions(Fns* fn) {
     if ((e = hipModuleGetFunction(&fn->mg_p, mod, "k_pbkdf2_gfx950_mg_p")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->one_q, mod, "k_pbkdf2_gfx950_q")) != hipSuccess) return e;
     if ((e = hipModuleGetFunction(&fn->mg_q, mod, "k_pbkdf2_gfx950_mg_q")) != hipSuccess) return e;
-    if ((e = hipModuleGetFunction(&fn->ms_c, mod, "k_pbkdf2_gfx950_ms_c")) != hipSuccess) return e;
     int cus = 0;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
     fn->level_lanes = (uint64_t)(cus > 0 ? cus : 256) * 4 * 64;
@@ -145,38 +143,6 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
     const uint32_t wg = wg_size();
     return hipModuleLaunchKernel(use_prio(fn, std::min(count, cap)) ? fn.ms_p : fn.ms, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args,
                                  nullptr);
-}
-
-// k_pbkdf2_gfx950_ms_c over `count` unique PMKs: chains = 2 x ceil(count / 64) (64 slots x output block), each
-// cut into `nchunks` pieces; the grid holds min(7/8 of the chains, 8 per SIMD) waves, all resident at once.
-// ctl needs pbkdf2_chunk_ctl_words(count) words (counters + one ring per XCD) and state
-// 10 x 64 x chains words; ctl is zeroed here, on the launch's stream.
-uint32_t pbkdf2_chunk_chains(uint32_t count) { return 2u * ((count + 63u) / 64u); }
-size_t pbkdf2_chunk_ctl_words(uint32_t count) {
-    const size_t q = 2 * (((size_t)pbkdf2_chunk_chains(count) + 7) / 8) + 2;  // ring entries per XCD
-    return 64 + 8 * 2 * q;
-}
-
-hipError_t launch_pbkdf2_ms_chunked(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                                    const uint32_t* sref, uint32_t* pmk, uint32_t* state, uint32_t* ctl,
-                                    uint32_t nchunks, hipStream_t s) {
-    if (count == 0) return hipSuccess;
-    if (nchunks < 1 || nchunks > 4096) return hipErrorInvalidValue;
-    Fns fn;
-    hipError_t e = tuned_functions(&fn);
-    if (e != hipSuccess) return e;
-    const uint32_t chains = pbkdf2_chunk_chains(std::min(count, cap));
-    if ((e = hipMemsetAsync(ctl, 0, pbkdf2_chunk_ctl_words(std::min(count, cap)) * 4, s)) != hipSuccess) return e;
-    // fewer waves than chains (DWPA_CHUNK_WAVES sixteenths of them, default 14): item (k, c) is taken about
-    // 16 / DWPA_CHUNK_WAVES chunk times after (k - 1, c), so it rarely waits
-    const char* fe = getenv("DWPA_CHUNK_WAVES");
-    const int frac = fe && *fe ? std::max(1, std::min(16, atoi(fe))) : 14;
-    const uint64_t waves =
-        std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)chains * frac / 16, 8 * fn.level_lanes / 64));
-    const uint32_t blocks = (uint32_t)((waves + 3) / 4);
-    void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk,
-                    (void*)&state, (void*)&ctl, (void*)&nchunks};
-    return hipModuleLaunchKernel(fn.ms_c, blocks, 1, 1, 256, 1, 1, 0, s, args, nullptr);
 }
 
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,

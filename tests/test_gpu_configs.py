@@ -80,16 +80,12 @@ def test_c5_mixed_batch_full_size():
         print(f"DWPA_FULL_ORACLE: {len(sel)} jobs prefix-checked, {len(jobs)} exact, 0 mismatches")
 
 
-@pytest.mark.parametrize("chunks", ["0", "16", "7"])
-def test_batch_head_tail_split(chunks, monkeypatch):
+def test_batch_head_tail_split():
     """A derive of >= 4 waves per SIMD of unique (ESSID, key) pairs is split: the head (whole waves per SIMD) and
     the tail (the remainder, on the second stream, overlapping the head's verify).  Hits are planted in head slots,
     in tail slots that derive a tail PMK, and in tail slots that re-use a head PMK (same ESSID, later job), and
-    re-derived by the oracle from the winning key alone; the random keys around them never match.  chunks: the
-    same derive as one work queue of iteration chunks instead (DWPA_CHECK_CHUNKS; 7 does not divide 4096, so the
-    chunks differ in length)."""
+    re-derived by the oracle from the winning key alone; the random keys around them never match."""
     import random
-    monkeypatch.setenv("DWPA_CHECK_CHUNKS", chunks)
     rng = random.Random(91)
     n_per = 36000  # 4 ESSIDs x 36,000 unique keys = 144,000 > 4 x 32,768 (MI355X: 256 CUs x 4 SIMDs x 64 / 2)
     nets = [S.random_net(rng, essid_len=9 + e) for e in range(4)]
