@@ -490,7 +490,7 @@ def main():
         dist.init_process_group("gloo")
 
     import dwpa_amd
-    from dwpa_amd import synth as S
+    from tests import synth as S
     from dwpa_amd.device import Dictionary, Event, Stream
     from dwpa_amd.shard import reduce_timing, weak_units
 
@@ -653,7 +653,7 @@ def main_strong(args, world, rank, local):
     PSK 73019412 must be reported by the rank whose range holds it, in every timed pass."""
     import torch.distributed as dist
     import dwpa_amd
-    from dwpa_amd import synth as S
+    from tests import synth as S
     from dwpa_amd.device import Event, Stream
     from dwpa_amd.shard import contiguous_shard, reduce_timing, strong_batches
 
@@ -750,7 +750,7 @@ def main_ffi(args, world, rank, local):
     import torch.distributed as dist
     import dwpa_amd
     from dwpa_amd import _lib as L
-    from dwpa_amd import synth as S
+    from tests import synth as S
     from dwpa_amd.shard import reduce_timing
 
     if world > 1:
@@ -802,6 +802,7 @@ def main_ffi(args, world, rank, local):
     window = [round(u0, 4), round(u0 + elapsed, 4)]
     if errors:
         raise errors[0]
+    call_stats = dwpa_amd.check_stats()  # the main thread's last timed call (dwpa_check_last_stats)
     keys_all = float(batch.nkeys * args.steps * callers)
     if world > 1:
         dist.barrier()
@@ -845,6 +846,8 @@ def main_ffi(args, world, rank, local):
             "hits": sum(1 for g in got if g),
             "mismatches": mismatches if args.workload == "c5" else None,
             "window_unix": window,
+            "last_call": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in call_stats.items()},
+            "tail_prio": int(os.environ.get("DWPA_TAIL_PRIO", "2")),
             "hits_checked": "every job's result against its planted key's [PSK, NC, endian, PMK] (re-derived by the "
                             "CPU oracle) or False" if args.workload == "c5" else "the planted PSK and its PMK"})
     if world > 1:
@@ -866,7 +869,7 @@ def main_latency(args, world, rank, local):
     import random
     import statistics
     import dwpa_amd
-    from dwpa_amd import synth as S
+    from tests import synth as S
     from oracle import oracle as O
     rng = random.Random(7)
     essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
@@ -979,7 +982,7 @@ def main_files(args, world, rank, local):
     import numpy as np
     import torch.distributed as dist
     import dwpa_amd
-    from dwpa_amd import synth as S
+    from tests import synth as S
     from dwpa_amd.shard import reduce_timing
 
     if world > 1:
@@ -1085,7 +1088,7 @@ def main_files_rules(args, world, rank, local):
     import numpy as np
     import torch.distributed as dist
     import dwpa_amd
-    from dwpa_amd import synth as S
+    from tests import synth as S
     from dwpa_amd.rulesets import server_rules, wpa_rules
     from dwpa_amd.shard import reduce_timing
 

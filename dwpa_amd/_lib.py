@@ -18,6 +18,7 @@ DWPA_E_NODEV, DWPA_E_HIP, DWPA_E_ARG, DWPA_E_NOMEM, DWPA_E_IO, DWPA_E_OVERFLOW, 
 DWPA_RC_CRACKED, DWPA_RC_EXHAUSTED, DWPA_RC_ERROR = 0, 1, -1
 DWPA_NC_PHP, DWPA_NC_HASHCAT = 0, 1
 DWPA_DICT_OK, DWPA_DICT_DAMAGED = 0, 1  # dwpa_crack_files_ex per-dictionary status (or DWPA_E_IO)
+DWPA_RULES_DEFAULT, DWPA_RULES_HASHCAT, DWPA_RULES_FULL = 0, 1, 2  # dwpa_config.rule_mode
 
 
 class DwpaError(RuntimeError):
@@ -42,13 +43,24 @@ class Job(ctypes.Structure):
 
 class Config(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device_mask", ctypes.c_uint32), ("batch", ctypes.c_uint32),
-                ("nc_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("nc_mode", ctypes.c_int32), ("rule_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
 
 
 class CrackStats(ctypes.Structure):
     _fields_ = [("words", ctypes.c_uint64), ("candidates", ctypes.c_uint64), ("hashes", ctypes.c_uint32),
                 ("cracked", ctypes.c_uint32), ("seconds", ctypes.c_double), ("rules", ctypes.c_uint32),
-                ("rules_skipped", ctypes.c_uint32)]
+                ("rules_skipped", ctypes.c_uint32), ("rules_rejmem", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class CheckStats(ctypes.Structure):
+    _fields_ = [("jobs", ctypes.c_uint32), ("slots", ctypes.c_uint32), ("pmks", ctypes.c_uint32),
+                ("tail_pmks", ctypes.c_uint32), ("tail_waves", ctypes.c_uint32), ("tail_waves_raised", ctypes.c_uint32),
+                ("hits", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("seconds", ctypes.c_double)]
+
+
+class RulesCounts(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint32) for n in ("present", "parsed", "loaded_hashcat", "rejmem", "invalid",
+                                               "first_invalid_line", "first_rejmem_line", "reserved")]
 
 
 class LineInfo(ctypes.Structure):
@@ -75,6 +87,7 @@ SIGNATURES = {
                            ctypes.c_int, ctypes.POINTER(Result)], ctypes.c_int),
     "dwpa_check_batch": ([ctypes.POINTER(Job), ctypes.c_size_t, ctypes.POINTER(Result), ctypes.POINTER(ctypes.c_int)],
                          ctypes.c_int),
+    "dwpa_check_last_stats": ([ctypes.POINTER(CheckStats)], ctypes.c_int),
     "dwpa_pbkdf2_pmk": ([ctypes.POINTER(Bytes), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),
     "dwpa_hc_unhex": ([ctypes.c_char_p, ctypes.c_size_t, _P, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dwpa_hash_m22000": ([ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),
@@ -92,6 +105,7 @@ SIGNATURES = {
                                 ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
     "dwpa_rules_count": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint32),
                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+    "dwpa_rules_count_ex": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(RulesCounts)], ctypes.c_int),
     "dwpa_rules_apply_host": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, _P,
                                ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
     "dwpa_scan_create": ([ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,

@@ -188,11 +188,6 @@ static bool trace_on() {
     return e && *e == '1';
 }
 
-// A field of the caller's dwpa_config counts only if its struct_size covers it (an older, shorter struct leaves the
-// later fields at their documented defaults).  struct_size 0 = the full current struct.
-#define DWPA_CFG_HAS(cfg, field) \
-    ((cfg) && (!(cfg)->struct_size || (cfg)->struct_size >= offsetof(dwpa_config, field) + sizeof((cfg)->field)))
-
 static int crack_impl(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file, int nec,
                       const char* out_file, const dwpa_config* cfg, int32_t* dict_status) {
     const auto t_call = std::chrono::steady_clock::now();
@@ -252,14 +247,19 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     }
     if (sh.valid == 0) return DWPA_RC_ERROR;  // hashcat: "No hashes loaded"
 
-    // hashcat -r: lines that do not parse are skipped with a message each (RuleSet::add_line) and counted in
-    // dwpa_crack_last_stats; a file with no valid rule left fails the call, as hashcat refuses to start
+    // hashcat -r: lines that do not parse -- and, in the default DWPA_RULES_HASHCAT mode, lines using reject or
+    // memory functions, which hashcat's -r loader skips too -- are skipped with a message each (RuleSet::add_line)
+    // and counted in dwpa_crack_last_stats; a file with no rule left fails the call, as hashcat refuses to start
     RuleSet rules;
+    const int want = DWPA_CFG_HAS(cfg, rule_mode) ? cfg->rule_mode : DWPA_RULES_DEFAULT;
+    if (want != DWPA_RULES_DEFAULT && want != DWPA_RULES_HASHCAT && want != DWPA_RULES_FULL) return DWPA_RC_ERROR;
+    rules.mode = want == DWPA_RULES_DEFAULT ? engine_rule_mode() : want;
     const RuleSet* rp = nullptr;
     if (rules_file) {
         const int lr = rules.load_file(rules_file);
         g_last_stats.rules = (uint32_t)rules.size();
         g_last_stats.rules_skipped = (uint32_t)rules.skipped.size();
+        g_last_stats.rules_rejmem = rules.rejmem;
         if (lr < 0) return DWPA_RC_ERROR;
         if (!rules.all_noop()) rp = &rules;
     }
@@ -427,11 +427,12 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     return sh.ncracked == sh.valid ? DWPA_RC_CRACKED : DWPA_RC_EXHAUSTED;
 }
 
-// One candidate as hashcat's --stdout writes it: $HEX[..] when a byte is outside 0x20..0x7e or the candidate itself
-// starts with "$HEX[" (a ':' needs no escaping here: there is no separator), else as it is.
+// One candidate as hashcat's --stdout writes it: the raw bytes and a newline.  A candidate holding '\n' or '\r'
+// would not survive as one line of a wordlist (hashcat's own output splits it), so it alone is written as $HEX[..],
+// which every dictionary reader here decodes back to the same bytes.
 static void stdout_plain(const uint8_t* p, size_t n, std::string& out) {
-    bool hex = n >= 5 && memcmp(p, "$HEX[", 5) == 0;
-    for (size_t i = 0; i < n && !hex; i++) hex = p[i] < 0x20 || p[i] > 0x7e;
+    bool hex = false;
+    for (size_t i = 0; i < n && !hex; i++) hex = p[i] == '\n' || p[i] == '\r';
     if (!hex) {
         out.append((const char*)p, n);
     } else {
@@ -460,6 +461,7 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
         fclose(f);
     }
     RuleSet rs;
+    rs.mode = engine_rule_mode();
     int rc = rs.load_file(rules_file);
     if (rc < 0) return rc;
     if ((rc = engine_init()) < 0) return rc;

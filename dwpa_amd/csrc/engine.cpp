@@ -209,6 +209,7 @@ struct Device {
     SlotTable slots;               // check path: the call's slots (capacity kept between calls)
     CheckScratch cs;               // check path: host-phase scratch
     std::vector<DedupPart> parts;  // check path: dedup output per host thread
+    dwpa_check_stats stats{};      // check path: the current call's statistics (dwpa_check_last_stats)
 };
 
 static std::mutex g_mu;
@@ -216,6 +217,7 @@ static bool g_init = false;
 static int g_ndev = 0;
 static uint32_t g_mask = 0;
 static uint32_t g_batch = 0;
+static int g_rule_mode = DWPA_RULES_DEFAULT;  // dwpa_init's cfg->rule_mode
 static std::vector<std::unique_ptr<Device>> g_dev;  // call contexts: [device * calls_per_device() + k]
 
 // Head fence of one physical device: concurrent calls launch their PBKDF2 heads one after another (each head
@@ -248,6 +250,7 @@ static int init_locked(const dwpa_config* cfg) {
     if (cfg) {
         g_mask = cfg->device_mask;
         g_batch = cfg->batch;
+        if (DWPA_CFG_HAS(cfg, rule_mode)) g_rule_mode = cfg->rule_mode;
     }
     if (g_init) return 0;
     int n = 0;
@@ -329,7 +332,7 @@ int Batch::reserve(uint32_t want_cap, uint32_t want_hitcap) {
         RCHK(hits.ensure((size_t)want_hitcap * sizeof(HitDev)));
         hitcap = want_hitcap;
     }
-    RCHK(counters.ensure(16));
+    RCHK(counters.ensure(32));  // [3] check path: head-done flag, [4] tail waves that raised their priority
     return 0;
 }
 
@@ -655,7 +658,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
     RCHK(upload_span(d.src, st.src, s));
     HIPCHK(hipMemcpyAsync(d.batch.ids.p, st.ids.data(), n * 8, hipMemcpyHostToDevice, s));
     // hit counter reset ahead of every kernel of this derive (the tail's verify may run before the head's)
-    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 16, s));
+    HIPCHK(hipMemsetAsync(d.batch.counters.p, 0, 32, s));
     tr.mark("  stage+upload");
     const uint32_t cap = d.batch.cap;
     const uint32_t* mid = (const uint32_t*)d.batch.mid.p;
@@ -668,11 +671,15 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
         std::lock_guard<std::mutex> fl(f.mu);
         if (head_fence_knob() && f.last && f.last != d.head_end) HIPCHK(hipStreamWaitEvent(s, f.last, 0));
         uint32_t* head_flag = (uint32_t*)d.batch.counters.p + 3;  // zeroed with the counters above
+        uint32_t* raised = (uint32_t*)d.batch.counters.p + 4;     // likewise; read back by collect_hits
+        d.stats.pmks += nu;
         if (nh < nu) {  // the tail first, beside the head (priority 0 until the head has ended: pbkdf2_lane_tail)
             HIPCHK(hipEventRecord(d.prep_done, s));
             HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
             HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh,
-                                         head_flag, (uint32_t)tail_prio_knob(), d.tail));
+                                         head_flag, (uint32_t)tail_prio_knob(), raised, d.tail));
+            d.stats.tail_pmks += nu - nh;
+            d.stats.tail_waves += 2 * ((nu - nh + 63) / 64);  // two output-block lanes per PMK
         }
         HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
         if (nh < nu) HIPCHK(launch_set_flag(head_flag, s));
@@ -778,11 +785,12 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
             nwaves[k] += (uint32_t)(((uint64_t)sg.count * tb.lines[sg.line].natt + 63) / 64);
         }
     // per-key EapolKey state scratch of the attempt-parallel launches: one region per class (the classes may run
-    // on parallel streams), class k's stride = 64 x its segments
+    // on parallel streams), class k's stride = att_seg (the most keys an attempt-parallel segment holds) x its
+    // segments
     size_t koff[8] = {0}, ktotal = 0;
     for (int k = 4; k < 8; k++) {
         koff[k] = ktotal;
-        ktotal += (size_t)eapol_key_words(bucket_vc(k)) * bucket[k].size() * 64;
+        ktotal += (size_t)eapol_key_words(bucket_vc(k)) * bucket[k].size() * att_seg;
     }
     if (ktotal) RCHK(keybuf.ensure(ktotal * 4));
     std::vector<SegDev> segs;
@@ -822,8 +830,8 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
                                  (const AttDev*)d.atts.p, (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap, vc, vsk));
         else
             HIPCHK(launch_verify_att((const uint32_t*)d.batch.pmk.p, d.batch.cap, (const uint64_t*)d.batch.ids.p, sg,
-                                     nb, nwaves[k], (uint32_t*)keybuf.p + koff[k], (uint32_t)bucket[k].size() * 64,
-                                     (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p,
+                                     nb, nwaves[k], (uint32_t*)keybuf.p + koff[k], (uint32_t)bucket[k].size() * att_seg,
+                                     att_seg, (const LineDev*)d.lines.p, (const uint32_t*)d.pool.p, (const AttDev*)d.atts.p,
                                      (HitDev*)d.batch.hits.p, hitcnt, d.batch.hitcap,
                                      first_key_exit_knob() ? (uint32_t*)d.first_hit.p : nullptr, vc, vsk));
     }
@@ -841,10 +849,12 @@ static int collect_hits(Device& d, std::vector<HitDev>& hits_out) {
     RCHK(join_tail(d));
     const uint32_t* hitcnt = (const uint32_t*)d.batch.counters.p + 1;
     RCHK(d.hits_host.ensure(16 + (size_t)d.batch.hitcap * sizeof(HitDev)));
-    HIPCHK(launch_hits_out(hitcnt, (const HitDev*)d.batch.hits.p, d.batch.hitcap, (uint32_t*)d.hits_host.dev, s));
+    HIPCHK(launch_hits_out(hitcnt, (const HitDev*)d.batch.hits.p, d.batch.hitcap, (uint32_t*)d.hits_host.dev,
+                           (const uint32_t*)d.batch.counters.p + 4, s));
     HIPCHK(hipStreamSynchronize(s));
     tr.mark("  device wait");
     const uint32_t nh = *(volatile const uint32_t*)d.hits_host.p;
+    d.stats.tail_waves_raised += *((volatile const uint32_t*)d.hits_host.p + 1);
     if (nh > d.batch.hitcap) return DWPA_E_OVERFLOW;
     size_t old = hits_out.size();
     hits_out.resize(old + nh);
@@ -897,13 +907,33 @@ static Device* pick_device() {
     return d;
 }
 
+// dwpa_check_last_stats: the calling thread's last check call
+static thread_local dwpa_check_stats g_check_stats;
+static thread_local bool g_have_check_stats = false;
+
+static int check_batch_body(Device& d, const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs,
+                            DrainOnExit& drain);
+
 static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs) {
+    const auto t0 = std::chrono::steady_clock::now();
+    g_check_stats = dwpa_check_stats{};
+    g_have_check_stats = true;
     RCHK(ensure_init());
     Device* dp = pick_device();
     if (!dp) return DWPA_E_NODEV;
     std::lock_guard<std::mutex> lk(dp->mu, std::adopt_lock);
     DrainOnExit drain{*dp};
     Device& d = *dp;
+    d.stats = dwpa_check_stats{};
+    d.stats.jobs = (uint32_t)std::min<size_t>(njobs, UINT32_MAX);
+    const int rc = check_batch_body(d, jobs, njobs, out, rcs, drain);
+    g_check_stats = d.stats;
+    g_check_stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+static int check_batch_body(Device& d, const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs,
+                            DrainOnExit& drain) {
     HIPCHK(hipSetDevice(d.id));
     RCHK(device_stream(d));
 
@@ -982,6 +1012,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         }
     }
     cs.gslot[G] = (uint32_t)nslots;
+    d.stats.slots = (uint32_t)std::min<size_t>(nslots, UINT32_MAX);
     if (!nslots) return 0;
     if (nslots >= SLOT_CALLER) return DWPA_E_ARG;
     tr.mark("essid groups");
@@ -1094,6 +1125,7 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
         if (best[j] < 0) continue;
         const LineDev& L = tb.lines[job_line[j]];
         rcs[j] = DWPA_HIT;
+        d.stats.hits++;
         out[j].key_index = (int32_t)T.kidx[cs.jslot[j] + (size_t)best[j]];  // ordinal -> the caller's index
         pmk_bytes(best_hit[j]->pmk, out[j].pmk);
         if (L.kind == LINE_PMKID) {
@@ -1453,6 +1485,14 @@ int scan_device(const dwpa_scan* sc) { return sc->device; }
 // helpers for crack.cpp
 // ---------------------------------------------------------------------------------------------------------
 int engine_init() { return ensure_init(); }
+int engine_rule_mode() {
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (g_rule_mode == DWPA_RULES_HASHCAT || g_rule_mode == DWPA_RULES_FULL) return g_rule_mode;
+    }
+    const char* e = getenv("DWPA_RULE_MODE");
+    return e && strcmp(e, "full") == 0 ? DWPA_RULES_FULL : DWPA_RULES_HASHCAT;
+}
 std::vector<int> engine_devices(uint32_t mask) { return active_devices(mask); }
 uint32_t engine_batch() { return default_batch(); }
 
@@ -1469,6 +1509,8 @@ int dwpa_abi_version(void) { return DWPA_ABI_VERSION; }
 
 int dwpa_init(const dwpa_config* cfg) {
     if (cfg && cfg->struct_size && cfg->struct_size < sizeof(uint32_t) * 3) return DWPA_E_ARG;
+    if (DWPA_CFG_HAS(cfg, rule_mode) && (cfg->rule_mode < DWPA_RULES_DEFAULT || cfg->rule_mode > DWPA_RULES_FULL))
+        return DWPA_E_ARG;
     std::lock_guard<std::mutex> lk(g_mu);
     return init_locked(cfg);
 }
@@ -1546,6 +1588,12 @@ int dwpa_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* 
     if ((!jobs || !out || !rcs) && njobs) return DWPA_E_ARG;
     if (njobs == 0) return 0;
     return check_batch_impl(jobs, njobs, out, rcs);
+}
+
+int dwpa_check_last_stats(dwpa_check_stats* out) {
+    if (!out || !dwpa::g_have_check_stats) return DWPA_E_ARG;
+    *out = dwpa::g_check_stats;
+    return 0;
 }
 
 int dwpa_pbkdf2_pmk(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* pmks_out) {

@@ -27,7 +27,15 @@ struct Batch {
     int reserve(uint32_t cap, uint32_t hitcap);
 };
 
+// A field of the caller's dwpa_config counts only if its struct_size covers it (an older, shorter struct leaves the
+// later fields at their documented defaults).  struct_size 0 = the full current struct.
+#define DWPA_CFG_HAS(cfg, field) \
+    ((cfg) && (!(cfg)->struct_size || (cfg)->struct_size >= offsetof(dwpa_config, field) + sizeof((cfg)->field)))
+
 int engine_init();
+// Rule-file loader mode of the process: dwpa_init's cfg->rule_mode when given, else DWPA_RULE_MODE=full|hashcat
+// from the environment, else DWPA_RULES_HASHCAT.  Host only (no device needed).
+int engine_rule_mode();
 std::vector<int> engine_devices(uint32_t mask);  // mask 0 = the dwpa_init() selection
 uint32_t engine_batch();
 

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 // The check path's PBKDF2 tail (pbkdf2_lane_tail): same slots and salt entries as k_pbkdf2_ms.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_ms_tail(
     const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
-    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, const uint32_t* __restrict__ flag, uint32_t prio) {
+    const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, uint32_t* flag, uint32_t prio, uint32_t* raised) {
     const uint32_t blk = blockIdx.y;
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= min(count, cap)) return;
@@ -133,13 +133,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     load_mid(mid, cap, s, hi, ho);
     const uint32_t* e = pool + sref[s];
     const uint32_t nsalt = e[0];
-    pbkdf2_lane_tail(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t, flag, prio);
+    pbkdf2_lane_tail(hi, ho, e + 1 + (size_t)blk * nsalt * 16, nsalt, t, flag, prio, raised);
     store_block(pmk, cap, s, blk, t);
 }
 
-// Sets the tail's head-done flag (agent scope: the tail's waves poll it from every XCD).
-__global__ void k_set_flag(uint32_t* __restrict__ flag) {
-    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Sets the tail's head-done flag with an agent-scope atomic (the tail's waves poll it with atomics from every XCD).
+__global__ void k_set_flag(uint32_t* flag) {
+    if (threadIdx.x == 0) __hip_atomic_exchange(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Wave priority of the check path's post-derive kernels (DWPA_CHECK_PRIO, set per device by set_check_prio); the
@@ -173,9 +173,10 @@ __global__ __launch_bounds__(256) void k_gather_pmk(const uint32_t* __restrict__
 // Hit count and hits -> host-mapped pinned memory (word 0 = count, the min(count, hitcap) HitDev records from byte
 // 16): the check path reads its results without a device-to-host copy, whose runtime blit kernel would run at wave
 // priority 0 and starve beside another call's PBKDF2 head.
+// Word 1 = *raised (the tail waves that raised their priority, pbkdf2_lane_tail; 0 without a counter).
 __global__ __launch_bounds__(256) void k_hits_out(const uint32_t* __restrict__ hitcnt,
                                                   const HitDev* __restrict__ hits, uint32_t hitcap,
-                                                  uint32_t* __restrict__ out) {
+                                                  uint32_t* __restrict__ out, const uint32_t* __restrict__ raised) {
     __builtin_amdgcn_s_setprio(3);
     const uint32_t n = min(*hitcnt, hitcap);
     constexpr uint32_t W = sizeof(HitDev) / 4;
@@ -183,7 +184,10 @@ __global__ __launch_bounds__(256) void k_hits_out(const uint32_t* __restrict__ h
     const uint32_t total = n * W;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
         out[4 + i] = src[i];
-    if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = *hitcnt;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[0] = *hitcnt;
+        out[1] = raised ? *raised : 0u;
+    }
 }
 
 // Caller-supplied PMK for one slot (check_key_m22000's $pmk argument, common.php:157,178).
@@ -543,7 +547,8 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
 //
 // k_eapol_keys: lane = (segment, key) pair, computes everything of the check that depends on the PMK but not on
 // the attempt (HMAC key midstates, PRF prefix: EapolKey) once per pair into a SoA scratch array, word w of pair
-// (segment i, key k) at keys[w * kstride + 64 i + k].
+// (segment i, key k) at keys[w * kstride + segk * i + k] (segk = the most keys a segment holds, 1..64: the host cuts
+// attempt-parallel segments to DWPA_ATT_SEG_KEYS keys, so the scratch is sized for that, not for 64).
 //
 // k_verify_att: the (key, attempt) items of a segment are laid out key-major and cut into waves of 64 lanes, so
 // every lane runs one attempt and a wave ends only where the segment does (segs[i].pad = the segment's first wave
@@ -560,20 +565,20 @@ __global__ __launch_bounds__(256) void k_eapol_keys(const uint32_t* __restrict__
                                                     const SegDev* __restrict__ segs, uint32_t nsegs,
                                                     const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool, uint32_t* __restrict__ keys,
-                                                    uint32_t kstride) {
+                                                    uint32_t kstride, uint32_t segk) {
     check_prio_vc<VC>();
     const uint32_t segi = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t k = threadIdx.x & 63;
     if (segi >= nsegs) return;
     const SegDev sg = segs[segi];
-    if (k >= sg.count) return;
+    if (k >= sg.count || k >= segk) return;
     const LineDev L = lines[sg.line];
     uint32_t p[8];
 #pragma unroll
     for (int w = 0; w < 8; w++) p[w] = pmk[(size_t)w * cap + sg.slot + k];
     EapolKey K;
     eapol_key<VC>(L, pool, p, K);
-    uint32_t* o = keys + (size_t)segi * 64 + k;
+    uint32_t* o = keys + (size_t)segi * segk + k;
     if ((VC & VC_KV3) && L.keyver == 3) {
 #pragma unroll
         for (int w = 0; w < 8; w++) {
@@ -595,7 +600,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                     const uint64_t* __restrict__ ids,
                                                     const SegDev* __restrict__ segs, uint32_t nsegs, uint32_t nwaves,
                                                     const uint32_t* __restrict__ keys, uint32_t kstride,
-                                                    const LineDev* __restrict__ lines,
+                                                    uint32_t segk, const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool,
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                     uint32_t* __restrict__ hitcnt, uint32_t hitcap,
@@ -622,11 +627,15 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     const uint32_t segi = lo;
     const SegDev sg = segs[segi];
     const LineDev L = lines[sg.line];
-    // first-key early exit: every key of this wave comes after a key of the same job that already matched
+    // first-key early exit: every key of this wave comes after a key of the same job that already matched.
+    // first_hit holds key ordinals (ids: a job's keys in input order, numbered across the call's chunks), so the
+    // rule holds across chunks too.
     if (first_hit) {
         const uint32_t f = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(first_hit + sg.line, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (sg.slot + (gw - sg.pad) * 64 / L.natt > f) return;
+        const uint32_t s0 = sg.slot + (gw - sg.pad) * 64 / L.natt;  // the wave's first key (wave-uniform)
+        const uint32_t o0 = ids ? (uint32_t)ids[s0] : s0;
+        if (o0 > f) return;
     }
     const uint32_t item = (gw - sg.pad) * 64 + lane;
     const uint32_t k = item / L.natt, a = item - k * L.natt;
@@ -635,7 +644,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     const uint32_t slot = sg.slot + kk;
     const uint64_t cand = ids ? ids[slot] : (uint64_t)slot;
     EapolKey K;
-    const uint32_t* kp = keys + (size_t)segi * 64 + kk;
+    const uint32_t* kp = keys + (size_t)segi * segk + kk;
     if ((VC & VC_KV3) && L.keyver == 3) {
 #pragma unroll
         for (int w = 0; w < 8; w++) {
@@ -653,7 +662,8 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     uint32_t mic[4];
     eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic, rk);
     const bool found = active && mic_match(L, mic);
-    if (found && first_hit) __hip_atomic_fetch_min(first_hit + sg.line, slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (found && first_hit)
+        __hip_atomic_fetch_min(first_hit + sg.line, (uint32_t)cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     report_hits(found, lane, cand, sg.line, a, pmk + slot, cap, hits, hitcnt, hitcap);
 }
 
@@ -727,19 +737,19 @@ hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t
 }
 
 hipError_t launch_hits_out(const uint32_t* hitcnt, const HitDev* hits, uint32_t hitcap, uint32_t* out,
-                           hipStream_t s) {
+                           const uint32_t* raised, hipStream_t s) {
     const uint32_t blocks = cdiv((uint64_t)hitcap * (sizeof(HitDev) / 4), 256);
     hipLaunchKernelGGL(k_hits_out, dim3(blocks < 1 ? 1 : blocks > 64 ? 64 : blocks), dim3(256), 0, s, hitcnt, hits,
-                       hitcap, out);
+                       hitcap, out, raised);
     return hipGetLastError();
 }
 
 hipError_t launch_pbkdf2_ms_tail(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                                 const uint32_t* sref, uint32_t* pmk, const uint32_t* flag, uint32_t prio,
-                                 hipStream_t s) {
+                                 const uint32_t* sref, uint32_t* pmk, uint32_t* flag, uint32_t prio,
+                                 uint32_t* raised, hipStream_t s) {
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pbkdf2_ms_tail, dim3(cdiv(count, 256), 2), dim3(256), 0, s, mid, cap, count, pool, sref, pmk,
-                       flag, prio);
+                       flag, prio, raised);
     return hipGetLastError();
 }
 
@@ -786,16 +796,17 @@ hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids,
 uint32_t eapol_key_words(uint32_t vc) { return (vc & VC_KV3) ? 16u : 10u; }
 
 hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
-                             uint32_t nsegs, uint32_t nwaves, uint32_t* keys, uint32_t kstride, const LineDev* lines,
-                             const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt,
-                             uint32_t hitcap, uint32_t* first_hit, uint32_t vc, hipStream_t s) {
+                             uint32_t nsegs, uint32_t nwaves, uint32_t* keys, uint32_t kstride, uint32_t segk,
+                             const LineDev* lines, const uint32_t* pool, const AttDev* atts, HitDev* hits,
+                             uint32_t* hitcnt, uint32_t hitcap, uint32_t* first_hit, uint32_t vc, hipStream_t s) {
     if (nsegs == 0 || nwaves == 0) return hipSuccess;
-    if (kstride < nsegs * 64) return hipErrorInvalidValue;
+    if (segk < 1 || segk > 64 || kstride < (uint64_t)nsegs * segk) return hipErrorInvalidValue;
 #define DWPA_LAUNCH_VERIFY_ATT(V)                                                                                 \
     hipLaunchKernelGGL(k_eapol_keys<V>, dim3(cdiv((uint64_t)nsegs * 64, 256)), dim3(256), 0, s, pmk, cap, segs,   \
-                       nsegs, lines, pool, keys, kstride);                                                         \
+                       nsegs, lines, pool, keys, kstride, segk);                                                   \
     hipLaunchKernelGGL(k_verify_att<V>, dim3(cdiv(nwaves, vc_block(V) / 64)), dim3(vc_block(V)), 0, s, pmk, cap, \
-                       ids, segs, nsegs, nwaves, keys, kstride, lines, pool, atts, hits, hitcnt, hitcap, first_hit)
+                       ids, segs, nsegs, nwaves, keys, kstride, segk, lines, pool, atts, hits, hitcnt, hitcap,    \
+                       first_hit)
     DWPA_VC_DISPATCH(vc & ~VC_PMKID, DWPA_LAUNCH_VERIFY_ATT)
 #undef DWPA_LAUNCH_VERIFY_ATT
     return hipGetLastError();

@@ -31,15 +31,16 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
 hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                   const uint32_t* sref, uint32_t* pmk, hipStream_t s);
 // attempt-parallel verification of EAPOL lists with >= ATT_PARALLEL_MIN attempts: lane = (key, attempt) item,
-// segs[i].pad = first wave of segment i (ceil(count * natt / 64) waves each, nwaves in all); keys = scratch of
-// eapol_key_words(vc) x kstride words, kstride >= 64 * nsegs
+// segs[i].pad = first wave of segment i (ceil(count * natt / 64) waves each, nwaves in all), segs[i].count <= segk
+// (1..64); keys = scratch of eapol_key_words(vc) x kstride words, kstride >= segk * nsegs
 uint32_t eapol_key_words(uint32_t vc);
-// first_hit (nullable): per line, the smallest slot with a hit so far (~0u: none); waves whose keys all come after
-// it exit at once, and hits lower it (the check wants only the first key in input order)
+// first_hit (nullable): per line, the smallest key ordinal (ids[slot]: a job's keys numbered in input order, across
+// all chunks of the call) with a hit so far (~0u: none); waves whose keys all come after it exit at once, and hits
+// lower it (the check wants only the first key in input order).  Reset it once per call, not per chunk.
 hipError_t launch_verify_att(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const SegDev* segs,
-                             uint32_t nsegs, uint32_t nwaves, uint32_t* keys, uint32_t kstride, const LineDev* lines,
-                             const uint32_t* pool, const AttDev* atts, HitDev* hits, uint32_t* hitcnt,
-                             uint32_t hitcap, uint32_t* first_hit, uint32_t vc, hipStream_t s);
+                             uint32_t nsegs, uint32_t nwaves, uint32_t* keys, uint32_t kstride, uint32_t segk,
+                             const LineDev* lines, const uint32_t* pool, const AttDev* atts, HitDev* hits,
+                             uint32_t* hitcnt, uint32_t hitcap, uint32_t* first_hit, uint32_t vc, hipStream_t s);
 // many ESSID groups x one batch per launch (cap % 64 == 0): gsalt[c] = {salt word offset, nsalt} of chunk group c,
 // PMK word k of (c, slot) at pmk[k * pstride + c * cap + slot]
 hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* counter, uint32_t ngroups,
@@ -49,10 +50,11 @@ hipError_t launch_pbkdf2_mg_plain(const uint32_t* mid, uint32_t cap, const uint3
                                   const uint32_t* salt, const uint32_t* gsalt, uint32_t* pmk, uint32_t pstride,
                                   hipStream_t s);
 // Check-path tail: PBKDF2 of slots [0, count) like launch_pbkdf2_ms_plain, at wave priority 0 until *flag != 0,
-// then at `prio` (0 = never raised).  launch_set_flag sets the flag (queue it after the head).
+// then at `prio` (0 = never raised); every wave that raises itself adds 1 to *raised.  launch_set_flag sets the
+// flag (queue it after the head).
 hipError_t launch_pbkdf2_ms_tail(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
-                                 const uint32_t* sref, uint32_t* pmk, const uint32_t* flag, uint32_t prio,
-                                 hipStream_t s);
+                                 const uint32_t* sref, uint32_t* pmk, uint32_t* flag, uint32_t prio,
+                                 uint32_t* raised, hipStream_t s);
 hipError_t launch_set_flag(uint32_t* flag, hipStream_t s);
 // Wave priority (0..3) of the check path's post-derive kernels (PMK gather, EAPOL key states, verifies) on the
 // current device; the hit copy-out always runs at 3.
@@ -62,9 +64,10 @@ hipError_t set_kv3_prio(uint32_t prio);
 constexpr uint32_t GATHER_CALLER = 0x80000000u;
 hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t* cpmk, const uint32_t* src,
                              uint32_t n, uint32_t* pmk, uint32_t cap, hipStream_t s);
-// out: host-mapped, >= 16 + hitcap * sizeof(HitDev) bytes (word 0 = hit count, HitDev records from byte 16)
+// out: host-mapped, >= 16 + hitcap * sizeof(HitDev) bytes (word 0 = hit count, word 1 = *raised or 0, HitDev
+// records from byte 16)
 hipError_t launch_hits_out(const uint32_t* hitcnt, const HitDev* hits, uint32_t hitcap, uint32_t* out,
-                           hipStream_t s);
+                           const uint32_t* raised, hipStream_t s);
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s);
 hipError_t launch_verify(const uint32_t* pmk, uint32_t cap, const uint64_t* ids, const uint32_t* counter,
                          const SegDev* segs, uint32_t nsegs, uint32_t line_base, uint32_t nlines, const LineDev* lines,

@@ -77,9 +77,13 @@ __device__ __forceinline__ void set_wave_prio(uint32_t p) {
 // The check path's tail lane (the PBKDF2 remainder of under one wave per SIMD, launched beside the head): wave
 // priority 0 while *flag == 0, so it takes only the issue slots the head leaves; once the head has ended (the
 // engine sets the flag from the head's stream) it raises itself to `prio`, ahead of the verify waves that share its
-// SIMDs.  The flag is polled every 64 iterations with an agent-scope load (the writer may sit on another XCD).
+// SIMDs.  The flag is polled every 64 iterations with an agent-scope read-modify-write (fetch_add 0): the writer
+// may sit on another XCD, and a plain agent-scope load of a word this XCD's L2 already holds can keep returning
+// that stale copy, while an atomic is performed where every XCD sees the same word.  Each wave that
+// raises itself bumps *raised once (dwpa_check_last_stats.tail_waves_raised).
 __device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uint32_t ho[5], const uint32_t* sb,
-                                                 uint32_t nsalt, uint32_t t[5], const uint32_t* flag, uint32_t prio) {
+                                                 uint32_t nsalt, uint32_t t[5], uint32_t* flag, uint32_t prio,
+                                                 uint32_t* raised) {
     uint32_t st[5] = {hi[0], hi[1], hi[2], hi[3], hi[4]};
     for (uint32_t b = 0; b < nsalt; b++) {
         uint32_t m[16];
@@ -95,11 +99,17 @@ __device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uin
     for (int k = 0; k < 5; k++) t[k] = u[k];
     int it = 1;
     if (prio) {
+        bool up = false;  // wave-uniform (readfirstlane)
+        // an operand the compiler cannot see is zero: an RMW of a known 0 is folded into a plain atomic load
+        uint32_t zero;
+        __asm__ volatile("s_mov_b32 %0, 0" : "=s"(zero));
 #pragma unroll 1
         for (; it < 4096; it++) {
             if ((it & 63) == 0 &&
-                __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_fetch_add(flag, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                 set_wave_prio(prio);
+                up = true;
                 break;
             }
             sha1_84(MI, u, x);
@@ -107,6 +117,10 @@ __device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uin
 #pragma unroll
             for (int k = 0; k < 5; k++) t[k] ^= u[k];
         }
+        // outside the loop: a lane-0-only atomic inside a loop can make the compiler split the loop by lanes
+        const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        if (up && lane == __builtin_amdgcn_readfirstlane(lane))
+            __hip_atomic_fetch_add(raised, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll 1
     for (; it < 4096; it++) {

@@ -92,6 +92,18 @@ bool parse_rule(const std::string& line_in, std::vector<RuleOp>* ops, bool* is_r
     return true;
 }
 
+bool rule_uses_rejmem(const std::vector<RuleOp>& ops) {
+    for (const RuleOp& o : ops)
+        switch (o.op) {
+        case '<': case '>': case '_': case '!': case '/': case '(': case ')': case '=': case '%': case 'Q':  // reject
+        case 'M': case '4': case '6': case 'X':                                                               // memory
+            return true;
+        default:
+            break;
+        }
+    return false;
+}
+
 int RuleSet::add_line(const std::string& line_in, uint32_t lineno) {
     std::string line = line_in;
     while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
@@ -107,6 +119,18 @@ int RuleSet::add_line(const std::string& line_in, uint32_t lineno) {
         if (!quiet)
             fprintf(stderr, "[dwpa] skipping invalid or unsupported rule in %s on line %u: %s\n", source.c_str(),
                     lineno, line.c_str());
+        return -1;
+    }
+    if (mode == DWPA_RULES_HASHCAT && rule_uses_rejmem(ops)) {
+        // hashcat's -r loader takes no reject / memory function (they work only with -j/-k): the same message
+        skipped.push_back(line);
+        skipped_lines.push_back(lineno);
+        rejmem++;
+        if (!quiet)
+            fprintf(stderr,
+                    "[dwpa] skipping invalid or unsupported rule in %s on line %u: %s (reject / memory functions "
+                    "work only with -j/-k; DWPA_RULE_MODE=full runs them)\n",
+                    source.c_str(), lineno, line.c_str());
         return -1;
     }
     rules.push_back(std::move(ops));
@@ -128,7 +152,7 @@ void RuleSet::load_text(const char* t, size_t len) {
     if (!cur.empty()) add_line(cur, lineno);
 }
 
-int RuleSet::load_file(const char* path) {
+int RuleSet::load_file(const char* path) {  // mode as set by the caller
     FILE* f = fopen(path, "rb");
     if (!f) return DWPA_E_IO;
     std::string all;
@@ -281,6 +305,30 @@ extern "C" int dwpa_rules_count(const char* rules_text, size_t rules_len, uint32
     if (nrules_parsed) *nrules_parsed = (uint32_t)rs.size();
     if (first_skipped_line)
         *first_skipped_line = rs.skipped_lines.empty() ? 0 : rs.skipped_lines[0];
+    return 0;
+}
+
+extern "C" int dwpa_rules_count_ex(const char* rules_text, size_t rules_len, dwpa_rules_counts* out) {
+    using namespace dwpa;
+    if ((!rules_text && rules_len) || !out) return DWPA_E_ARG;
+    RuleSet full;  // the interpreter's load; the hashcat loader keeps its parsed lines without reject / memory ones
+    full.quiet = true;
+    full.load_text(rules_text, rules_len);
+    RuleSet hc;
+    hc.quiet = true;
+    hc.mode = DWPA_RULES_HASHCAT;
+    hc.load_text(rules_text, rules_len);
+    memset(out, 0, sizeof(*out));
+    out->present = full.present;
+    out->parsed = (uint32_t)full.size();
+    out->loaded_hashcat = (uint32_t)hc.size();
+    out->rejmem = hc.rejmem;
+    out->invalid = (uint32_t)full.skipped.size();
+    out->first_invalid_line = full.skipped_lines.empty() ? 0 : full.skipped_lines[0];
+    for (size_t i = 0; i < hc.skipped_lines.size() && !out->first_rejmem_line; i++)
+        if (std::find(full.skipped_lines.begin(), full.skipped_lines.end(), hc.skipped_lines[i]) ==
+            full.skipped_lines.end())
+            out->first_rejmem_line = hc.skipped_lines[i];
     return 0;
 }
 

@@ -15,6 +15,12 @@
 // oracle/rules.py, the test oracle all three implementations are held to; hashcat itself is third party, so they
 // are parity unpinned by the reference.  A rule line that does not parse is skipped and reported (stderr, hashcat's
 // "Skipping invalid or unsupported rule", and the counts below), never dropped silently.
+//
+// Loader modes (RuleSet::mode): rules *files* (dwpa_crack_files' -r, dwpa_rules_expand_file) load as hashcat's -r
+// loader does by default (DWPA_RULES_HASHCAT): reject functions (< > _ ! / ( ) = % Q) and memory functions (M 4 6 X)
+// work only with -j/-k, so a line using one is skipped and counted like an invalid line and the candidate set is
+// exactly hashcat -r's; DWPA_RULES_FULL runs them (a superset).  The text entry points are the interpreter and load
+// every function.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,18 +40,23 @@ struct RuleOp {
     uint8_t op, p1, p2, p3;
 };
 
+// True when the rule uses a reject or a memory function (hashcat's -r loader skips such lines).
+bool rule_uses_rejmem(const std::vector<RuleOp>& ops);
+
 struct RuleSet {
     std::vector<std::vector<RuleOp>> rules;
     std::vector<std::string> text;
+    int mode = DWPA_RULES_FULL;           // DWPA_RULES_HASHCAT: skip reject / memory lines (files set it)
     uint32_t present = 0;                 // rule lines seen (not empty, not a '#' comment)
-    std::vector<std::string> skipped;     // lines that did not parse
+    std::vector<std::string> skipped;     // lines skipped: not parsing, or (HASHCAT mode) reject / memory
     std::vector<uint32_t> skipped_lines;  // their 1-based line numbers
+    uint32_t rejmem = 0;                  // of skipped, the reject / memory lines (HASHCAT mode)
     std::string source = "rules";         // file name for the messages
     bool quiet = false;                   // no stderr message per skipped line
     size_t size() const { return rules.size(); }
     int load_file(const char* path);
     void load_text(const char* text, size_t len);
-    int add_line(const std::string& line, uint32_t lineno = 0);  // 1 added, 0 not a rule, -1 skipped (invalid)
+    int add_line(const std::string& line, uint32_t lineno = 0);  // 1 added, 0 not a rule, -1 skipped
     bool all_noop() const;
     // the candidate, or false when the input or a reject / memory function rejects it
     bool apply_host(size_t rule, const std::string& word, std::string* out) const;

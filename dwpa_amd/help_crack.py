@@ -1,34 +1,44 @@
 """help_crack.py drop-in: run the m22000 attack in-process through libdwpa22000.so instead of a hashcat subprocess.
 
-Replaces ``HelpCrack.run_cracker`` (help_crack/help_crack.py:765-802) and the ``hashcat --stdout -r`` rule
-expansions (:508, :575) with the same inputs, outputs and return codes:
+Replaces, with the same inputs, outputs and return codes:
 
-* inputs   -- ``conf["hash_file"]`` (one m22000 line per hash, written by prepare_work :439-442),
-              ``conf["rules"]`` ("" or "-S -r <file>", :445-447 / :931-933), ``conf["key_file"]``, the dictionary
-              list (plain or .gz), ``conf["coptions"]`` (``-d 1,2`` selects devices like hashcat's ``-d``);
-* output   -- the ``-o`` key file in hashcat's m22000 outfile format, parsed unchanged by ``get_key`` (:804-879);
-* rc       -- hashcat semantics: 0 all cracked, 1 exhausted (drives the second pass at :930); device errors are
-              retried after ``sleepy()`` as the reference's loop does (:776-786), never returned; dictionary
-              errors are not retried (see run_cracker).
+* ``HelpCrack.run_cracker`` (help_crack/help_crack.py:765-802, command line :773, rc handling :776-786):
+  ``conf["hash_file"]`` (one m22000 line per hash, written by prepare_work :439-442), ``conf["rules"]`` ("" or
+  "-S -r <file>", :445-447 / :931-933), ``conf["key_file"]``, the dictionary list (plain or .gz),
+  ``conf["coptions"]`` (``-d 1,2`` selects devices like hashcat's ``-d``) -> the ``-o`` key file in hashcat's m22000
+  outfile format, parsed unchanged by ``get_key`` (:804-879), and hashcat's rc (0 all cracked, 1 exhausted: drives
+  the second pass at :930; device errors are retried after ``sleepy()`` as the reference's loop does, never
+  returned; dictionary errors are not retried, see run_cracker);
+* ``HelpCrack.check_tools`` (:191-307), which looks for a hashcat >= 6.2.6 or john binary and ``sys.exit(1)``s
+  without one (:286-290): the replacement needs no binary, checks that a gfx950 device is usable, and sets
+  ``conf["cracker"]`` and ``conf["format"] = "22000"`` (what ``set_format`` does for hashcat, :278-284), so that
+  prepare_challenge (:705-708), prepare_work (:441) and prepare_dicts (:536, :571) take their m22000 branches;
+* the two ``./hashcat.bin --stdout ... -r bestWPA.rule source.txt`` expansions -- ``expandcracked`` (:508-509) and
+  the prdict expansion inline in ``prepare_dicts`` (:575-576) -- answered by the GPU rule engine
+  (dwpa_rules_expand_file) through help_crack's module-level ``subprocess``: every other subprocess call
+  (hcxpsktool :645, imeigen :684) goes to the real module unchanged.
 
-Usage from help_crack.py (the one-line change INTEGRATION.md shows)::
+Usage: two lines in help_crack.py's ``__main__`` block, before ``hc = HelpCrack(conf)`` (:995)::
 
-    from dwpa_amd.help_crack import run_cracker as _gpu_run_cracker
-    HelpCrack.run_cracker = lambda self, dictlist, disablestdout=False: _gpu_run_cracker(
-        self.conf, dictlist, sleepy=self.sleepy, pprint=self.pprint, quiet=disablestdout)
+    from dwpa_amd.help_crack import install
+    install(HelpCrack)
 """
 from __future__ import annotations
 
 import gzip
 import os
 import shlex
+import shutil
 import sys
+import tempfile
 import time
 
 from . import m22000 as M
 from . import _lib as L
 
 NONCE_ERROR_CORRECTIONS = 8  # help_crack.py:773 passes --nonce-error-corrections=8
+CRACKER = "libdwpa22000 (gfx950)"  # conf["cracker"] after the installed check_tools
+HASHCAT_NAMES = ("hashcat", "hashcat.bin", "hashcat.exe")  # the binaries check_tools looks for (:244)
 
 
 def _parse_options(rules: str, coptions: str):
@@ -166,3 +176,159 @@ def expand_rules(rules_file: str, source: str, out_path: str, gzip_level: int = 
     to start.  Returns the number of candidates written."""
     _, cands = M.rules_expand_file(rules_file, [source], out_path, gzip_level, device)
     return cands
+
+
+class HashcatArgError(ValueError):
+    """A `hashcat --stdout` command line this replacement does not take (it names what)."""
+
+
+def parse_hashcat_stdout(argv):
+    """`hashcat --stdout` argv -> (rules files, wordlists, outfile or None).  Takes what help_crack.py:508,575 pass --
+    ``--stdout --quiet -w 4 -o <out> -r <rules> <wordlist>`` -- in hashcat's spellings (``-oFILE``, ``--outfile=``,
+    ``--rules-file``, ``-w4``, ``--workload-profile``); options that do not change the candidates (``--quiet``,
+    ``-w``, ``--session``, ``--potfile-disable``, ...) are accepted and ignored.  Anything that would (masks,
+    ``-a``, ``-j``/``-k``, ``-g`` random rules, ...) raises HashcatArgError."""
+    rules, words, out = [], [], None
+    ignore_flag = {"--stdout", "--quiet", "--potfile-disable", "--logfile-disable", "--advice-disable", "-O",
+                   "--optimized-kernel-enable", "--force", "--status", "--machine-readable"}
+    ignore_val = {"-w", "--workload-profile", "--session", "-d", "--backend-devices", "--status-timer",
+                  "--outfile-format"}
+    i, toks = 1, list(argv)
+    while i < len(toks):
+        t = toks[i]
+        if t in ignore_flag or t.startswith("--session=") or t.startswith("--workload-profile="):
+            i += 1
+        elif t in ignore_val:
+            i += 2
+        elif t.startswith("-w") and t[2:].isdigit():
+            i += 1
+        elif t in ("-o", "--outfile"):
+            out = toks[i + 1] if i + 1 < len(toks) else None
+            i += 2
+        elif t.startswith("--outfile="):
+            out = t.split("=", 1)[1]
+            i += 1
+        elif t.startswith("-o") and len(t) > 2:
+            out = t[2:]
+            i += 1
+        elif t in ("-r", "--rules-file"):
+            if i + 1 >= len(toks):
+                raise HashcatArgError(f"{t} needs a file")
+            rules.append(toks[i + 1])
+            i += 2
+        elif t.startswith("--rules-file="):
+            rules.append(t.split("=", 1)[1])
+            i += 1
+        elif t.startswith("-r") and len(t) > 2:
+            rules.append(t[2:])
+            i += 1
+        elif t.startswith("-") and t != "-":
+            raise HashcatArgError(f"option {t} is not supported by the GPU --stdout replacement")
+        else:
+            words.append(t)
+            i += 1
+    if not words:
+        raise HashcatArgError("no wordlist")
+    if len(rules) > 1:
+        raise HashcatArgError("stacked -r rule files are not supported (help_crack passes one)")
+    return rules, words, out
+
+
+def is_hashcat_stdout(argv) -> bool:
+    return bool(argv) and os.path.basename(str(argv[0])) in HASHCAT_NAMES and "--stdout" in argv
+
+
+def hashcat_stdout(argv, device: int = 0, pprint=None) -> int:
+    """Run a `hashcat --stdout [-r rules] [-o out] wordlists...` command line (help_crack.py:508, :575) on the GPU:
+    every word x every rule, written word-major as hashcat writes it (expand_rules).  Without -r every word is
+    written once (the ':' rule); without -o the candidates go to stdout.  Returns 0, or -1 with a message (a bad
+    command line, an unreadable wordlist or rules file), as hashcat fails."""
+    pprint = pprint or (lambda mess, code="HEADER": print(mess, file=sys.stderr))
+    try:
+        rules, words, out = parse_hashcat_stdout(argv)
+    except HashcatArgError as e:
+        pprint(f"hashcat --stdout replacement: {e}", "FAIL")
+        return -1
+    tmp = []
+    try:
+        if not rules:
+            fd, noop = tempfile.mkstemp(suffix=".rule")
+            os.write(fd, b":\n")
+            os.close(fd)
+            tmp.append(noop)
+            rules = [noop]
+        target = out
+        if out is None:
+            fd, target = tempfile.mkstemp(suffix=".txt")
+            os.close(fd)
+            tmp.append(target)
+        M.rules_expand_file(rules[0], words, target, 0, device)
+        if out is None:
+            with open(target, "rb") as f:
+                shutil.copyfileobj(f, sys.stdout.buffer)
+            sys.stdout.flush()
+        return 0
+    except L.DwpaError as e:
+        pprint(f"hashcat --stdout replacement failed: {e}", "FAIL")
+        return -1
+    finally:
+        for t in tmp:
+            if os.path.exists(t):
+                os.unlink(t)
+
+
+class SubprocessShim:
+    """help_crack's module-level ``subprocess`` after install(): ``call`` answers a ``hashcat --stdout`` command line
+    (help_crack.py:508-509 expandcracked, :575-576 prdict) with hashcat_stdout on the GPU; every other attribute and
+    call is the real module's (hcxpsktool :645, imeigen :684 run as before)."""
+
+    def __init__(self, real, device: int = 0):
+        self._real = real
+        self._device = device
+
+    def __getattr__(self, name):
+        return getattr(self._real, name)
+
+    def call(self, args, *a, **kw):
+        argv = shlex.split(args) if isinstance(args, str) else list(args)
+        if is_hashcat_stdout(argv):
+            return hashcat_stdout(argv, self._device)
+        return self._real.call(args, *a, **kw)
+
+
+def install(helpcrack_cls, device: int = 0):
+    """Bind the GPU engine into help_crack's ``HelpCrack`` class (help_crack/help_crack.py:56) and module, so that
+    ``HelpCrack.run()`` (:881-957) runs end to end on a box with no hashcat or john binary:
+
+    * ``check_tools`` (:191-307): no binary search; exits like the original (:288-290) when no gfx950 device is
+      usable, else sets ``conf["cracker"]`` and ``conf["format"] = "22000"`` and returns the cracker name;
+    * ``run_cracker`` (:765-802): dwpa_amd.help_crack.run_cracker over ``self.conf``, with the instance's
+      ``sleepy``/``pprint`` and ``disablestdout`` as ``quiet``;
+    * the module's ``subprocess`` becomes a SubprocessShim, so the ``hashcat --stdout`` expansions of
+      ``expandcracked`` (:508) and ``prepare_dicts`` (:575) run on the GPU (``device``) unchanged.
+
+    Idempotent.  Returns the class."""
+    module = sys.modules.get(helpcrack_cls.__module__)
+
+    def check_tools(self):
+        try:
+            ndev = M.device_count()
+        except L.DwpaError:
+            ndev = 0
+        if ndev < 1:
+            self.pprint("libdwpa22000: no usable gfx950 device (hashcat is not needed)", "FAIL")
+            sys.exit(1)
+        self.conf["cracker"] = CRACKER
+        self.conf["format"] = "22000"
+        return self.conf["cracker"]
+
+    def run_cracker_method(self, dictlist, disablestdout=False):
+        return run_cracker(self.conf, dictlist, sleepy=self.sleepy, pprint=self.pprint, quiet=disablestdout)
+
+    check_tools.__doc__ = "help_crack.py:191-307 without a cracker binary (dwpa_amd.help_crack.install)"
+    run_cracker_method.__doc__ = "help_crack.py:765-802 in-process on the GPU (dwpa_amd.help_crack.install)"
+    helpcrack_cls.check_tools = check_tools
+    helpcrack_cls.run_cracker = run_cracker_method
+    if module is not None and hasattr(module, "subprocess") and not isinstance(module.subprocess, SubprocessShim):
+        module.subprocess = SubprocessShim(module.subprocess, device)
+    return helpcrack_cls

@@ -134,6 +134,14 @@ class BatchJobs:
         return res
 
 
+def check_stats():
+    """dwpa_check_last_stats: {jobs, slots, pmks, tail_pmks, tail_waves, tail_waves_raised, hits, seconds} of this
+    thread's last check call."""
+    st = L.CheckStats()
+    L.check(L.load().dwpa_check_last_stats(ctypes.byref(st)), "check_last_stats")
+    return {k: getattr(st, k) for k, _ in L.CheckStats._fields_ if k != "reserved"}
+
+
 def check_batch(jobs):
     """jobs: iterable of (hashline, keys, pmk_or_False, nc).  Returns a list of check_key_m22000 results."""
     b = BatchJobs(jobs)
@@ -159,6 +167,15 @@ def rules_count(rules_text):
     L.check(L.load().dwpa_rules_count(rt, len(rt), ctypes.byref(present), ctypes.byref(parsed), ctypes.byref(first)),
             "rules_count")
     return present.value, parsed.value, first.value
+
+
+def rules_count_ex(rules_text) -> dict:
+    """Both loaders' counts (host only): {present, parsed (DWPA_RULES_FULL loads these), loaded_hashcat (hashcat's
+    -r loader keeps these), rejmem, invalid, first_invalid_line, first_rejmem_line}."""
+    rt = _b(rules_text)
+    c = L.RulesCounts()
+    L.check(L.load().dwpa_rules_count_ex(rt, len(rt), ctypes.byref(c)), "rules_count_ex")
+    return {k: getattr(c, k) for k, _ in L.RulesCounts._fields_ if k != "reserved"}
 
 
 def rules_apply_host(rules_text, rule_index: int, word):
@@ -208,16 +225,20 @@ def rules_expand(rules_text, words, device: int = 0):
 
 
 def crack_files(hash_file, dicts, rules_file=None, nonce_error_corrections: int = 8, out_file="help_crack.key",
-                device_mask: int = 0, batch: int = 0, nc_mode: int = L.DWPA_NC_HASHCAT) -> int:
-    """In-process hashcat -m22000 replacement; returns a hashcat exit code (0 cracked, 1 exhausted, -1 error)."""
+                device_mask: int = 0, batch: int = 0, nc_mode: int = L.DWPA_NC_HASHCAT,
+                rule_mode: int = L.DWPA_RULES_DEFAULT) -> int:
+    """In-process hashcat -m22000 replacement; returns a hashcat exit code (0 cracked, 1 exhausted, -1 error).
+    rule_mode: DWPA_RULES_DEFAULT (the process's: hashcat's -r loader unless DWPA_RULE_MODE=full), _HASHCAT or _FULL
+    (reject / memory lines run too)."""
     return crack_files_ex(hash_file, dicts, rules_file, nonce_error_corrections, out_file, device_mask, batch,
-                          nc_mode)[0]
+                          nc_mode, rule_mode)[0]
 
 
 def crack_files_ex(hash_file, dicts, rules_file=None, nonce_error_corrections: int = 8, out_file="help_crack.key",
-                   device_mask: int = 0, batch: int = 0, nc_mode: int = L.DWPA_NC_HASHCAT):
+                   device_mask: int = 0, batch: int = 0, nc_mode: int = L.DWPA_NC_HASHCAT,
+                   rule_mode: int = L.DWPA_RULES_DEFAULT):
     """crack_files plus one status per dictionary: (rc, [DWPA_DICT_OK | DWPA_DICT_DAMAGED | DWPA_E_IO])."""
-    cfg = L.Config(ctypes.sizeof(L.Config), device_mask, batch, nc_mode)
+    cfg = L.Config(ctypes.sizeof(L.Config), device_mask, batch, nc_mode, rule_mode)
     dl = [_b(d) for d in dicts]
     darr = (ctypes.c_char_p * max(1, len(dl)))(*dl)
     st = (ctypes.c_int32 * max(1, len(dl)))()
@@ -227,12 +248,13 @@ def crack_files_ex(hash_file, dicts, rules_file=None, nonce_error_corrections: i
 
 
 def crack_stats():
-    """dwpa_crack_last_stats: {words, candidates, hashes, cracked, seconds, rules, rules_skipped} of this thread's
-    last crack call."""
+    """dwpa_crack_last_stats: {words, candidates, hashes, cracked, seconds, rules, rules_skipped, rules_rejmem} of
+    this thread's last crack call."""
     st = L.CrackStats()
     L.check(L.load().dwpa_crack_last_stats(ctypes.byref(st)), "crack_last_stats")
     return {"words": st.words, "candidates": st.candidates, "hashes": st.hashes, "cracked": st.cracked,
-            "seconds": st.seconds, "rules": st.rules, "rules_skipped": st.rules_skipped}
+            "seconds": st.seconds, "rules": st.rules, "rules_skipped": st.rules_skipped,
+            "rules_rejmem": st.rules_rejmem}
 
 
 class Scan:

@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define DWPA_ABI_VERSION 2   /* 2: dwpa_crack_stats.rules / rules_skipped, dwpa_rules_count */
+#define DWPA_ABI_VERSION 3   /* 2: dwpa_crack_stats.rules / rules_skipped, dwpa_rules_count; 3: dwpa_check_last_stats,
+                                dwpa_config.rule_mode, dwpa_rules_count_ex, dwpa_crack_stats.rules_rejmem */
 
 /* ---- return codes ------------------------------------------------------------------------------------------ */
 #define DWPA_MISS 0            /* no key matched (PHP: False)                                                 */
@@ -52,6 +53,15 @@ extern "C" {
 #define DWPA_RC_CRACKED 0      /* every hashline cracked                                                       */
 #define DWPA_RC_EXHAUSTED 1    /* keyspace exhausted, not every hashline cracked                               */
 #define DWPA_RC_ERROR (-1)
+
+/* rule-file loading (dwpa_config.rule_mode; dwpa_crack_files' -r rules and dwpa_rules_expand_file) */
+#define DWPA_RULES_DEFAULT 0   /* the process's mode: dwpa_init's rule_mode, else DWPA_RULE_MODE=full|hashcat from the
+                                  environment, else DWPA_RULES_HASHCAT                                            */
+#define DWPA_RULES_HASHCAT 1   /* hashcat's -r loader: a line using a reject function (< > _ ! / ( ) = % Q) or a memory
+                                  function (M 4 6 X) is skipped and counted like an invalid one -- those work only
+                                  with -j/-k -- so the candidates are exactly the ones hashcat -r tries (default)  */
+#define DWPA_RULES_FULL 2      /* every line of the whole rule language runs, reject and memory functions included (a
+                                  superset of hashcat -r's candidates)                                             */
 
 /* nonce-error-correction semantics */
 #define DWPA_NC_PHP 0          /* common.php:250-300: N+0, then V+k,V-k,N+k,N-k for k = 1..(nc>>1)+1, $n mutated */
@@ -86,7 +96,8 @@ typedef struct {
     uint32_t device_mask;      /* bit d = use device d; 0 = all visible devices */
     uint32_t batch;            /* candidate slots per device per launch; 0 = auto */
     int32_t nc_mode;           /* DWPA_NC_PHP or DWPA_NC_HASHCAT (crack_files default: HASHCAT) */
-    int32_t reserved[4];
+    int32_t rule_mode;         /* DWPA_RULES_DEFAULT (0) / _HASHCAT / _FULL (ABI 3; was reserved[0]) */
+    int32_t reserved[3];
 } dwpa_config;
 
 typedef struct {
@@ -118,6 +129,23 @@ int dwpa_check_m22000(const char *line, size_t line_len, const dwpa_bytes *keys,
  * each (ESSID, key) PMK is derived once.  rcs[i] / out[i] as for dwpa_check_m22000.  Returns 0 or a
  * negative code if the whole batch failed (device error). */
 int dwpa_check_batch(const dwpa_job *jobs, size_t njobs, dwpa_result *out, int *rcs);
+/* What the calling thread's last dwpa_check_m22000 / dwpa_check_batch call did (ABI 3): its jobs, the non-null keys
+ * of usable lines (slots), the (ESSID, key) PMKs derived after deduplication, how many of those the tail launch
+ * derived (the remainder under one wave per SIMD, run beside the head at low wave priority), the tail's waves and
+ * how many of them saw the head end and raised their priority (DWPA_TAIL_PRIO), the hits, and the call's wall time.
+ * Returns 0, or DWPA_E_ARG before any check call in this thread. */
+typedef struct {
+    uint32_t jobs;
+    uint32_t slots;
+    uint32_t pmks;
+    uint32_t tail_pmks;
+    uint32_t tail_waves;
+    uint32_t tail_waves_raised;
+    uint32_t hits;
+    uint32_t reserved;
+    double seconds;
+} dwpa_check_stats;
+int dwpa_check_last_stats(dwpa_check_stats *out);
 
 /* ---- primitives exposed for parity tests and wrappers ------------------------------------------------------ */
 /* PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes, no $HEX[] decoding). */
@@ -183,12 +211,18 @@ typedef struct {
     uint32_t cracked;
     double seconds;
     uint32_t rules;            /* rules loaded from rules_file (ABI 2) */
-    uint32_t rules_skipped;    /* rule lines of rules_file that did not parse (ABI 2) */
+    uint32_t rules_skipped;    /* rule lines of rules_file skipped: not parsing, or (DWPA_RULES_HASHCAT) using reject /
+                                  memory functions (ABI 2) */
+    uint32_t rules_rejmem;     /* of rules_skipped, the lines skipped for reject / memory functions (ABI 3) */
+    uint32_t reserved;
 } dwpa_crack_stats;
 int dwpa_crack_last_stats(dwpa_crack_stats *out);
 
 /* hashcat rules (the whole rule language of hashcat >= 6.2.6: every mangling, reject and memory function; one
- * rule per line, '#' comments; semantics in dwpa_amd/csrc/rules.hpp and oracle/rules.py).
+ * rule per line, '#' comments; semantics in dwpa_amd/csrc/rules.hpp and oracle/rules.py).  The text entry points
+ * below (dwpa_rules_expand, dwpa_rules_apply_host, dwpa_rules_count, dwpa_scan_set_rules) are the interpreter and
+ * take every function; the rules *files* of dwpa_crack_files and dwpa_rules_expand_file go through hashcat's -r
+ * loader rule unless DWPA_RULES_FULL (dwpa_config.rule_mode / dwpa_init / DWPA_RULE_MODE=full) is selected.
  * GPU rule application (replaces `hashcat --stdout -r rules words`, help_crack.py:508,575): out holds
  * nwords*nrules candidates of 256 bytes (word-major), out_len their lengths (0xFFFFFFFF = the input word or a
  * reject / memory function rejected it).  With out == NULL only *nrules_out is set (number of rules that parse).
@@ -196,9 +230,12 @@ int dwpa_crack_last_stats(dwpa_crack_stats *out);
 int dwpa_rules_expand(int device, const char *rules_text, size_t rules_len, const dwpa_bytes *words, size_t nwords,
                       uint8_t *out, uint32_t *out_len, uint32_t *nrules_out);
 /* `hashcat --stdout -r rules_file sources... -o out_path` (help_crack.py:508 expandcracked, :575 prdict): every word of
- * the sources (plain or gzip, one per line, $HEX[] decoded) x every rule of rules_file, expanded on `device`, written
- * to out_path one candidate per line in word-major order, rejected candidates skipped, as hashcat writes plains
- * ($HEX[..] when a byte is outside 0x20..0x7e); gzip_level 0 = plain text (what hashcat writes), 1..9 = gzip.
+ * the sources (plain or gzip, one per line, $HEX[] decoded) x every rule of rules_file (loaded under the process's
+ * rule mode, DWPA_RULES_HASHCAT unless dwpa_init / DWPA_RULE_MODE chose full), expanded on `device`, written to
+ * out_path one candidate per line in word-major order, rejected candidates skipped, raw bytes as hashcat's --stdout
+ * writes them -- except a candidate holding '\n' or '\r', which would not survive as one line and is written as
+ * $HEX[..] (the dictionary readers decode it; hashcat would have split it); gzip_level 0 = plain text (what hashcat
+ * writes), 1..9 = gzip.
  * Counts the words read and the candidates written.  Returns 0 or a negative code (DWPA_E_IO: a source cannot be
  * opened or the output cannot be written; DWPA_E_RULE: no valid rule). */
 int dwpa_rules_expand_file(int device, const char *rules_file, const char *const *sources, size_t nsources,
@@ -211,6 +248,19 @@ int dwpa_rules_apply_host(const char *rules_text, size_t rules_len, uint32_t rul
  * number of the first one that does not (0 = none). */
 int dwpa_rules_count(const char *rules_text, size_t rules_len, uint32_t *nrules_present, uint32_t *nrules_parsed,
                      uint32_t *first_skipped_line);
+/* Host only (ABI 3): both loaders' counts for one rules text -- what DWPA_RULES_FULL loads (parsed) and what
+ * hashcat's -r loader (DWPA_RULES_HASHCAT) keeps (loaded_hashcat = parsed - rejmem). */
+typedef struct {
+    uint32_t present;             /* rule lines (neither empty nor '#' comments)                               */
+    uint32_t parsed;              /* lines that parse in the whole language: DWPA_RULES_FULL loads these        */
+    uint32_t loaded_hashcat;      /* parsed lines free of reject / memory functions: DWPA_RULES_HASHCAT loads these */
+    uint32_t rejmem;              /* parsed lines using a reject or memory function                            */
+    uint32_t invalid;             /* lines that do not parse (skipped in both modes)                           */
+    uint32_t first_invalid_line;  /* 1-based line numbers, 0 = none                                            */
+    uint32_t first_rejmem_line;
+    uint32_t reserved;
+} dwpa_rules_counts;
+int dwpa_rules_count_ex(const char *rules_text, size_t rules_len, dwpa_rules_counts *out);
 
 /* ---- device-resident scan API (inputs already in HBM; used by the client loop and bench.py) --------------- */
 typedef struct dwpa_scan dwpa_scan;

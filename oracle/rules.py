@@ -26,9 +26,10 @@ processor's bounds.  Conventions:
   * Spaces between functions are ignored; a line of spaces is the no-op rule.  Lines starting with '#' and empty
     lines are not rules.  Any other line that does not parse completely is skipped (hashcat: "Skipping invalid or
     unsupported rule"), and counted.
-hashcat's own rule-file loader accepts only functions its GPU rule engine has (not the reject and memory
-functions, which work only with -j/-k); this engine runs those lines too, a superset: a candidate it adds can only
-be an extra hit that the server re-verifies (web/common.php:902), never a lost one.
+hashcat's own rule-file loader (-r) accepts only functions its GPU rule engine has -- not the reject functions
+(< > _ ! / ( ) = % Q) nor the memory functions (M 4 6 X), which work only with -j/-k -- and skips such a line like
+an invalid one: `hashcat_loads` below.  The library's rule files follow it by default (DWPA_RULES_HASHCAT); its
+DWPA_RULES_FULL mode runs those lines too, a superset.
 """
 from __future__ import annotations
 
@@ -102,6 +103,16 @@ def parse(line: str):
         else:
             return None
     return ops or [(":", 0, 0, 0)]
+
+
+REJECT_OPS = set("<>_!/()=%Q")
+MEMORY_OPS = set("M46X")
+
+
+def hashcat_loads(line: str) -> bool:
+    """Whether hashcat's -r loader keeps this rule line: it parses and uses no reject or memory function."""
+    ops = parse(line)
+    return ops is not None and not any(op in REJECT_OPS | MEMORY_OPS for op, *_ in ops)
 
 
 def count(lines):

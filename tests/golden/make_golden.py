@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 
 from oracle import oracle as O  # noqa: E402
-from dwpa_amd import synth as S  # noqa: E402
+from tests import synth as S  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 

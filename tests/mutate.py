@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import random
 
-from dwpa_amd import synth as S
+from tests import synth as S
 
 TYPES = [b"01", b"02", b"1", b"2", b"001", b"002", b" 1", b"2 ", b"+1", b"1.0", b"2e0", b"0x1", b"", b"3", b"00",
          b"1 ", b" 02", b"02.", b".2e1", b"-1", b"1e", b"01\t", b"\n2"]

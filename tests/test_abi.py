@@ -8,7 +8,7 @@ import pytest
 
 from dwpa_amd import _lib as L
 from oracle import oracle as O
-from dwpa_amd import synth as S
+from tests import synth as S
 
 
 def declared_symbols():
@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     lib = L.load()
-    assert lib.dwpa_abi_version() == 2  # 2: dwpa_crack_stats.rules / rules_skipped, dwpa_rules_count
+    assert lib.dwpa_abi_version() == 3  # 3: dwpa_check_last_stats, rule_mode, dwpa_rules_count_ex, rules_rejmem
     for code in [0, 1, -1, -2, -3, -4, -10, -12, -13, -14, -15, -16, -999]:
         assert lib.dwpa_strerror(code)
 

@@ -21,7 +21,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 import dwpa_amd  # noqa: E402
-from dwpa_amd import synth as S  # noqa: E402
+from tests import synth as S  # noqa: E402
 from dwpa_amd.device import Dictionary  # noqa: E402
 from dwpa_amd.rulesets import wpa_rules  # noqa: E402
 from oracle import oracle as O  # noqa: E402

@@ -17,7 +17,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 import dwpa_amd  # noqa: E402
-from dwpa_amd import synth as S  # noqa: E402
+from tests import synth as S  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
 THREADS = max(1, min(16, len(os.sched_getaffinity(0))))

@@ -13,7 +13,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 import dwpa_amd  # noqa: E402
-from dwpa_amd import synth as S  # noqa: E402
+from dwpa_amd import _lib as L  # noqa: E402
+from tests import synth as S  # noqa: E402
 from dwpa_amd.rulesets import wpa_rules  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 from oracle import rules as R  # noqa: E402
@@ -263,12 +264,18 @@ def test_rules_fuzz_gpu_vs_oracle():
     assert not bad, bad[:8]
 
 
-def test_crack_files_every_rule_family(tmp_path):
+@pytest.mark.parametrize("mode", ["hashcat", "full"])
+def test_crack_files_every_rule_family(tmp_path, mode):
     """A work unit whose server rule file (-S -r, help_crack.py:931-933) uses every family of the language beyond
     bestWPA.rule's ops -- insert/overwrite/extract/omit, swaps and byte arithmetic, block duplication, title case and
-    toggle-after-separator, reject functions, memory functions -- plus lines that do not parse.  A PSK planted
-    behind each family is found; a PSK only a rejected candidate would equal is not; the skipped lines are counted
-    in dwpa_crack_last_stats, not dropped silently."""
+    toggle-after-separator, reject functions, memory functions -- plus lines that do not parse.  The skipped lines are
+    counted in dwpa_crack_last_stats, not dropped silently.
+
+    * hashcat (the default, DWPA_RULES_HASHCAT): hashcat's -r loader skips the lines using reject or memory
+      functions (they work only with -j/-k), so exactly the PSKs behind the other families are found and the reject
+      / memory lines count as skipped (rules_rejmem) -- the reference client's `-S -r` run tries the same candidates.
+    * full (DWPA_RULES_FULL): every family runs and a PSK planted behind each one is found; a PSK only a rejected
+      candidate would equal is not."""
     rng = random.Random(21)
     essid, _, sta, _, _ = S.random_net(rng)
     base = [S.random_psk(rng, 6, 14) for _ in range(3000)]
@@ -300,9 +307,10 @@ def test_crack_files_every_rule_family(tmp_path):
     d = tmp_path / "d.txt"
     d.write_bytes(b"\n".join(base) + b"\n")
     out = tmp_path / "o.key"
-    rc = dwpa_amd.crack_files(str(hf), [str(d)], str(rf), 8, str(out), batch=1 << 16)
+    rmode = {"hashcat": L.DWPA_RULES_HASHCAT, "full": L.DWPA_RULES_FULL}[mode]
+    rc = dwpa_amd.crack_files(str(hf), [str(d)], str(rf), 8, str(out), batch=1 << 16, rule_mode=rmode)
     assert all(R.apply(R.parse(r), w) != never for r in rules + ["<8 $!"] for w in base)  # no candidate equals it
-    assert rc == 1  # every planted line cracked, the never line not
+    assert rc == 1  # the never line stays uncracked
     got = {}
     for rec in out.read_bytes().strip().split(b"\n"):
         f = rec.split(b":", 4)
@@ -310,9 +318,18 @@ def test_crack_files_every_rule_family(tmp_path):
         if v.startswith(b"$HEX[") and v.endswith(b"]"):
             v = bytes.fromhex(v[5:-1].decode())
         got[f[1].decode()] = v
-    assert got == {k: v for k, v in planted.items()}
+    rejmem = {"reject", "reject_eq", "memory", "memory_x", "memory_q"}
+    kept = [n for n in family if mode == "full" or n not in rejmem]
+    aps = list(planted)
+    assert got == {aps[k]: planted[aps[k]] for k, n in enumerate(family) if n in kept}
     st = dwpa_amd.m22000.crack_stats()
-    assert (st["rules"], st["rules_skipped"]) == (len(rules) + 1, len(invalid))
+    if mode == "full":
+        assert (st["rules"], st["rules_skipped"], st["rules_rejmem"]) == (len(rules) + 1, len(invalid), 0)
+    else:  # the five reject / memory families and the '<8 $!' line
+        assert (st["rules"], st["rules_skipped"], st["rules_rejmem"]) == (len(kept), len(invalid) + 6, 6)
+    counts = dwpa_amd.rules_count_ex(rf.read_bytes())
+    assert (counts["parsed"], counts["loaded_hashcat"], counts["rejmem"], counts["invalid"]) == \
+        (len(rules) + 1, len(rules) + 1 - 6, 6, len(invalid))
 
 
 def test_crack_files_challenge(tmp_path):
@@ -537,8 +554,9 @@ def test_help_crack_truncated_dictionary_no_livelock(tmp_path):
 
 
 def _stdout_plain(c: bytes) -> bytes:
-    """hashcat's --stdout form of a candidate: $HEX[..] for bytes outside 0x20..0x7e or a literal $HEX[ prefix."""
-    if c.startswith(b"$HEX[") or any(b < 0x20 or b > 0x7E for b in c):
+    """hashcat's --stdout form of a candidate: its raw bytes; one holding '\\n' or '\\r' (which would not stay one
+    line) as $HEX[..]."""
+    if b"\n" in c or b"\r" in c:
         return b"$HEX[" + c.hex().encode() + b"]"
     return c
 
@@ -547,13 +565,15 @@ def _stdout_plain(c: bytes) -> bytes:
 def test_help_crack_expand_rules_file(tmp_path, gzip_level):
     """`hashcat --stdout -r bestWPA.rule source.txt -o cracked.txt.gz` (help_crack.py:508) via the GPU rule engine
     and the library's packing (dwpa_rules_expand_file): the output equals the rule oracle's expansion in word-major
-    order with rejected candidates skipped and non-printable candidates as $HEX[] -- over 20k words x 148 rules
-    (3M candidates: several sub-batches, both slot sets), $HEX[] source words decoded, a 300-byte word rejected.
-    Plain text (what hashcat writes) and gzip.  Parity with hashcat itself unpinned."""
+    order with rejected candidates skipped, raw bytes as hashcat's --stdout writes them and $HEX[] only for a
+    candidate holding a newline -- over 20k words x 148 rules (3M candidates: several sub-batches, both slot sets),
+    $HEX[] source words decoded, a 300-byte word rejected.  Plain text (what hashcat writes) and gzip.  Parity with
+    hashcat itself unpinned."""
     from dwpa_amd.help_crack import expand_rules
     rng = random.Random(32)
     words = [S.random_psk(rng, 1, 20) for _ in range(20000)] + [b"x" * 300]
     words[7] = b"\x00\xffAb"
+    words[9] = b"ab\ncd\rxy"
     rules = wpa_rules()
     src = tmp_path / "source.txt"
     src.write_bytes(b"\n".join(b"$HEX[" + w.hex().encode() + b"]" if any(b < 0x20 or b > 0x7E for b in w) else w
@@ -569,7 +589,7 @@ def test_help_crack_expand_rules_file(tmp_path, gzip_level):
     got = raw.split(b"\n")[:-1]
     assert n == len(exp) and len(got) == len(exp)
     assert got == exp
-    assert any(g.startswith(b"$HEX[00ff") for g in got)
+    assert any(g.startswith(b"\x00\xffAb") for g in got) and any(g.startswith(b"$HEX[61620a6364") for g in got)
 
 
 def test_crack_files_several_dictionaries(tmp_path):
@@ -781,3 +801,26 @@ def test_issue_pass_kernels_at_small_sizes():
                        timeout=110)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " passed" in r.stdout
+
+
+@pytest.mark.parametrize("exit_on", ["1", "0"])
+def test_first_key_exit_across_chunks(exit_on):
+    """the first-key early exit of the attempt-parallel verify (first_hit) across chunks and segments.
+    Jobs at nc=128 (keyver 2 and 3, 261 attempts: attempt-parallel) whose PSK appears several times -- in one
+    segment, in several segments, and in later chunks of the call (dwpa_init batch = 128 slots, so 300-key jobs span
+    three chunks) -- with null keys in between: key_index is the first copy, and every result equals the CPU
+    oracle's, with the early exit on (default) and off (DWPA_FIRST_KEY_EXIT=0; one process each, the switch is read
+    once)."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, DWPA_FIRST_KEY_EXIT=exit_on)
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "first_key_child.py")], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["exit"] == exit_on
+    assert res["got"] == res["exp"] == res["single"]
+    assert res["key_index"] == res["first_copy"]
+    assert res["key_index"][:4] == [20, 140, 5, 299] and res["got"][4] is False

@@ -15,7 +15,7 @@ import pytest
 
 from dwpa_amd import _lib as L
 from dwpa_amd import help_crack as H
-from dwpa_amd import synth as S
+from tests import synth as S
 from dwpa_amd.help_crack import run_cracker
 
 

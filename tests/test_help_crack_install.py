@@ -1,0 +1,145 @@
+"""CPU: dwpa_amd.help_crack.install() on the reference client's HelpCrack (its test double, tests/helpcrack_standin.py).
+
+VERDICT r4 missing #1: without a hashcat binary, HelpCrack.run() stopped in check_tools (help_crack.py:286-290), and
+the two `hashcat.bin --stdout` expansions (:508, :575) still shelled out.  After install():
+
+* check_tools needs no binary on PATH; it sets conf["format"] = "22000" so prepare_work/prepare_dicts take their
+  m22000 branches (:441, :536, :571), and exits like the original when no gfx950 device is usable;
+* run_cracker is the in-process GPU call with the instance's sleepy/pprint;
+* help_crack's module-level subprocess answers exactly the two `--stdout` command lines with the GPU rule engine
+  and passes every other call (hcxpsktool, imeigen) to the real module.
+
+The device work itself is stubbed here (no GPU); tests/test_gpu_parity.py runs the same sequences on the GPU.
+"""
+import base64
+import importlib
+import os
+import shlex
+import subprocess
+import sys
+
+import pytest
+
+from dwpa_amd import _lib as L
+from dwpa_amd import help_crack as H
+
+
+@pytest.fixture
+def standin(monkeypatch, tmp_path):
+    """A fresh copy of the test double (its own class and its own module-level subprocess), in an empty cwd with no
+    hashcat or john on PATH."""
+    from tests import helpcrack_standin
+    mod = importlib.reload(helpcrack_standin)
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("PATH", str(tmp_path / "nobin"))
+    return mod
+
+
+def test_original_check_tools_exits_without_hashcat(standin):
+    hc = standin.HelpCrack()
+    with pytest.raises(SystemExit) as e:
+        hc.check_tools()
+    assert e.value.code == 1 and ("FAIL", "hashcat or john not found") in hc.log
+
+
+def test_installed_check_tools_sets_format_22000(standin, monkeypatch):
+    monkeypatch.setattr(H.M, "device_count", lambda: 1)
+    H.install(standin.HelpCrack)
+    hc = standin.HelpCrack()
+    assert hc.check_tools() == H.CRACKER
+    assert hc.conf["format"] == "22000" and hc.conf["cracker"] == H.CRACKER
+    # the m22000 branches follow: a gzip challenge dictionary (:705-708) and m22000 lines + rules (:441-447)
+    nd = hc.prepare_challenge()
+    assert nd["dictname"].endswith(".gz") and os.path.exists(nd["dictname"])
+    nd["rules"] = base64.b64encode(b"$1\nu").decode()
+    hc.prepare_work(nd)
+    assert open("help_crack.hash").read().splitlines() == nd["hashes"]
+    assert open("help_crack.rules", "rb").read() == b"$1\nu" and hc.conf["rules"] == "-S -r help_crack.rules"
+
+
+def test_installed_check_tools_without_device_exits(standin):
+    """This container has no GPU: the library answers DWPA_E_NODEV and check_tools exits 1 with a FAIL line, as the
+    original does when it finds no cracker."""
+    H.install(standin.HelpCrack)
+    hc = standin.HelpCrack()
+    with pytest.raises(SystemExit) as e:
+        hc.check_tools()
+    assert e.value.code == 1 and any(c == "FAIL" and "gfx950" in m for c, m in hc.log)
+
+
+def test_install_is_idempotent_and_keeps_other_subprocess_calls(standin):
+    H.install(standin.HelpCrack)
+    H.install(standin.HelpCrack)
+    shim = standin.subprocess
+    assert isinstance(shim, H.SubprocessShim) and not isinstance(shim._real, H.SubprocessShim)
+    # hcxpsktool-style calls reach the real module (PATH holds nothing here: absolute paths)
+    assert shim.call([sys.executable, "-c", "pass"]) == 0
+    assert shim.call(f"{sys.executable} -c 'raise SystemExit(3)'", shell=True) == 3
+    assert shim.PIPE is subprocess.PIPE and shim.run is subprocess.run
+
+
+def test_installed_run_cracker_binds_conf_and_quiet(standin, monkeypatch, capsys):
+    calls = []
+
+    def fake(hash_file, dicts, rules_file, nec, key_file, device_mask=0):
+        calls.append((hash_file, list(dicts), rules_file, nec, key_file, device_mask))
+        return 1, [L.DWPA_DICT_OK] * len(dicts)
+    monkeypatch.setattr(H.M, "crack_files_ex", fake)
+    monkeypatch.setattr(H.M, "crack_stats", lambda: {"words": 1, "candidates": 1, "hashes": 1, "cracked": 0,
+                                                     "seconds": 1.0, "rules": 0, "rules_skipped": 0})
+    H.install(standin.HelpCrack)
+    hc = standin.HelpCrack()
+    open("help_crack.hash", "w").write("x\n")
+    hc.conf["rules"] = "-S -r help_crack.rules"
+    hc.conf["coptions"] = "-d 2"
+    assert hc.run_cracker(["a.gz", "b.gz"], disablestdout=True) == 1
+    assert calls == [("help_crack.hash", ["a.gz", "b.gz"], "help_crack.rules", 8, "help_crack.key", 0b10)]
+    assert capsys.readouterr().out == ""  # disablestdout -> quiet
+    assert hc.run_cracker(["a.gz"]) == 1 and "Status...........: Exhausted" in capsys.readouterr().out
+
+
+@pytest.mark.parametrize("cmd", ["EXPAND_CRACKED", "EXPAND_PRDICT"])
+def test_shim_routes_the_reference_stdout_lines(standin, monkeypatch, cmd):
+    seen = []
+    monkeypatch.setattr(H.M, "rules_expand_file", lambda r, w, o, g, d: seen.append((r, list(w), o, g, d)) or (1, 1))
+    H.install(standin.HelpCrack, device=3)
+    line = getattr(standin, cmd)
+    assert standin.subprocess.call(shlex.split(line), stdout=None) == 0
+    out = "cracked.txt.gz" if cmd == "EXPAND_CRACKED" else "prdict.txt.gz"
+    assert seen == [("bestWPA.rule", ["source.txt"], out, 0, 3)]
+
+
+@pytest.mark.parametrize("argv,exp", [
+    ("hashcat --stdout -r r.rule w1 w2 -o out", (["r.rule"], ["w1", "w2"], "out")),
+    ("./hashcat.bin --stdout -oout --rules-file=r.rule -w4 --session x w", (["r.rule"], ["w"], "out")),
+    ("hashcat.bin --stdout --outfile=o --quiet w", ([], ["w"], "o")),
+    ("hashcat --stdout w", ([], ["w"], None)),
+])
+def test_parse_hashcat_stdout(argv, exp):
+    assert H.parse_hashcat_stdout(shlex.split(argv)) == exp
+
+
+@pytest.mark.parametrize("argv", ["hashcat --stdout -r a -r b w", "hashcat --stdout -a 3 w ?d?d",
+                                  "hashcat --stdout -o x", "hashcat --stdout -j u w"])
+def test_parse_hashcat_stdout_rejects(argv):
+    with pytest.raises(H.HashcatArgError):
+        H.parse_hashcat_stdout(shlex.split(argv))
+
+
+def test_hashcat_stdout_error_is_minus_one(tmp_path):
+    logs = []
+    assert H.hashcat_stdout(shlex.split("hashcat --stdout -r a -r b w"), pprint=lambda m, c="": logs.append(c)) == -1
+    assert logs == ["FAIL"]
+    # no GPU here: the library reports DWPA_E_IO/NODEV and the replacement fails like hashcat (rc -1), no traceback
+    (tmp_path / "r").write_text(":\n")
+    (tmp_path / "w").write_text("word\n")
+    assert H.hashcat_stdout(["hashcat", "--stdout", "-r", str(tmp_path / "r"), str(tmp_path / "w"), "-o",
+                             str(tmp_path / "o")], pprint=lambda m, c="": logs.append(c)) == -1
+
+
+def test_is_hashcat_stdout():
+    assert H.is_hashcat_stdout(["./hashcat.bin", "--stdout", "w"])
+    assert not H.is_hashcat_stdout(["./hashcat.bin", "-m22000", "h", "w"])
+    assert not H.is_hashcat_stdout(["./hcxpsktool", "--stdout"])
+    assert not H.is_hashcat_stdout([])
+    assert sys.modules["dwpa_amd.help_crack"] is H

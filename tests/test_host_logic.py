@@ -7,7 +7,7 @@ import pytest
 
 import dwpa_amd
 from dwpa_amd import _lib as L
-from dwpa_amd import synth as S
+from tests import synth as S
 from dwpa_amd.rulesets import wpa_rules
 from oracle import oracle as O
 from oracle import rules as R

@@ -5,7 +5,7 @@ import random
 import pytest
 
 from oracle import oracle as O
-from dwpa_amd import synth as S
+from tests import synth as S
 from tests.conftest import dec, job_args
 
 

@@ -25,6 +25,30 @@ def test_every_function_parses():
     assert (present, parsed, first) == (len(lines), len(lines), 0)
 
 
+def test_hashcat_loader_counts_vs_oracle():
+    """dwpa_rules_count_ex reports both loaders -- the whole language (DWPA_RULES_FULL) and
+    hashcat's -r loader (DWPA_RULES_HASHCAT, the default for rule files), which skips lines using reject or memory
+    functions -- equal to oracle/rules.py's parse / hashcat_loads, line by line, on the fuzz corpus and in bulk."""
+    rules = C.fuzz_rules() + C.single_function_rules() + C.memory_rules()
+    for r in rules:
+        c = dwpa_amd.rules_count_ex(r.encode("latin-1"))
+        ok = R.parse(r) is not None
+        assert (c["parsed"], c["loaded_hashcat"], c["rejmem"], c["invalid"]) == \
+            (int(ok), int(R.hashcat_loads(r)), int(ok and not R.hashcat_loads(r)), int(not ok)), r
+    text = "\n".join(rules).encode("latin-1")
+    c = dwpa_amd.rules_count_ex(text)
+    parsed = [r for r in rules if R.parse(r) is not None]
+    loads = [r for r in rules if R.hashcat_loads(r)]
+    assert c["present"] == R.count(rules)[0] and c["parsed"] == len(parsed) and c["loaded_hashcat"] == len(loads)
+    assert c["rejmem"] == len(parsed) - len(loads) > 0 and c["invalid"] == len(rules) - len(parsed) > 0
+    assert c["first_rejmem_line"] == 1 + next(i for i, r in enumerate(rules) if R.parse(r) and not R.hashcat_loads(r))
+    assert dwpa_amd.rules_count(text)[:2] == (c["present"], c["parsed"])  # the interpreter's count is the full one
+    # bestWPA.rule's ops (help_crack's --stdout expansion) use neither family: both loaders keep every line
+    from dwpa_amd.rulesets import wpa_rules
+    w = dwpa_amd.rules_count_ex("\n".join(wpa_rules()).encode())
+    assert w["parsed"] == w["loaded_hashcat"] == len(wpa_rules()) and w["rejmem"] == 0
+
+
 def test_invalid_rules_are_counted_not_dropped():
     bad = C.invalid_rules()
     assert all(R.parse(l) is None for l in bad), [l for l in bad if R.parse(l) is not None]

@@ -11,7 +11,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import dwpa_amd  # noqa: E402
-from dwpa_amd import synth as S  # noqa: E402
+from tests import synth as S  # noqa: E402
 from dwpa_amd.device import Dictionary, Event, Stream  # noqa: E402
 
 

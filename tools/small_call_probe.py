@@ -21,7 +21,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import dwpa_amd  # noqa: E402
-from dwpa_amd import synth as S  # noqa: E402
+from tests import synth as S  # noqa: E402
 
 KS = (1, 2, 16, 202)
 
