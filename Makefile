@@ -110,4 +110,5 @@ tools/bin/tail_placement: tools/tail_placement.hip
 # the parallel inflate (loader thread + workers + the reader) under ThreadSanitizer
 tools/bin/inflate_check_tsan: tools/inflate_check.cpp $(SRC)/inflate.hpp $(SRC)/pinflate.hpp
 	@mkdir -p tools/bin
-	g++ -O1 -g -std=c++17 -Wall -I$(SRC) -fsanitize=thread -o $@ tools/inflate_check.cpp -lz -lpthread
+	g++ -O1 -g -std=c++17 -Wall -I$(SRC) -fsanitize=thread -DDWPA_PINFLATE_LOAD_STEP=16384 -o $@ tools/inflate_check.cpp \
+	    -lz -lpthread

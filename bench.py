@@ -144,14 +144,22 @@ def parse():
                          "SIMDs, so the verify runs starved beside it -- and blurs the per-kernel events; default 1")
     ap.add_argument("--rule-words", type=int, default=1_000_000,
                     help="c3files: base words of the gz dictionary the WPA rule set is applied to")
-    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files", "c3files", "c1lat", "expand"],
+    ap.add_argument("--workload", choices=["c1", "c2", "c3", "c4", "c5", "c2files", "c3files", "c1lat", "c1cold",
+                                           "expand"],
                     default="c2",
                     help="c2 = BASELINE configs[1] (the bench line); c3/c4 = configs[2]/[3] legs; "
                          "c1/c5 = the FFI check path (host buffers, PCIe-inclusive); c2files = C2 through "
                          "dwpa_crack_files from a gz dictionary on disk (the help_crack client path); c3files = "
                          "the client's rule pass: a gz dictionary x the WPA rule set through dwpa_crack_files; "
-                         "c1lat = server call latency at 1/16/202 keys per call beside one CPU core; expand = "
-                         "help_crack's `hashcat --stdout -r` wordlist expansion (dwpa_rules_expand_file)")
+                         "c1lat = server call latency at 1/16/202 keys per call beside one CPU core; c1cold = the "
+                         "server path as PHP-FPM runs it: fresh worker processes, first-call cost, per-worker "
+                         "footprint, K concurrent workers; expand = help_crack's `hashcat --stdout -r` wordlist "
+                         "expansion (dwpa_rules_expand_file)")
+    ap.add_argument("--cold-role", choices=["parent", "worker", "context"], default="parent",
+                    help=argparse.SUPPRESS)  # c1cold: the child processes the parent starts
+    ap.add_argument("--cold-id", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--cold-k", default="4,16",
+                    help="c1cold: concurrent worker counts (each a fresh process; the box allows 16 GPU processes)")
     ap.add_argument("--rules-set", choices=["wpa", "server"], default="wpa",
                     help="c3files: the rules file -- wpa (148 rules of bestWPA.rule's ops) or server (those plus 67 "
                          "lines of the rest of hashcat's rule language: title case, inserts, memory, reject ...)")
@@ -453,6 +461,8 @@ def main():
     if os.environ.get("WORLD_SIZE") is None and (args.gpus or 1) > 1:
         sys.exit(spawn_ranks(args))
     quiet_stdout()
+    if args.workload == "c1cold":  # before anything touches the GPU: the parent never does
+        return {"parent": main_cold, "worker": cold_worker, "context": cold_context}[args.cold_role](args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus is not None and args.gpus != world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -968,6 +978,184 @@ def main_latency(args, world, rank, local):
                                                  "CPU core", "parallelism": "none"},
                           "rows": rows, "cpu_model": host_cpu()["cpu_model"], "hits_verified": ok})
     if rank == 0 and not ok:
+        sys.exit(3)
+
+
+def _proc_status(key):
+    try:
+        with open("/proc/self/status") as f:
+            return next((int(l.split()[1]) * 1024 for l in f if l.startswith(key + ":")), None)
+    except OSError:
+        return None
+
+
+def _hip_runtime():
+    """The HIP runtime library this process already maps (the one libdwpa22000.so loaded), else ROCm's."""
+    import ctypes
+    try:
+        with open("/proc/self/maps") as f:
+            path = next((l.split()[-1] for l in f if "libamdhip64.so" in l), None)
+    except OSError:
+        path = None
+    return ctypes.CDLL(path or os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so"))
+
+
+def _hip_mem_used(device=0):
+    """Device-wide bytes in use (hipMemGetInfo: total - free) through the HIP runtime already in this process."""
+    import ctypes
+    hip = _hip_runtime()
+    free, total = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    hip.hipSetDevice(device)
+    if hip.hipMemGetInfo(ctypes.byref(free), ctypes.byref(total)) != 0:
+        return None
+    return total.value - free.value
+
+
+def cold_context(args):
+    """c1cold child: a bare HIP context (hipInit + context creation, no library) and the device memory it holds --
+    what every process that touches the GPU pays before any library buffer."""
+    import ctypes
+    t0 = time.perf_counter()
+    hip = _hip_runtime()
+    assert hip.hipInit(0) == 0 and hip.hipSetDevice(0) == 0
+    assert hip.hipFree(None) == 0  # creates the context
+    t1 = time.perf_counter()
+    emit({"role": "context", "ms_runtime_and_context": round((t1 - t0) * 1e3, 2), "device_used_bytes": _hip_mem_used(),
+          "rss_bytes": _proc_status("VmRSS"), "threads": len(os.listdir("/proc/self/task"))})
+
+
+def cold_worker(args):
+    """c1cold child: one PHP-FPM worker's life in a fresh process (common.php:849 -> :902 per request): load the
+    library, make the first check call (HIP runtime + context, code-object load, the call context's buffers), the
+    second, then args.steps calls alternating one key against a PMKID line (put_work, :902) and 202 keys against an
+    EAPOL keyver-2 line at nc=128 (rkg.php:147 / a whole put_work candidate list).  Every result is checked."""
+    import random
+    from tests import synth as S
+    rng = random.Random(1000 + args.cold_id)
+    essid, ap, sta, an, sn = S.random_net(rng, essid_len=10)
+    psk = S.fast_psk(rng)
+    pmk = S.pmk(psk, essid)
+    one = (S.pmkid_line(psk, essid, ap, sta), [psk])
+    many = (S.eapol_line(psk, essid, ap, sta, an, sn, 2, -5, "BE", rng=rng), [S.fast_psk(rng) for _ in range(201)] + [psk])
+    exp_one, exp_many = [psk, None, None, pmk], [psk, -5, "BE", pmk]
+    t0 = time.perf_counter()
+    import dwpa_amd
+    from dwpa_amd import m22000 as M
+    dwpa_amd.load()
+    t_load = time.perf_counter() - t0
+    if args.start_at:
+        time.sleep(max(0.0, args.start_at - time.time()))
+    calls, errors = [], []
+
+    def call(kind):
+        line, keys = one if kind == "one" else many
+        t = time.perf_counter()
+        try:
+            r = dwpa_amd.check_key_m22000(line, keys)
+            ok = r == (exp_one if kind == "one" else exp_many)
+        except Exception as e:  # noqa: BLE001 -- an allocation or device failure is what K workers may hit
+            errors.append(repr(e)[:200])
+            ok = False
+        calls.append({"kind": kind, "ms": round((time.perf_counter() - t) * 1e3, 3), "ok": ok})
+    call("one")  # first call of the worker
+    call("one")  # second
+    for i in range(args.steps):
+        call("many" if i % 2 == 0 else "one")
+    res = M.resource_stats()
+    emit({"role": "worker", "id": args.cold_id, "ms_import_and_load": round(t_load * 1e3, 2), "calls": calls,
+          "errors": errors, "resources": res, "device_used_bytes": _hip_mem_used(),
+          "rss_bytes": _proc_status("VmRSS"), "locked_bytes": _proc_status("VmLck"),
+          "threads": len(os.listdir("/proc/self/task"))})
+
+
+def main_cold(args):
+    """--workload c1cold: the server path as PHP-FPM runs it.  Every PHP request reaches
+    check_key_m22000 in a pool worker (put_work.php:14 -> common.php:849 -> :902), and each worker process loads the
+    library and creates its own HIP context, call contexts and pinned staging.  This parent never touches the GPU;
+    it starts fresh child processes (never a re-exec) and reports:
+      * a bare context (runtime init + context, device memory it holds), 3 samples in turn;
+      * one worker at a time, 3 samples: library load, the first call (everything a cold worker pays), the second,
+        warm one-key and 202-key calls, and the worker's footprint (library device buffers and pinned memory by
+        dwpa_resource_stats, device-wide use by hipMemGetInfo, RSS, threads);
+      * K concurrent fresh workers (--cold-k, default 4 and 16; 16 also with DWPA_CALLS_PER_DEVICE=1 and
+        DWPA_HOST_THREADS=2, the many-worker setting): every call's latency and any failed call."""
+    import statistics
+    import subprocess
+
+    def spawn(role, i, env_extra=None, start_at=None, steps=None):
+        cmd = [sys.executable, os.path.abspath(__file__), "--workload", "c1cold", "--cold-role", role,
+               "--cold-id", str(i), "--steps", str(steps if steps is not None else args.steps)]
+        if start_at:
+            cmd += ["--start-at", repr(start_at)]
+        env = dict(os.environ, **(env_extra or {}))
+        return subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, text=True)
+
+    def collect(p, timeout=240):
+        out, err = p.communicate(timeout=timeout)
+        if p.returncode != 0:
+            raise SystemExit(f"c1cold child failed (rc {p.returncode}): {err[-2000:]}")
+        return json.loads(out.strip().splitlines()[-1])
+
+    def q(v, f):
+        v = sorted(v)
+        return round(v[min(len(v) - 1, int(f * len(v)))], 3) if v else None
+
+    ctx = [collect(spawn("context", i)) for i in range(3)]
+    seq = [collect(spawn("worker", i, steps=10)) for i in range(3)]
+    mib = 1 << 20
+    ctx_dev = statistics.median([c["device_used_bytes"] for c in ctx])
+    rows = {"context_only": {"ms_runtime_and_context": [c["ms_runtime_and_context"] for c in ctx],
+                             "device_used_mib": round(ctx_dev / mib, 1),
+                             "rss_mib": round(statistics.median([c["rss_bytes"] for c in ctx]) / mib, 1)},
+            "one_worker_at_a_time": []}
+    for w in seq:
+        c = w["calls"]
+        rows["one_worker_at_a_time"].append({
+            "ms_import_and_load": w["ms_import_and_load"], "ms_first_call": c[0]["ms"], "ms_second_call": c[1]["ms"],
+            "ms_one_key_warm_median": q([x["ms"] for x in c[2:] if x["kind"] == "one"], 0.5),
+            "ms_202_keys_warm_median": q([x["ms"] for x in c[2:] if x["kind"] == "many"], 0.5),
+            "library_device_mib": round(w["resources"]["device_bytes"] / mib, 1),
+            "library_pinned_host_mib": round(w["resources"]["pinned_host_bytes"] / mib, 1),
+            "device_used_mib_whole_device": round(w["device_used_bytes"] / mib, 1),
+            "device_used_mib_over_bare_context": round((w["device_used_bytes"] - ctx_dev) / mib, 1),
+            "rss_mib": round(w["rss_bytes"] / mib, 1), "threads": w["threads"],
+            "host_pool_threads": w["resources"]["host_pool_threads"],
+            "call_contexts_used": w["resources"]["call_contexts_used"], "all_ok": all(x["ok"] for x in c)})
+    conc = []
+    many_env = {"DWPA_CALLS_PER_DEVICE": "1", "DWPA_HOST_THREADS": "2"}
+    plans = [(int(k), {}) for k in args.cold_k.split(",") if k.strip()]
+    plans += [(k, many_env) for k, _ in plans if k >= 16]
+    for k, env in plans:
+        start = time.time() + 8.0  # every worker imported and loaded before the window opens
+        ps = [spawn("worker", 100 + i, env, start_at=start, steps=args.steps) for i in range(k)]
+        ws = [collect(p) for p in ps]
+        calls = [c for w in ws for c in w["calls"]]
+        first = [w["calls"][0]["ms"] for w in ws]
+        conc.append({
+            "workers": k, "env": env or "defaults",
+            "ms_first_call_median": q(first, 0.5), "ms_first_call_max": max(first),
+            "ms_one_key_median": q([c["ms"] for w in ws for c in w["calls"][1:] if c["kind"] == "one"], 0.5),
+            "ms_one_key_p95": q([c["ms"] for w in ws for c in w["calls"][1:] if c["kind"] == "one"], 0.95),
+            "ms_202_keys_median": q([c["ms"] for c in calls if c["kind"] == "many"], 0.5),
+            "ms_202_keys_p95": q([c["ms"] for c in calls if c["kind"] == "many"], 0.95),
+            "calls": len(calls), "failed_calls": sum(1 for c in calls if not c["ok"]),
+            "errors": sorted({e for w in ws for e in w["errors"]})[:5],
+            "library_device_mib_per_worker": round(statistics.median([w["resources"]["device_bytes"] for w in ws]) / mib, 1),
+            "library_pinned_host_mib_per_worker": round(
+                statistics.median([w["resources"]["pinned_host_bytes"] for w in ws]) / mib, 1),
+            "device_used_mib_whole_device_max": round(max(w["device_used_bytes"] for w in ws) / mib, 1),
+            "rss_mib_per_worker": round(statistics.median([w["rss_bytes"] for w in ws]) / mib, 1),
+            "threads_per_worker": statistics.median([w["threads"] for w in ws])})
+    first = [r["ms_first_call"] for r in rows["one_worker_at_a_time"]]
+    ok = all(r["all_ok"] for r in rows["one_worker_at_a_time"]) and all(c["failed_calls"] == 0 for c in conc)
+    emit({"metric": "ms, first check_key_m22000 call of a fresh PHP-FPM worker process (cold)",
+          "value": statistics.median(first), "unit": "ms", "n_gpus": 1, "steps": args.steps, "warmup": 0,
+          "higher_is_better": False, "dtype": "u32", "data": "synthetic",
+          "config": {"workload": "C1 cold: fresh worker processes (put_work.php:14 -> common.php:849,902), one key "
+                                 "vs a PMKID line and 202 keys vs an EAPOL keyver-2 line at nc=128",
+                     "parallelism": "processes"},
+          "rows": rows, "concurrent": conc, "cpu_model": host_cpu()["cpu_model"], "hits_verified": ok})
+    if not ok:
         sys.exit(3)
 
 

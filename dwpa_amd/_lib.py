@@ -58,6 +58,12 @@ class CheckStats(ctypes.Structure):
                 ("hits", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("seconds", ctypes.c_double)]
 
 
+class Resources(ctypes.Structure):
+    _fields_ = [("device_bytes", ctypes.c_uint64), ("pinned_host_bytes", ctypes.c_uint64),
+                ("host_pool_threads", ctypes.c_uint32), ("devices", ctypes.c_uint32), ("call_contexts", ctypes.c_uint32),
+                ("call_contexts_used", ctypes.c_uint32)]
+
+
 class RulesCounts(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in ("present", "parsed", "loaded_hashcat", "rejmem", "invalid",
                                                "first_invalid_line", "first_rejmem_line", "reserved")]
@@ -88,6 +94,7 @@ SIGNATURES = {
     "dwpa_check_batch": ([ctypes.POINTER(Job), ctypes.c_size_t, ctypes.POINTER(Result), ctypes.POINTER(ctypes.c_int)],
                          ctypes.c_int),
     "dwpa_check_last_stats": ([ctypes.POINTER(CheckStats)], ctypes.c_int),
+    "dwpa_resource_stats": ([ctypes.POINTER(Resources)], ctypes.c_int),
     "dwpa_pbkdf2_pmk": ([ctypes.POINTER(Bytes), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),
     "dwpa_hc_unhex": ([ctypes.c_char_p, ctypes.c_size_t, _P, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
     "dwpa_hash_m22000": ([ctypes.c_char_p, ctypes.c_size_t, _P], ctypes.c_int),

@@ -60,18 +60,26 @@ struct PhaseTrace {
         if (r_ < 0) return r_;     \
     } while (0)
 
+// What the library holds right now (dwpa_resource_stats): device buffers and pinned host memory.
+std::atomic<uint64_t> g_dev_bytes{0}, g_pinned_bytes{0};
+
 int DevBuf::ensure(size_t bytes) {
     if (n >= bytes && p) return 0;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
+    release();
     if (bytes == 0) bytes = 16;
-    if (hipMalloc(&p, bytes) != hipSuccess) return DWPA_E_NOMEM;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        p = nullptr;
+        return DWPA_E_NOMEM;
+    }
     n = bytes;
+    g_dev_bytes += n;
     return 0;
 }
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+        (void)hipFree(p);
+        g_dev_bytes -= n;
+    }
     p = nullptr;
     n = 0;
 }
@@ -85,11 +93,13 @@ struct PinnedArena {
     int reset(size_t bytes) {
         used = 0;
         if (cap >= bytes) return 0;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        if (hipHostMalloc((void**)&p, bytes, hipHostMallocDefault) != hipSuccess) return DWPA_E_NOMEM;
+        release();
+        if (hipHostMalloc((void**)&p, bytes, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return DWPA_E_NOMEM;
+        }
         cap = bytes;
+        g_pinned_bytes += cap;
         return 0;
     }
     template <typename T>
@@ -99,7 +109,10 @@ struct PinnedArena {
         return (T*)(p + off);
     }
     void release() {
-        if (p) (void)hipHostFree(p);
+        if (p) {
+            (void)hipHostFree(p);
+            g_pinned_bytes -= cap;
+        }
         p = nullptr;
         cap = used = 0;
     }
@@ -172,15 +185,19 @@ struct MappedHost {
             p = nullptr;
             return DWPA_E_NOMEM;
         }
+        cap = bytes;
+        g_pinned_bytes += cap;
         if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) {
             release();
             return DWPA_E_NOMEM;
         }
-        cap = bytes;
         return 0;
     }
     void release() {
-        if (p) (void)hipHostFree(p);
+        if (p) {
+            (void)hipHostFree(p);
+            g_pinned_bytes -= cap;
+        }
         p = nullptr;
         dev = nullptr;
         cap = 0;
@@ -431,6 +448,11 @@ class HostPool {
             if (task) task();
             else std::this_thread::yield();
         }
+    }
+
+    size_t workers() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return workers_;
     }
 
   private:
@@ -1588,6 +1610,20 @@ int dwpa_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* 
     if ((!jobs || !out || !rcs) && njobs) return DWPA_E_ARG;
     if (njobs == 0) return 0;
     return check_batch_impl(jobs, njobs, out, rcs);
+}
+
+int dwpa_resource_stats(dwpa_resources* out) {
+    if (!out) return DWPA_E_ARG;
+    memset(out, 0, sizeof(*out));
+    out->device_bytes = g_dev_bytes.load();
+    out->pinned_host_bytes = g_pinned_bytes.load();
+    out->host_pool_threads = (uint32_t)HostPool::get().workers();
+    std::lock_guard<std::mutex> lk(g_mu);
+    out->devices = (uint32_t)g_ndev;
+    for (auto& d : g_dev)
+        if (d->stream) out->call_contexts_used++;
+    out->call_contexts = (uint32_t)g_dev.size();
+    return 0;
 }
 
 int dwpa_check_last_stats(dwpa_check_stats* out) {

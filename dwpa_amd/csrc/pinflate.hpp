@@ -110,8 +110,12 @@ class ParallelGunzip {
         if (data_) munmap((void*)data_, maplen_);
     }
 
-    // The loader: the file in order, LOAD_STEP bytes per pread, publishing how far it got.
-    static constexpr size_t LOAD_STEP = 4u << 20;
+    // The loader: the file in order, LOAD_STEP bytes per pread, publishing how far it got (the ThreadSanitizer build
+    // uses 16 KiB steps, so boundary probes keep running into bytes still being loaded).
+#ifndef DWPA_PINFLATE_LOAD_STEP
+#define DWPA_PINFLATE_LOAD_STEP (4u << 20)
+#endif
+    static constexpr size_t LOAD_STEP = DWPA_PINFLATE_LOAD_STEP;
     void load(int fd, uint8_t* area) {
         size_t pos = 0;
         while (pos < n_ && !quit_flag_.load(std::memory_order_relaxed)) {
@@ -162,16 +166,33 @@ class ParallelGunzip {
         }
     }
 
+    // Input end a decoder may be given now: every byte it can read (its end plus GzipDecoder::PAD and a refill word)
+    // is below what the loader has published, so no read races the loader's pread into the same bytes.
+    size_t safe_end() const {
+        const size_t l = loaded_.load(std::memory_order_acquire);
+        constexpr size_t MARGIN = GzipDecoder::PAD + 16;
+        return l >= n_ ? n_ : (l > MARGIN ? l - MARGIN : 0);
+    }
+
     // first dynamic-block boundary in chunk j's bytes (NONE if there is none)
     uint64_t find(size_t j) {
         need((uint64_t)(j + 3) * chunk_);  // the chunk, and blocks probed from its end into the next ones
         const uint64_t b = (uint64_t)j * chunk_ * 8, e = (uint64_t)std::min(n_, (j + 1) * chunk_) * 8;
-        GzipDecoder dec(data_, n_, true);
+        size_t lim = safe_end();
+        auto dec = std::make_unique<GzipDecoder>(data_, lim, true);
         std::vector<uint16_t> scratch;
         for (uint64_t p = b; p < e; p++) {
             if (!GzipDecoder::maybe_dynamic(data_, p)) continue;
-            dec.start_block(p, nullptr, 0);
-            if (dec.probe_block(scratch)) return p;
+            for (;;) {
+                // a probe decodes a whole candidate block, which may run past the chunks loaded so far: the decoder
+                // sees only [0, lim), and a probe that reached lim is no verdict -- wait for more input, probe again
+                dec->start_block(p, nullptr, 0);
+                if (dec->probe_block(scratch)) return p;
+                if (lim >= n_ || dec->bit_pos() / 8 + 16 < lim) break;
+                need(lim + GzipDecoder::PAD + 16 + LOAD_STEP);
+                lim = safe_end();
+                dec = std::make_unique<GzipDecoder>(data_, lim, true);
+            }
         }
         return NONE;
     }

@@ -142,6 +142,14 @@ def check_stats():
     return {k: getattr(st, k) for k, _ in L.CheckStats._fields_ if k != "reserved"}
 
 
+def resource_stats():
+    """dwpa_resource_stats: {device_bytes, pinned_host_bytes, host_pool_threads, devices, call_contexts,
+    call_contexts_used} this process's library holds now (host only)."""
+    st = L.Resources()
+    L.check(L.load().dwpa_resource_stats(ctypes.byref(st)), "resource_stats")
+    return {k: getattr(st, k) for k, _ in L.Resources._fields_}
+
+
 def check_batch(jobs):
     """jobs: iterable of (hashline, keys, pmk_or_False, nc).  Returns a list of check_key_m22000 results."""
     b = BatchJobs(jobs)

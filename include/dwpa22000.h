@@ -146,6 +146,19 @@ typedef struct {
     double seconds;
 } dwpa_check_stats;
 int dwpa_check_last_stats(dwpa_check_stats *out);
+/* What this process's copy of the library holds right now (ABI 3; host only, never initialises a device): device
+ * buffers and pinned host memory of every call context, scan and crack call, the host pool's worker threads (grown
+ * on demand up to DWPA_HOST_THREADS - 1), and the call contexts (devices x DWPA_CALLS_PER_DEVICE) and how many of them
+ * have run a call.  For sizing PHP-FPM pools, where every worker process loads its own copy. */
+typedef struct {
+    uint64_t device_bytes;
+    uint64_t pinned_host_bytes;
+    uint32_t host_pool_threads;
+    uint32_t devices;
+    uint32_t call_contexts;
+    uint32_t call_contexts_used;
+} dwpa_resources;
+int dwpa_resource_stats(dwpa_resources *out);
 
 /* ---- primitives exposed for parity tests and wrappers ------------------------------------------------------ */
 /* PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes, no $HEX[] decoding). */
