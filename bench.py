@@ -158,7 +158,7 @@ def parse():
     ap.add_argument("--cold-role", choices=["parent", "worker", "context"], default="parent",
                     help=argparse.SUPPRESS)  # c1cold: the child processes the parent starts
     ap.add_argument("--cold-id", type=int, default=0, help=argparse.SUPPRESS)
-    ap.add_argument("--cold-k", default="4,16",
+    ap.add_argument("--cold-k", default="4,8,16",
                     help="c1cold: concurrent worker counts (each a fresh process; the box allows 16 GPU processes)")
     ap.add_argument("--rules-set", choices=["wpa", "server"], default="wpa",
                     help="c3files: the rules file -- wpa (148 rules of bestWPA.rule's ops) or server (those plus 67 "
@@ -989,6 +989,11 @@ def _proc_status(key):
         return None
 
 
+def _rss():
+    """Resident memory in MiB: total, anonymous, file-backed, shared (the HIP runtime maps device files)."""
+    return {k: round((_proc_status(k) or 0) / (1 << 20), 1) for k in ("VmRSS", "RssAnon", "RssFile", "RssShmem")}
+
+
 def _hip_runtime():
     """The HIP runtime library this process already maps (the one libdwpa22000.so loaded), else ROCm's."""
     import ctypes
@@ -1021,7 +1026,7 @@ def cold_context(args):
     assert hip.hipFree(None) == 0  # creates the context
     t1 = time.perf_counter()
     emit({"role": "context", "ms_runtime_and_context": round((t1 - t0) * 1e3, 2), "device_used_bytes": _hip_mem_used(),
-          "rss_bytes": _proc_status("VmRSS"), "threads": len(os.listdir("/proc/self/task"))})
+          "rss_bytes": _proc_status("VmRSS"), "rss_mib": _rss(), "threads": len(os.listdir("/proc/self/task"))})
 
 
 def cold_worker(args):
@@ -1043,8 +1048,13 @@ def cold_worker(args):
     from dwpa_amd import m22000 as M
     dwpa_amd.load()
     t_load = time.perf_counter() - t0
+    rss = {"loaded": _rss()}
     if args.start_at:
         time.sleep(max(0.0, args.start_at - time.time()))
+    t0 = time.perf_counter()
+    ndev = dwpa_amd.device_count()  # the HIP runtime's initialisation, split out of the first call
+    t_init = time.perf_counter() - t0
+    rss["runtime_init"] = _rss()
     calls, errors = [], []
 
     def call(kind):
@@ -1058,12 +1068,15 @@ def cold_worker(args):
             ok = False
         calls.append({"kind": kind, "ms": round((time.perf_counter() - t) * 1e3, 3), "ok": ok})
     call("one")  # first call of the worker
+    rss["first_call"] = _rss()
     call("one")  # second
     for i in range(args.steps):
         call("many" if i % 2 == 0 else "one")
+    rss["end"] = _rss()
     res = M.resource_stats()
-    emit({"role": "worker", "id": args.cold_id, "ms_import_and_load": round(t_load * 1e3, 2), "calls": calls,
-          "errors": errors, "resources": res, "device_used_bytes": _hip_mem_used(),
+    emit({"role": "worker", "id": args.cold_id, "ms_import_and_load": round(t_load * 1e3, 2),
+          "ms_runtime_init": round(t_init * 1e3, 2), "devices": ndev, "calls": calls,
+          "errors": errors, "resources": res, "device_used_bytes": _hip_mem_used(), "rss_mib": rss,
           "rss_bytes": _proc_status("VmRSS"), "locked_bytes": _proc_status("VmLck"),
           "threads": len(os.listdir("/proc/self/task"))})
 
@@ -1106,12 +1119,14 @@ def main_cold(args):
     ctx_dev = statistics.median([c["device_used_bytes"] for c in ctx])
     rows = {"context_only": {"ms_runtime_and_context": [c["ms_runtime_and_context"] for c in ctx],
                              "device_used_mib": round(ctx_dev / mib, 1),
-                             "rss_mib": round(statistics.median([c["rss_bytes"] for c in ctx]) / mib, 1)},
+                             "rss_mib": round(statistics.median([c["rss_bytes"] for c in ctx]) / mib, 1),
+                             "rss_mib_detail": ctx[0]["rss_mib"]},
             "one_worker_at_a_time": []}
     for w in seq:
         c = w["calls"]
         rows["one_worker_at_a_time"].append({
-            "ms_import_and_load": w["ms_import_and_load"], "ms_first_call": c[0]["ms"], "ms_second_call": c[1]["ms"],
+            "ms_import_and_load": w["ms_import_and_load"], "ms_runtime_init": w["ms_runtime_init"],
+            "ms_first_call": c[0]["ms"], "ms_second_call": c[1]["ms"], "rss_mib_by_stage": w["rss_mib"],
             "ms_one_key_warm_median": q([x["ms"] for x in c[2:] if x["kind"] == "one"], 0.5),
             "ms_202_keys_warm_median": q([x["ms"] for x in c[2:] if x["kind"] == "many"], 0.5),
             "library_device_mib": round(w["resources"]["device_bytes"] / mib, 1),
@@ -1124,7 +1139,10 @@ def main_cold(args):
     conc = []
     many_env = {"DWPA_CALLS_PER_DEVICE": "1", "DWPA_HOST_THREADS": "2"}
     plans = [(int(k), {}) for k in args.cold_k.split(",") if k.strip()]
-    plans += [(k, many_env) for k, _ in plans if k >= 16]
+    for k, _ in list(plans):
+        if k >= 8:  # the many-worker settings: one call context, two host threads, fewer HIP hardware queues
+            plans += [(k, many_env), (k, dict(many_env, GPU_MAX_HW_QUEUES="2")),
+                      (k, dict(many_env, GPU_MAX_HW_QUEUES="1"))]
     for k, env in plans:
         start = time.time() + 8.0  # every worker imported and loaded before the window opens
         ps = [spawn("worker", 100 + i, env, start_at=start, steps=args.steps) for i in range(k)]
@@ -1133,6 +1151,7 @@ def main_cold(args):
         first = [w["calls"][0]["ms"] for w in ws]
         conc.append({
             "workers": k, "env": env or "defaults",
+            "ms_runtime_init_median": q([w["ms_runtime_init"] for w in ws], 0.5),
             "ms_first_call_median": q(first, 0.5), "ms_first_call_max": max(first),
             "ms_one_key_median": q([c["ms"] for w in ws for c in w["calls"][1:] if c["kind"] == "one"], 0.5),
             "ms_one_key_p95": q([c["ms"] for w in ws for c in w["calls"][1:] if c["kind"] == "one"], 0.95),
