@@ -25,7 +25,6 @@ Usage: two lines in help_crack.py's ``__main__`` block, before ``hc = HelpCrack(
 """
 from __future__ import annotations
 
-import gzip
 import os
 import shlex
 import shutil

@@ -34,6 +34,12 @@ final class Dwpa22000
     const FIRST_DEVICE_ERROR = -10;  /* DWPA_E_NODEV; every code <= this is a device/runtime failure */
 
     private static $ffi = null;
+    /* whether this worker process has made a library call yet: its first one also initialises the HIP runtime, loads
+     * the code objects and creates the call context (bench.py --workload c1cold, INTEGRATION.md section 2) */
+    public static $warm = false;
+    /* a cold worker sends a derive to the GPU only from this many keys on: PHP's ~1.1 ms per key then costs about what
+     * the first call does (~0.2-0.3 s for a worker started alone, up to ~0.7 s in a start-up storm of 16) */
+    const COLD_MIN_KEYS = 256;
 
     public static function ffi()
     {
@@ -44,6 +50,7 @@ typedef struct { int32_t key_index; int32_t nc; int8_t endian; uint8_t nc_valid;
 typedef struct { const char *line; size_t line_len; const dwpa_bytes *keys; size_t nkeys; const uint8_t *pmk; int32_t nc; } dwpa_job;
 int dwpa_check_m22000(const char *line, size_t line_len, const dwpa_bytes *keys, size_t nkeys, const uint8_t *pmk, int nc, dwpa_result *out);
 int dwpa_check_batch(const dwpa_job *jobs, size_t njobs, dwpa_result *out, int *rcs);
+int dwpa_device_count(void);
 const char *dwpa_strerror(int code);
 CDEF;
             $lib = getenv('DWPA_LIB') ?: (defined('DWPA_LIB') ? DWPA_LIB : '/opt/dwpa/libdwpa22000.so');
@@ -138,6 +145,7 @@ function check_key_m22000_gpu($hashline, $keys, $pmk = False, $nc = 128)
     $res = $ffi->new('dwpa_result');
     $rc = $ffi->dwpa_check_m22000($hashline, strlen($hashline), $arr, count($vals),
                                   $pm === null ? null : FFI::addr($pm[0]), (int) $nc, FFI::addr($res));
+    Dwpa22000::$warm = true;
     if ($rc == Dwpa22000::HIT) {
         return Dwpa22000::result($vals, $res);
     }
@@ -189,6 +197,7 @@ function check_keys_m22000_gpu_batch($jobs)
         $out = $ffi->new("dwpa_result[$m]");
         $rcs = $ffi->new("int[$m]");
         $rc = $ffi->dwpa_check_batch($cj, $m, $out, $rcs);
+        Dwpa22000::$warm = true;
         foreach ($gpu as $s => $i) {
             // the whole batch failed (rc < 0), or this job did: the PHP check decides, never a silent False
             $jrc = $rc < 0 ? $rc : $rcs[$s];
@@ -220,6 +229,29 @@ function check_key_m22000_routed($hashline, $keys, $pmk = False, $nc = 128)
         if ($pmk ? $pmkid : count($keys) < 2) {
             return check_key_m22000_php($hashline, $keys, $pmk, $nc);
         }
+        // a worker's first library call pays the runtime start-up (round 5, profiles/r05/c1cold/): until then only
+        // a derive big enough to cost PHP as much goes to the GPU; caller-PMK checks (<= 1.8 ms in PHP) stay in PHP
+        if (!Dwpa22000::$warm && ($pmk || count($keys) < Dwpa22000::COLD_MIN_KEYS)) {
+            return check_key_m22000_php($hashline, $keys, $pmk, $nc);
+        }
     }
     return check_key_m22000_gpu($hashline, $keys, $pmk, $nc);
+}
+
+/* Optional, for pools that keep their workers (pm = static, pm.max_requests = 0): pay the start-up in this worker
+ * now -- the runtime, the code objects and the call context, through one one-key check of a fixed PMKID line (a
+ * miss) -- e.g. from an auto_prepend_file on the worker's first request, so that its later calls are all warm.
+ * Returns the number of usable gfx950 devices (0: none -- every check then goes to check_key_m22000_php). */
+function dwpa22000_warmup()
+{
+    $ffi = Dwpa22000::ffi();
+    $n = $ffi->dwpa_device_count();
+    if ($n > 0) {
+        $line = 'WPA*01*' . str_repeat('0', 32) . '*020000000001*020000000002*7761726d7570***';
+        [$arr, $keep, $vals] = Dwpa22000::keys(['warmup-key']);
+        $res = $ffi->new('dwpa_result');
+        $rc = $ffi->dwpa_check_m22000($line, strlen($line), $arr, 1, null, 128, FFI::addr($res));
+        Dwpa22000::$warm = $rc >= 0;
+    }
+    return max(0, $n);
 }

@@ -116,3 +116,21 @@ def test_routed_check_follows_the_latency_table():
     assert "strncmp($hashline, 'WPA*01*', 7) === 0" in body
     assert "$pmk ? $pmkid : count($keys) < 2" in body
     assert body.index("return check_key_m22000_php(") < body.index("return check_key_m22000_gpu(")
+
+
+def test_routed_check_accounts_for_the_cold_first_call():
+    """Round 5 (profiles/r05/c1cold/): a worker's first library call also starts the HIP runtime (~0.2-0.7 s), so a
+    cold worker routes only derives of >= COLD_MIN_KEYS keys to the GPU; every library call marks the worker warm;
+    dwpa22000_warmup() pays the start-up with one fixed one-key check and marks it warm only on success."""
+    src = _src()
+    body = _function(src, "check_key_m22000_routed")
+    assert "!Dwpa22000::$warm && ($pmk || count($keys) < Dwpa22000::COLD_MIN_KEYS)" in body
+    assert "const COLD_MIN_KEYS = 256;" in src
+    assert _function(src, "check_key_m22000_gpu").count("Dwpa22000::$warm = true;") == 1
+    assert _function(src, "check_keys_m22000_gpu_batch").count("Dwpa22000::$warm = true;") == 1
+    warm = _function(src, "dwpa22000_warmup")
+    assert "dwpa_device_count()" in warm and "Dwpa22000::$warm = $rc >= 0;" in warm
+    line = "WPA*01*" + "0" * 32 + "*020000000001*020000000002*7761726d7570***"
+    assert line.split("*")[3:6] == ["020000000001", "020000000002", "7761726d7570"]
+    import dwpa_amd
+    assert dwpa_amd.parse_m22000(line)["type"] == 1  # the warm-up line is a valid PMKID line
