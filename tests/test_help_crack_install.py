@@ -143,3 +143,20 @@ def test_is_hashcat_stdout():
     assert not H.is_hashcat_stdout(["./hcxpsktool", "--stdout"])
     assert not H.is_hashcat_stdout([])
     assert sys.modules["dwpa_amd.help_crack"] is H
+
+
+def test_hashcat_stdout_without_outfile_writes_stdout(monkeypatch, capfdbinary, tmp_path):
+    """`hashcat --stdout -r r w` with no -o: the candidates go to stdout, as hashcat writes them; without -r the
+    words are written once (a ':' rule file)."""
+    seen = []
+
+    def fake(rules, words, out, gz, dev):
+        seen.append(open(rules, "rb").read())
+        with open(out, "wb") as f:
+            f.write(b"cand1\ncand2\n")
+        return 1, 2
+    monkeypatch.setattr(H.M, "rules_expand_file", fake)
+    assert H.hashcat_stdout(["hashcat", "--stdout", str(tmp_path / "w")]) == 0
+    assert capfdbinary.readouterr().out == b"cand1\ncand2\n"
+    assert seen == [b":\n"]
+    assert not list(tmp_path.iterdir())  # no temporary file left behind
