@@ -163,6 +163,9 @@ def parse():
     ap.add_argument("--rules-set", choices=["wpa", "server"], default="wpa",
                     help="c3files: the rules file -- wpa (148 rules of bestWPA.rule's ops) or server (those plus 67 "
                          "lines of the rest of hashcat's rule language: title case, inserts, memory, reject ...)")
+    ap.add_argument("--rule-mode", choices=["hashcat", "full"], default="hashcat",
+                    help="c3files: the rules file's loader -- hashcat (default: lines with reject / memory functions "
+                         "are skipped, as hashcat's -r loader does) or full (they run too)")
     ap.add_argument("--essids", type=int, default=1000, help="c3: number of ESSIDs (BASELINE: 1000)")
     ap.add_argument("--scan-run", action="store_true",
                     help="c2/c4: derive + verify through dwpa_scan_run (the multi-group kernel C3 uses) instead of "
@@ -1313,8 +1316,12 @@ def main_files_rules(args, world, rank, local):
     plant_word = n - 1000
     word = text[int(ends[plant_word - 1]):int(ends[plant_word]) - 1].tobytes()
     row = dwpa_amd.rules_expand(rules_text, [word], device=local)[0]
-    good = [r for r, c in enumerate(row) if c is not None and 8 <= len(c) <= 63]
-    # wpa: a rule in the middle of the set; server: the last kept one (a memory / reject line of the added part)
+    # the rules this pass loads: all of them (full), or those hashcat's -r loader keeps (no reject / memory function)
+    loads = [args.rule_mode == "full" or dwpa_amd.rules_count_ex(r.encode("latin-1"))["loaded_hashcat"] == 1
+             for r in rules]
+    good = [r for r, c in enumerate(row) if c is not None and 8 <= len(c) <= 63 and loads[r]]
+    # wpa: a rule in the middle of the set; server: the last kept one (of the added part: a memory / reject line
+    # with --rule-mode full, a byte-arithmetic line under hashcat's loader)
     plant_rule = good[len(good) // 2] if args.rules_set == "wpa" else good[-1]
     psk = row[plant_rule]
     # candidates inside the filter per base-word length (rule output lengths depend on the input length only)
@@ -1343,11 +1350,13 @@ def main_files_rules(args, world, rank, local):
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        rc = dwpa_amd.crack_files(hpath, [dpath], rpath, 8, opath, device_mask=1 << local, batch=args.batch)
+        from dwpa_amd import _lib as L
+        rc = dwpa_amd.crack_files(hpath, [dpath], rpath, 8, opath, device_mask=1 << local, batch=args.batch,
+                                  rule_mode=L.DWPA_RULES_FULL if args.rule_mode == "full" else L.DWPA_RULES_HASHCAT)
         el = time.perf_counter() - t0
         st = dwpa_amd.m22000.crack_stats()
         reported = st["candidates"]
-        rules_loaded = (st["rules"], st["rules_skipped"])
+        rules_loaded = (st["rules"], st["rules_skipped"], st["rules_rejmem"])
         all_passes.append(round(el, 3))
         if rep >= args.warmup:
             times.append(el)
@@ -1371,7 +1380,8 @@ def main_files_rules(args, world, rank, local):
             "config": {"workload": f"client rule pass via dwpa_crack_files: {n}-word gzip dictionary x {len(rules)} "
                                    f"{args.rules_set} rules (rules file, amplified on the GPU, 8..63 filter), one "
                                    "EAPOL keyver-2 line, hashcat NC mode 8", "rule_words": n, "rules": len(rules),
-                       "rules_set": args.rules_set, "rules_loaded_skipped": list(rules_loaded),
+                       "rules_set": args.rules_set, "rule_mode": args.rule_mode,
+                       "rules_loaded_skipped_rejmem": list(rules_loaded),
                        "candidates_counted": "length-only count up to the plant" if args.rules_set == "wpa" else
                                              "the library's count of derived candidates (dwpa_crack_last_stats)",
                        "candidates_per_pass": cands, "candidates_reported_by_library": reported,
