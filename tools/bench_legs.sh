@@ -6,7 +6,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/legs}
 mkdir -p $OUT
-LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm c3files c3files_server expand"}
+LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm c3files c3files_server c3files_server_full expand"}
 for leg in $LEGS; do
   case $leg in
     peak)    OUT=$OUT/peak tools/regen_peak.sh > /dev/null ;;
@@ -28,6 +28,8 @@ for leg in $LEGS; do
                > $OUT/c3files.json 2> $OUT/c3files.err ;;
     c3files_server) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --rules-set server --steps 2 \
                --warmup 0 > $OUT/c3files_server.json 2> $OUT/c3files_server.err ;;
+    c3files_server_full) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --rules-set server \
+               --rule-mode full --steps 2 --warmup 0 > $OUT/c3files_server_full.json 2> $OUT/c3files_server_full.err ;;
     expand)  timeout -k 10 300 python3 bench.py --workload expand --rule-words 5000000 --steps 2 --warmup 1 \
                > $OUT/expand.json 2> $OUT/expand.err ;;
     *) echo "unknown leg $leg" >&2; exit 2 ;;
