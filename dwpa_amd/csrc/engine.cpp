@@ -227,6 +227,7 @@ struct Device {
     CheckScratch cs;               // check path: host-phase scratch
     std::vector<DedupPart> parts;  // check path: dedup output per host thread
     dwpa_check_stats stats{};      // check path: the current call's statistics (dwpa_check_last_stats)
+    std::atomic<bool> used{false}; // its streams exist (a call ran on it); read by dwpa_resource_stats
 };
 
 static std::mutex g_mu;
@@ -334,6 +335,7 @@ static int device_stream(Device& d) {
         HIPCHK(hipEventCreateWithFlags(&d.head_end, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.vs_go, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.vs_done, hipEventDisableTiming));
+        d.used.store(true, std::memory_order_release);
     }
     return 0;
 }
@@ -1621,7 +1623,7 @@ int dwpa_resource_stats(dwpa_resources* out) {
     std::lock_guard<std::mutex> lk(g_mu);
     out->devices = (uint32_t)g_ndev;
     for (auto& d : g_dev)
-        if (d->stream) out->call_contexts_used++;
+        if (d->used.load(std::memory_order_acquire)) out->call_contexts_used++;
     out->call_contexts = (uint32_t)g_dev.size();
     return 0;
 }
