@@ -1,6 +1,7 @@
 """A/B of dwpa_rules_expand_file between two builds of the library (GPU box): the same synthetic source as
 `bench.py --workload expand` (5M words of 6..16 printable bytes x the 148-rule WPA set), each library called through
-raw ctypes (no dwpa_amd signature table, so an older build loads too), alternating, `reps` times each.  Output goes
+raw ctypes (no dwpa_amd signature table, so an older build loads too), in alternating order (A B, B A, ...) with a
+sync between calls, `reps` times each.  Output goes
 to OUT_DIR (default: a temporary directory).  Prints one JSON line per call and a summary."""
 import ctypes
 import json
@@ -40,8 +41,11 @@ def main():
         handles.append(fn)
     src = (ctypes.c_char_p * 1)(spath.encode())
     res = {p: [] for p in libs}
-    for rep in range(reps + 1):  # rep 0 warms each library
-        for p, fn in zip(libs, handles):
+    for rep in range(reps + 1):  # rep 0 warms each library; the order alternates (A B, B A, ...)
+        order = list(zip(libs, handles))
+        if rep % 2:
+            order.reverse()
+        for p, fn in order:
             w, c = ctypes.c_uint64(0), ctypes.c_uint64(0)
             t0 = time.perf_counter()
             rc = fn(0, rpath.encode(), src, 1, opath.encode(), 0, ctypes.byref(w), ctypes.byref(c))
@@ -52,6 +56,8 @@ def main():
             if rep:
                 res[p].append(el)
             os.remove(opath)
+            os.sync()  # the next call starts without the last one's 10 GB of dirty pages still being written back
+            time.sleep(2)
     for x in (spath, rpath):
         os.remove(x)
     os.rmdir(tmp)
