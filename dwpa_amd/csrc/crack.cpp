@@ -427,12 +427,27 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     return sh.ncracked == sh.valid ? DWPA_RC_CRACKED : DWPA_RC_EXHAUSTED;
 }
 
+// Whether candidate p[0, n) holds a '\n' or '\r' byte.  Eight bytes per step (SWAR zero-byte test on p ^ 0x0a..
+// and p ^ 0x0d..): the candidate sits in its 256-byte expansion slot, so whole words up to the slot's end can be read;
+// bytes past n are masked off.  A byte-wise loop here cost ~25 % of a 740M-candidate expansion (profiles/r05/
+// expand_ab/).
+static inline bool has_line_break(const uint8_t* p, size_t n) {
+    constexpr uint64_t ONES = 0x0101010101010101ull, HIGHS = 0x8080808080808080ull;
+    for (size_t i = 0; i < n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        const uint64_t live = n - i >= 8 ? ~0ull : (1ull << (8 * (n - i))) - 1;
+        const uint64_t a = w ^ (0x0a * ONES), b = w ^ (0x0d * ONES);
+        if (((a - ONES) & ~a & HIGHS & live) | ((b - ONES) & ~b & HIGHS & live)) return true;
+    }
+    return false;
+}
+
 // One candidate as hashcat's --stdout writes it: the raw bytes and a newline.  A candidate holding '\n' or '\r'
 // would not survive as one line of a wordlist (hashcat's own output splits it), so it alone is written as $HEX[..],
-// which every dictionary reader here decodes back to the same bytes.
+// which every dictionary reader here decodes back to the same bytes.  p points into a 256-byte slot (n <= 256).
 static void stdout_plain(const uint8_t* p, size_t n, std::string& out) {
-    bool hex = false;
-    for (size_t i = 0; i < n && !hex; i++) hex = p[i] == '\n' || p[i] == '\r';
+    const bool hex = has_line_break(p, n);
     if (!hex) {
         out.append((const char*)p, n);
     } else {

@@ -1,8 +1,8 @@
-# round 5, calls f and g (g: alternating order, a sync between calls, 4 reps): the expand leg measured 15.8 s per 740M-candidate expansion in r05e against 10.15 s in round 4.
+# round 5, calls f, g (alternating order, a sync between calls, 4 reps) and h (after the SWAR line-break check): the expand leg measured 15.8 s per 740M-candidate expansion in r05e against 10.15 s in round 4.
 # Same box, same source, the round-4 library (ab/r04, built from a186d45) against this round's, alternating -- a
 # regression or the box?  Output on /tmp and on the repo's own filesystem.
 cd $GRAFT_REPO_ROOT
-O=${O:-gpurun_out/r05g}
+O=${O:-gpurun_out/r05h}
 mkdir -p $O
 guard() { case $1 in 0) ;; 124|134|137|139) echo "stop: rc $1" >&2; exit $1;; *) echo "fail: rc $1" >&2; exit 1;; esac; }
 df -h /tmp . > $O/df.txt 2>&1
