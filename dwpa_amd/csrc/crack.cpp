@@ -427,46 +427,14 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     return sh.ncracked == sh.valid ? DWPA_RC_CRACKED : DWPA_RC_EXHAUSTED;
 }
 
-// Whether candidate p[0, n) holds a '\n' or '\r' byte.  Eight bytes per step (SWAR zero-byte test on p ^ 0x0a..
-// and p ^ 0x0d..): the candidate sits in its 256-byte expansion slot, so whole words up to the slot's end can be read;
-// bytes past n are masked off.  A byte-wise loop here cost ~25 % of a 740M-candidate expansion (profiles/r05/
-// expand_ab/).
-static inline bool has_line_break(const uint8_t* p, size_t n) {
-    constexpr uint64_t ONES = 0x0101010101010101ull, HIGHS = 0x8080808080808080ull;
-    for (size_t i = 0; i < n; i += 8) {
-        uint64_t w;
-        memcpy(&w, p + i, 8);
-        const uint64_t live = n - i >= 8 ? ~0ull : (1ull << (8 * (n - i))) - 1;
-        const uint64_t a = w ^ (0x0a * ONES), b = w ^ (0x0d * ONES);
-        if (((a - ONES) & ~a & HIGHS & live) | ((b - ONES) & ~b & HIGHS & live)) return true;
-    }
-    return false;
-}
-
-// One candidate as hashcat's --stdout writes it: the raw bytes and a newline.  A candidate holding '\n' or '\r'
-// would not survive as one line of a wordlist (hashcat's own output splits it), so it alone is written as $HEX[..],
-// which every dictionary reader here decodes back to the same bytes.  p points into a 256-byte slot (n <= 256).
-static void stdout_plain(const uint8_t* p, size_t n, std::string& out) {
-    const bool hex = has_line_break(p, n);
-    if (!hex) {
-        out.append((const char*)p, n);
-    } else {
-        static const char* H = "0123456789abcdef";
-        out.append("$HEX[");
-        for (size_t i = 0; i < n; i++) {
-            out.push_back(H[p[i] >> 4]);
-            out.push_back(H[p[i] & 15]);
-        }
-        out.push_back(']');
-    }
-    out.push_back('\n');
-}
-
 // `hashcat --stdout -r rules_file sources... -o out_path` (help_crack.py:508 expandcracked, :575 prdict): the words
 // of the sources (plain or gzip, one per line, $HEX[] decoded, as hashcat reads wordlists) x every rule, expanded on
-// the GPU in sub-batches of ~1M candidates (256-byte slots, k_rules_expand), packed on the host in word-major order,
-// rejected candidates skipped, written as hashcat writes plains.  The device part of each sub-batch overlaps the
-// host's packing and writing of the previous one (two slot sets, two streams).
+// the GPU in sub-batches of ~1M candidates (k_rules_expand into 256-byte slots), and packed on the GPU too
+// (k_text_*: a scan of every candidate's text length, then each candidate copied to its offset): word-major order,
+// rejected candidates skipped, raw bytes and '\n' as hashcat's --stdout writes them, $HEX[..] for a candidate holding
+// '\n' or '\r'.  Only the packed text (~14 bytes per candidate) crosses PCIe -- round 4 copied the 256-byte slots
+// back (189 GB for 740M candidates) and packed them on one host thread.  Two sets on two streams: the GPU expands and
+// packs sub-batch i+1 while the host writes sub-batch i.
 static int rules_expand_file_impl(int device, const char* rules_file, const char* const* sources, size_t nsources,
                                   const char* out_path, int gzip_level, uint64_t* words_out, uint64_t* cands_out) {
     if (!rules_file || !out_path || (!sources && nsources)) return DWPA_E_ARG;
@@ -497,21 +465,31 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
     const size_t nr = rs.size();
     const size_t wpb = std::max<size_t>(1, (1u << 20) / nr);  // words per sub-batch: ~1M candidate slots
     const size_t ncap = wpb * nr;
+    const size_t nblk = text_pack_blocks((uint32_t)ncap);
     struct Set {
-        DevBuf off, bytes, out, len;
-        uint8_t* h_out = nullptr;
-        uint32_t* h_len = nullptr;
+        DevBuf off, bytes, out, len, tlen, bsum, bcnt, tot, text;
+        uint32_t* h_tot = nullptr;  // pinned: text bytes, kept candidates
+        uint8_t* h_text = nullptr;  // pinned, h_cap bytes (== text.n)
+        size_t h_cap = 0;
         hipStream_t s = nullptr;
-        hipEvent_t done = nullptr, up = nullptr;  // expansion copied back / inputs uploaded
+        hipEvent_t done = nullptr, up = nullptr;  // expansion + pack done and totals copied back / inputs uploaded
         std::vector<uint64_t> hoff;
-        size_t words = 0, base = 0;  // words of the sub-batch, first word's index in the chunk
+        size_t words = 0;  // words of the sub-batch
         bool busy = false;
+        int grow(size_t bytes) {  // device text buffer and its pinned host mirror, both `bytes`
+            if (h_text) (void)hipHostFree(h_text);
+            h_text = nullptr;
+            h_cap = 0;
+            if (text.ensure(bytes) || hipHostMalloc((void**)&h_text, bytes) != hipSuccess) return DWPA_E_NOMEM;
+            h_cap = bytes;
+            return 0;
+        }
     } set[2];
     for (Set& S : set) {
         if (rc < 0) break;
-        if (S.out.ensure(ncap * 256) || S.len.ensure(ncap * 4) || S.off.ensure((wpb + 1) * 8) ||
-            hipHostMalloc((void**)&S.h_out, ncap * 256) != hipSuccess ||
-            hipHostMalloc((void**)&S.h_len, ncap * 4) != hipSuccess)
+        if (S.out.ensure(ncap * 256) || S.len.ensure(ncap * 4) || S.tlen.ensure(ncap * 4) ||
+            S.off.ensure((wpb + 1) * 8) || S.bsum.ensure(nblk * 4) || S.bcnt.ensure(nblk * 4) || S.tot.ensure(8) ||
+            S.grow(ncap * 24) || hipHostMalloc((void**)&S.h_tot, 8) != hipSuccess)
             rc = DWPA_E_NOMEM;
         else if (hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking) != hipSuccess ||
                  hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess ||
@@ -519,21 +497,34 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
             rc = DWPA_E_HIP;
     }
     uint64_t words = 0, cands = 0;
-    std::string text;
-    auto drain = [&](Set& S) -> int {  // wait for S's expansion, pack and write it
+    auto pack = [&](Set& S) -> int {  // pack S's expansion into its text buffer, copy the totals back
+        const uint32_t n = (uint32_t)(S.words * nr);
+        if (launch_text_pack((const uint8_t*)S.out.p, (const uint32_t*)S.len.p, (const uint32_t*)S.tlen.p, n,
+                             (uint32_t*)S.bsum.p, (uint32_t*)S.bcnt.p, (uint32_t*)S.tot.p, (uint8_t*)S.text.p, S.h_cap,
+                             S.s) != hipSuccess ||
+            hipMemcpyAsync(S.h_tot, S.tot.p, 8, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+            hipEventRecord(S.done, S.s) != hipSuccess)
+            return DWPA_E_HIP;
+        return 0;
+    };
+    auto drain = [&](Set& S) -> int {  // wait for S's text, copy it back and write it
         if (!S.busy) return 0;
         S.busy = false;
         if (hipEventSynchronize(S.done) != hipSuccess) return DWPA_E_HIP;
-        text.clear();
-        for (size_t c = 0; c < S.words * nr; c++) {
-            const uint32_t n = S.h_len[c];
-            if (n == 0xFFFFFFFFu) continue;  // rejected (input word, or a reject / memory function)
-            stdout_plain(S.h_out + c * 256, n, text);
-            cands++;
+        size_t bytes = S.h_tot[0];
+        if (bytes > S.h_cap) {  // longer candidates than budgeted: a bigger buffer, and the same slots packed again
+            if (S.grow(bytes + bytes / 4) < 0) return DWPA_E_NOMEM;
+            int r = pack(S);
+            if (r < 0) return r;
+            if (hipEventSynchronize(S.done) != hipSuccess) return DWPA_E_HIP;
+            bytes = S.h_tot[0];
         }
-        const size_t put = gz ? (size_t)gzwrite(gz, text.data(), (unsigned)text.size())
-                              : fwrite(text.data(), 1, text.size(), fo);
-        return put == text.size() ? 0 : DWPA_E_IO;
+        if (bytes && (hipMemcpyAsync(S.h_text, S.text.p, bytes, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
+                      hipStreamSynchronize(S.s) != hipSuccess))
+            return DWPA_E_HIP;
+        cands += S.h_tot[1];
+        const size_t put = gz ? (size_t)gzwrite(gz, S.h_text, (unsigned)bytes) : fwrite(S.h_text, 1, bytes, fo);
+        return put == bytes ? 0 : DWPA_E_IO;
     };
     if (rc >= 0) {
         std::vector<std::string> paths(sources, sources + nsources);
@@ -562,13 +553,11 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
                     hipEventRecord(S.up, S.s) != hipSuccess ||
                     launch_rules_expand((const uint64_t*)S.off.p, (const uint8_t*)S.bytes.p, (uint32_t)S.words,
                                         (const uint32_t*)dr.offs, (const uint32_t*)dr.code, (uint32_t)nr,
-                                        (uint8_t*)S.out.p, (uint32_t*)S.len.p, S.s) != hipSuccess ||
-                    hipMemcpyAsync(S.h_len, S.len.p, S.words * nr * 4, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
-                    hipMemcpyAsync(S.h_out, S.out.p, S.words * nr * 256, hipMemcpyDeviceToHost, S.s) != hipSuccess ||
-                    hipEventRecord(S.done, S.s) != hipSuccess) {
+                                        (uint8_t*)S.out.p, (uint32_t*)S.len.p, S.s, (uint32_t*)S.tlen.p) != hipSuccess) {
                     rc = DWPA_E_HIP;
                     break;
                 }
+                if ((rc = pack(S)) < 0) break;
                 S.busy = true;  // S.hoff is rewritten only after drain(S); the chunk only after uploads_done()
                 words += S.words;
                 cur ^= 1;
@@ -581,12 +570,9 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
     }
     for (Set& S : set) {
         if (S.s) (void)hipStreamSynchronize(S.s);
-        S.off.release();
-        S.bytes.release();
-        S.out.release();
-        S.len.release();
-        if (S.h_out) (void)hipHostFree(S.h_out);
-        if (S.h_len) (void)hipHostFree(S.h_len);
+        for (DevBuf* b : {&S.off, &S.bytes, &S.out, &S.len, &S.tlen, &S.bsum, &S.bcnt, &S.tot, &S.text}) b->release();
+        if (S.h_text) (void)hipHostFree(S.h_text);
+        if (S.h_tot) (void)hipHostFree(S.h_tot);
         if (S.done) (void)hipEventDestroy(S.done);
         if (S.up) (void)hipEventDestroy(S.up);
         if (S.s) (void)hipStreamDestroy(S.s);

@@ -81,9 +81,19 @@ void rules_release(DevRules* r);
 int rules_load(dwpa_scan* scan, const DevRules* r, const uint64_t* off, const uint8_t* bytes, uint64_t first,
                uint32_t nwords, hipStream_t s, bool fill = false);
 
+// out: nwords x nrules 256-byte slots, out_len their lengths (0xFFFFFFFF = rejected); text_len (nullable): each
+// candidate's bytes in --stdout text (raw + '\n', or $HEX[..] + '\n' when it holds '\n' / '\r'; 0 = rejected).
 hipError_t launch_rules_expand(const uint64_t* off, const uint8_t* bytes, uint32_t nwords, const uint32_t* roffs,
                                const uint32_t* rcode, uint32_t nrules, uint8_t* out, uint32_t* out_len,
-                               hipStream_t s);
+                               hipStream_t s, uint32_t* text_len = nullptr);
+// The --stdout text of candidates [0, n) of a launch_rules_expand with text_len, packed on the GPU in candidate
+// order into text: bsum / bcnt scratch of text_pack_blocks(n) words each; tot[0] = text bytes, tot[1] = kept
+// candidates (both on the device).  Only candidates whose text ends within `cap` bytes are written: when tot[0] >
+// cap, grow text and pack again (the slots are unchanged).
+uint32_t text_pack_blocks(uint32_t n);
+hipError_t launch_text_pack(const uint8_t* out, const uint32_t* out_len, const uint32_t* text_len, uint32_t n,
+                            uint32_t* bsum, uint32_t* bcnt, uint32_t* tot, uint8_t* text, uint64_t cap,
+                            hipStream_t s);
 hipError_t launch_rules_prep(const uint64_t* off, const uint8_t* bytes, uint64_t first, uint32_t nwords,
                              const uint32_t* roffs, const uint32_t* rcode, uint32_t nrules, uint32_t minlen,
                              uint32_t maxlen, uint32_t* mid, uint64_t* ids, uint32_t* counter, uint32_t cap,

@@ -824,3 +824,25 @@ def test_first_key_exit_across_chunks(exit_on):
     assert res["got"] == res["exp"] == res["single"]
     assert res["key_index"] == res["first_copy"]
     assert res["key_index"][:4] == [20, 140, 5, 299] and res["got"][4] is False
+
+
+def test_expand_rules_file_long_candidates_grow_the_text_buffer(tmp_path):
+    """The wordlist text is packed on the GPU into a buffer budgeted at 24 bytes per candidate; candidates of 100-256
+    bytes overflow it, and the sub-batch is packed again into a bigger one.  Output = the rule oracle's expansion,
+    in order, with a '\\r' inside some candidates written as $HEX[]."""
+    from dwpa_amd.help_crack import expand_rules
+    rng = random.Random(33)
+    words = [S.random_psk(rng, 90, 120) for _ in range(40000)]
+    words[5] = b"x" * 50 + b"\r" + b"y" * 50
+    rules = [":", "d", "f", "p2", "$\r $!", "] ] ]"]
+    src = tmp_path / "source.txt"
+    src.write_bytes(b"\n".join(b"$HEX[" + w.hex().encode() + b"]" if b"\r" in w else w for w in words) + b"\n")
+    rf = tmp_path / "long.rule"
+    rf.write_bytes("\n".join(rules).encode() + b"\n")
+    out = tmp_path / "out.txt"
+    n = expand_rules(str(rf), str(src), str(out))
+    exp = [_stdout_plain(c) for row in R.expand(rules, words) for c in row if c is not None]
+    got = out.read_bytes().split(b"\n")[:-1]
+    assert n == len(exp) and got == exp
+    ncap = (1 << 20) // len(rules) * len(rules)  # the sub-batch's candidate slots (all words fit in one)
+    assert sum(len(e) + 1 for e in exp) > 24 * ncap  # the 24-bytes-per-slot budget was exceeded
