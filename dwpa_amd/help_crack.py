@@ -41,7 +41,11 @@ HASHCAT_NAMES = ("hashcat", "hashcat.bin", "hashcat.exe")  # the binaries check_
 
 
 def _parse_options(rules: str, coptions: str):
-    rules_file, devices = None, 0
+    """The parts of help_crack's hashcat command line (:773) that change the work: ``conf["rules"]`` ("-S -r <file>")
+    and the user's ``-co`` options -- the rules file, hashcat's ``-d`` device list (numbered from 1) and a
+    ``--nonce-error-corrections`` that overrides the command line's 8 (hashcat takes the last one given).  Returns
+    (rules file or None, device mask, nonce-error-corrections or None)."""
+    rules_file, devices, nec = None, 0, None
     toks = shlex.split(rules or "") + shlex.split(coptions or "")
     i = 0
     while i < len(toks):
@@ -58,8 +62,14 @@ def _parse_options(rules: str, coptions: str):
                     devices |= 1 << (int(d) - 1)  # hashcat numbers devices from 1
             i += 2
             continue
+        elif t == "--nonce-error-corrections" and i + 1 < len(toks) and toks[i + 1].isdigit():
+            nec = int(toks[i + 1])
+            i += 2
+            continue
+        elif t.startswith("--nonce-error-corrections=") and t.split("=", 1)[1].isdigit():
+            nec = int(t.split("=", 1)[1])
         i += 1
-    return rules_file, devices
+    return rules_file, devices, nec
 
 
 def _sleepy(sec: int = 123) -> None:
@@ -95,7 +105,9 @@ def _summary(rc: int) -> str:
         f"Time.............: {st['seconds']:.2f} s",
     ]
     if st.get("rules") or st.get("rules_skipped"):
-        lines.insert(4, f"Rules............: {st['rules']} loaded, {st['rules_skipped']} skipped (invalid or unsupported)")
+        rejmem = f", {st['rules_rejmem']} of them for reject / memory functions" if st.get("rules_rejmem") else ""
+        lines.insert(4, f"Rules............: {st['rules']} loaded, {st['rules_skipped']} skipped (invalid or "
+                        f"unsupported{rejmem})")
     return "\n".join(lines)
 
 
@@ -125,7 +137,9 @@ def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR
         raise FileNotFoundError(conf["hash_file"])
     sleepy = sleepy or _sleepy
     pprint = pprint or (lambda mess, code="HEADER": print(mess, file=sys.stderr))
-    rules_file, mask = _parse_options(conf.get("rules", ""), conf.get("coptions", ""))
+    rules_file, mask, nec = _parse_options(conf.get("rules", ""), conf.get("coptions", ""))
+    if nec is not None:
+        nonce_error_corrections = nec
     key_file = conf["key_file"]
     dictlist = list(dictlist)
     tries = 0

@@ -160,3 +160,21 @@ def test_hashcat_stdout_without_outfile_writes_stdout(monkeypatch, capfdbinary, 
     assert capfdbinary.readouterr().out == b"cand1\ncand2\n"
     assert seen == [b":\n"]
     assert not list(tmp_path.iterdir())  # no temporary file left behind
+
+
+@pytest.mark.parametrize("co,exp", [("", 8), ("--nonce-error-corrections=16", 16), ("--nonce-error-corrections 0", 0),
+                                    ("-d 1 --nonce-error-corrections=4 -w 3", 4)])
+def test_coptions_nonce_error_corrections(standin, monkeypatch, co, exp):
+    """A user's -co option (help_crack.py:977,987) comes after --nonce-error-corrections=8 on hashcat's command line
+    (:773), so it wins; the drop-in passes it on likewise."""
+    seen = []
+    monkeypatch.setattr(H.M, "crack_files_ex",
+                        lambda hf, d, r, nec, kf, device_mask=0: seen.append(nec) or (1, [L.DWPA_DICT_OK] * len(d)))
+    monkeypatch.setattr(H.M, "crack_stats", lambda: {"words": 0, "candidates": 0, "hashes": 1, "cracked": 0,
+                                                     "seconds": 0.0, "rules": 5, "rules_skipped": 2,
+                                                     "rules_rejmem": 1})
+    H.install(standin.HelpCrack)
+    hc = standin.HelpCrack()
+    open("help_crack.hash", "w").write("x\n")
+    hc.conf["coptions"] = co
+    assert hc.run_cracker(["a.gz"]) == 1 and seen == [exp]
