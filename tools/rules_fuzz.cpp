@@ -25,7 +25,7 @@ hipError_t launch_rules_prep(const uint64_t*, const uint8_t*, uint64_t, uint32_t
     not_here();
 }
 hipError_t launch_rules_expand(const uint64_t*, const uint8_t*, uint32_t, const uint32_t*, const uint32_t*, uint32_t,
-                               uint8_t*, uint32_t*, hipStream_t) {
+                               uint8_t*, uint32_t*, hipStream_t, uint32_t*) {
     not_here();
 }
 }  // namespace dwpa
