@@ -83,10 +83,11 @@ def test_rule_parser_matches_oracle_count():
 
 
 @pytest.mark.parametrize("rules,coptions,expect", [
-    ("", "", (None, 0)),
-    ("-S -r help_crack.rules", "", ("help_crack.rules", 0)),          # help_crack.py:445-447
-    ("", "-d 1,3 --force", (None, 0b101)),                             # hashcat numbers devices from 1
-    ("--rules-file=x.rule", "--backend-devices 2", ("x.rule", 0b10)),
+    ("", "", (None, 0, None)),
+    ("-S -r help_crack.rules", "", ("help_crack.rules", 0, None)),          # help_crack.py:445-447
+    ("", "-d 1,3 --force", (None, 0b101, None)),                             # hashcat numbers devices from 1
+    ("--rules-file=x.rule", "--backend-devices 2", ("x.rule", 0b10, None)),
+    ("", "--nonce-error-corrections=16", (None, 0, 16)),                     # a -co NC value overrides the 8
 ])
 def test_help_crack_option_parsing(rules, coptions, expect):
     from dwpa_amd.help_crack import _parse_options
