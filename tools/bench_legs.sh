@@ -1,7 +1,7 @@
 #!/bin/bash
 # Every BASELINE.json config as a bench.py leg, one JSON line each, plus the VALU issue-cost re-measurement the
 # roofline is priced on.  Run on the GPU box from the repo root; results land in gpurun_out/legs/.
-# LEGS="c2 c4" restricts the set.  Each step has its own time limit and the chain stops at the first failure.
+# LEGS="c2 c4" restricts the set (c1cold, the PHP-FPM worker-process leg, runs only when named).  Each step has its own time limit and the chain stops at the first failure.
 set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/legs}
@@ -30,6 +30,7 @@ for leg in $LEGS; do
                --warmup 0 > $OUT/c3files_server.json 2> $OUT/c3files_server.err ;;
     c3files_server_full) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --rules-set server \
                --rule-mode full --steps 2 --warmup 0 > $OUT/c3files_server_full.json 2> $OUT/c3files_server_full.err ;;
+    c1cold)  timeout -k 10 900 python3 bench.py --workload c1cold --steps 20 > $OUT/c1cold.json 2> $OUT/c1cold.err ;;
     expand)  timeout -k 10 300 python3 bench.py --workload expand --rule-words 5000000 --steps 2 --warmup 1 \
                > $OUT/expand.json 2> $OUT/expand.err ;;
     *) echo "unknown leg $leg" >&2; exit 2 ;;
