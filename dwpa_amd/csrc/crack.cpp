@@ -476,12 +476,12 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
         std::vector<uint64_t> hoff;
         size_t words = 0;  // words of the sub-batch
         bool busy = false;
-        int grow(size_t bytes) {  // device text buffer and its pinned host mirror, both `bytes`
+        int grow(size_t want) {  // device text buffer and its pinned host mirror, both `want` bytes
             if (h_text) (void)hipHostFree(h_text);
             h_text = nullptr;
             h_cap = 0;
-            if (text.ensure(bytes) || hipHostMalloc((void**)&h_text, bytes) != hipSuccess) return DWPA_E_NOMEM;
-            h_cap = bytes;
+            if (text.ensure(want) || hipHostMalloc((void**)&h_text, want) != hipSuccess) return DWPA_E_NOMEM;
+            h_cap = want;
             return 0;
         }
     } set[2];

@@ -1415,11 +1415,11 @@ static int scan_mg_rebuild(dwpa_scan* sc, hipStream_t s) {
             sc->mg_gsalt_h.push_back(grp[k]->salt_off);
             sc->mg_gsalt_h.push_back(grp[k]->nsalt);
         }
-        for (uint32_t c = 0; c < 4; c++) {
-            ch.cls[c] = (uint32_t)sc->mg_list_h.size() - ch.list0;
+        for (uint32_t vc = 0; vc < 4; vc++) {
+            ch.cls[vc] = (uint32_t)sc->mg_list_h.size() - ch.list0;
             for (uint32_t k = 0; k < size; k++)
                 for (uint32_t l = grp[k]->line_begin; l < grp[k]->line_end; l++) {
-                    if (sc->cracked[l] || verify_class(sc->tb.lines[l]) != (1u << c)) continue;
+                    if (sc->cracked[l] || verify_class(sc->tb.lines[l]) != (1u << vc)) continue;
                     sc->mg_list_h.push_back(l);
                     sc->mg_poff_h[l] = k * cap;
                 }

@@ -119,7 +119,7 @@ __device__ __forceinline__ void pbkdf2_lane_tail(const uint32_t hi[5], const uin
         }
         // outside the loop: a lane-0-only atomic inside a loop can make the compiler split the loop by lanes
         const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        if (up && lane == __builtin_amdgcn_readfirstlane(lane))
+        if (up && lane == (uint32_t)__builtin_amdgcn_readfirstlane(lane))
             __hip_atomic_fetch_add(raised, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll 1
