@@ -182,7 +182,8 @@ def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR
 def expand_rules(rules_file: str, source: str, out_path: str, gzip_level: int = 0, device: int = 0) -> int:
     """`hashcat --stdout -r rules_file source -o out_path` (help_crack.py:508 expandcracked, :575 prdict) with the
     rules applied on the GPU and the candidates packed and written by the library (dwpa_rules_expand_file): one per
-    line, word-major, rejected candidates skipped, $HEX[] for non-printable ones.  Like hashcat, the output is plain
+    line, word-major, rejected candidates skipped, raw bytes as hashcat writes them ($HEX[] only for a candidate
+    holding '\\n' or '\\r', which would not stay one line).  Like hashcat, the output is plain
     text whatever its name (help_crack names it cracked.txt.gz; the dictionary readers take plain and gzip alike);
     gzip_level 1..9 compresses it.  Rule lines that do not parse are reported by the library on stderr ("skipping
     invalid or unsupported rule in <file> on line <n>"), and a file without a valid rule raises, as hashcat refuses
