@@ -251,6 +251,13 @@ static void put_u32(uint8_t *d, uint32_t v, int big) {
     else { d[0] = v; d[1] = v >> 8; d[2] = v >> 16; d[3] = v >> 24; }
 }
 
+/* The returned key (after hc_unhex): key_len is its full length, the buffer holds at most sizeof(out->key) bytes of
+ * it (hash_pbkdf2 takes keys of any length; a caller reads a longer one from keys[key_index]). */
+static void result_key(oracle_result *out, const buf_t *key) {
+    memcpy(out->key, key->p, key->n < sizeof out->key ? key->n : sizeof out->key);
+    out->key_len = key->n;
+}
+
 int oracle_check_m22000(const char *line, size_t len, const oracle_key *keys, size_t nkeys,
                         const uint8_t *pmk_in, int nc, oracle_result *out) {
     const uint8_t *s = (const uint8_t *)line;
@@ -288,8 +295,7 @@ int oracle_check_m22000(const char *line, size_t len, const oracle_key *keys, si
                 out->nc_is_null = 1;
                 out->endian = 0;
                 memcpy(out->pmk, pmk, 32);
-                memcpy(out->key, key.p, key.n);
-                out->key_len = key.n;
+                result_key(out, &key);
                 rc = 1;
                 goto done;
             }
@@ -368,8 +374,7 @@ int oracle_check_m22000(const char *line, size_t len, const oracle_key *keys, si
                     if (php_strncmp(test, keyver == 2 ? 20 : 16, keymic.p, keymic.n, 16) == 0) {
                         out->key_index = (int32_t)i;
                         memcpy(out->pmk, pmk, 32);
-                        memcpy(out->key, key.p, key.n);
-                        out->key_len = key.n;
+                        result_key(out, &key);
                         out->nc_is_null = 0;
                         if (joff[0] == 0) { out->nc = 0; out->endian = 0; }
                         else { out->nc = (int32_t)joff[jj]; out->endian = jbig[jj] ? 1 : 2; }

@@ -15,8 +15,8 @@ typedef struct {
     int32_t nc_is_null;  /* 1: PHP Null (PMKID lines) */
     int32_t endian;      /* 0: Null, 1: 'BE', 2: 'LE' */
     uint8_t pmk[32];
-    uint8_t key[4096];   /* the key as returned by PHP (after hc_unhex) */
-    size_t key_len;
+    uint8_t key[4096];   /* the key as returned by PHP (after hc_unhex), its first 4096 bytes */
+    size_t key_len;      /* its full length */
 } oracle_result;
 
 int oracle_valid_hex(const uint8_t *s, size_t n);

@@ -323,8 +323,9 @@ def _keys_array(keys):
     return arr, keep
 
 
-def _result_to_php(r: OResult):
-    key = bytes(r.key[:r.key_len])
+def _result_to_php(r: OResult, src: bytes):
+    # the C result holds the first len(r.key) bytes of the key; a longer one is the input key, decoded the same way
+    key = bytes(r.key[:r.key_len]) if r.key_len <= len(r.key) else hc_unhex(bytes(src))
     pmk = bytes(r.pmk)
     if r.nc_is_null:
         return [key, None, None, pmk]
@@ -340,7 +341,7 @@ def c_check_key_m22000(hashline, keys, pmk=False, nc: int = 128):
                                    ctypes.byref(res))
     if rc != 1:
         return False
-    return _result_to_php(res)
+    return _result_to_php(res, keys[res.key_index])
 
 
 def c_check_many(hashline: bytes, keys, nc: int = 128, threads: int = 1):
@@ -348,7 +349,7 @@ def c_check_many(hashline: bytes, keys, nc: int = 128, threads: int = 1):
     arr, keep = _keys_array(keys)
     res = OResult()
     idx = lib().oracle_check_many(hashline, len(hashline), arr, len(keys), nc, threads, ctypes.byref(res))
-    return idx, (_result_to_php(res) if idx >= 0 else False)
+    return idx, (_result_to_php(res, keys[idx]) if idx >= 0 else False)
 
 
 def c_pbkdf2_many(keys, essid: bytes, threads: int = 1) -> bytes:

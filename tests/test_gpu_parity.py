@@ -43,6 +43,27 @@ def test_pbkdf2_random_lengths():
         assert b"".join(got) == exp, essid_len
 
 
+def test_pbkdf2_long_keys():
+    """hash_pbkdf2 takes a key of any length (common.php:178,246): keys longer than the 64-byte HMAC block are
+    hashed first, on the GPU in k_prep_keys (sha1_long_key), up to tens of KB per lane."""
+    rng = random.Random(8)
+    keys = [bytes(rng.randrange(256) for _ in range(n)) for n in (1000, 4095, 4096, 4097, 65537)]
+    keys += [b"A" * 64 * 1024]
+    got = dwpa_amd.pbkdf2_pmk(keys, b"ThisIsASSID")
+    assert b"".join(got) == O.c_pbkdf2_many(keys, b"ThisIsASSID", threads=8)
+    # and through the check path, plain and as $HEX[], PMKID and EAPOL: the first long key that verifies
+    ap, sta = bytes.fromhex("020000000001"), bytes.fromhex("020000000002")
+    lines = [S.pmkid_line(keys[4], b"ThisIsASSID", ap, sta, got[4]),
+             S.eapol_line(keys[4], b"ThisIsASSID", ap, sta, bytes(range(32)), bytes(range(32, 64)), 2, nc=2,
+                          mp=0x80, the_pmk=got[4])]
+    jobs = [(line, cand, False, 8) for line in lines
+            for cand in ([b"x" * 9, keys[3], keys[4]], [keys[0], b"$HEX[" + keys[4].hex().encode() + b"]"])]
+    exp = [O.c_check_key_m22000(*j) for j in jobs]
+    assert all(e and e[0] == keys[4] for e in exp)
+    assert [dwpa_amd.check_key_m22000(*j) for j in jobs] == exp
+    assert dwpa_amd.check_batch(jobs) == exp
+
+
 def test_challenge_kat(kat):
     for c in kat["challenge"]:
         assert dwpa_amd.check_key_m22000(c["line"], [b"aaaa1234"]) == dec(c["expect"])

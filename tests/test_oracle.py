@@ -89,3 +89,18 @@ def test_hc_unhex_cases():
     assert O.hc_unhex(b"$HEX[41zz]") == b"$HEX[41zz]"
     assert O.hc_unhex(b"$HEX[4142]x") == b"$HEX[4142]x"
     assert O.hc_unhex(b"plain") == b"plain"
+
+
+def test_long_keys_both_oracles():
+    """Keys longer than the C oracle's 4096-byte result buffer (hash_pbkdf2 takes any length): the C and Python
+    restatements agree, and the key comes back whole, plain or from its $HEX[] form."""
+    ap, sta = bytes.fromhex("020000000001"), bytes.fromhex("020000000002")
+    for n in (4096, 4097, 20000):
+        k = bytes(random.Random(n).randrange(256) for _ in range(n))
+        pmk = O.c_pbkdf2(k, b"ESSID")
+        assert pmk == O.pbkdf2_pmk(k, b"ESSID")
+        line = S.pmkid_line(k, b"ESSID", ap, sta, pmk)
+        for cand in ([b"x" * 9, k], [b"$HEX[" + k.hex().encode() + b"]"]):
+            r = O.c_check_key_m22000(line, cand)
+            assert r == O.py_check_key_m22000(line, cand) and r[0] == k and r[3] == pmk
+        assert O.c_check_many(line, [b"y" * 8, k])[0] == 1
