@@ -64,6 +64,25 @@ def test_pbkdf2_long_keys():
     assert dwpa_amd.check_batch(jobs) == exp
 
 
+def test_essid_lengths_check_path():
+    """ESSIDs of 0..1000 bytes through the check path (hex2bin takes any even-length field, common.php:165,233; an
+    empty field fails valid_hex): the salt of 1, 2 and 16+ SHA-1 blocks (salt + INT(i) + padding crosses a block at 52
+    and 116 bytes), PMKID and EAPOL, one call per job and one batch."""
+    rng = random.Random(9)
+    ap, sta = bytes.fromhex("020000000001"), bytes.fromhex("020000000002")
+    jobs = []
+    for n in (0, 1, 32, 33, 51, 52, 55, 56, 64, 115, 116, 255, 1000):
+        essid = bytes(rng.randrange(256) for _ in range(n))
+        psk = S.random_psk(rng)
+        jobs.append((S.pmkid_line(psk, essid, ap, sta), [b"wrongpsk1", psk], False, 8))
+        jobs.append((S.eapol_line(psk, essid, ap, sta, rng.randbytes(32), rng.randbytes(32), 1 + n % 3, -1, "BE",
+                                  rng=rng), [psk], False, 8))
+    exp = [O.c_check_key_m22000(*j) for j in jobs]
+    assert exp[0] is False and exp[1] is False and all(exp[2:])
+    assert [dwpa_amd.check_key_m22000(*j) for j in jobs] == exp
+    assert dwpa_amd.check_batch(jobs) == exp
+
+
 def test_challenge_kat(kat):
     for c in kat["challenge"]:
         assert dwpa_amd.check_key_m22000(c["line"], [b"aaaa1234"]) == dec(c["expect"])
