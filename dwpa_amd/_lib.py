@@ -17,6 +17,7 @@ DWPA_E_FORMAT, DWPA_E_HEX, DWPA_E_TYPE, DWPA_E_KEYVER = -1, -2, -3, -4
 DWPA_E_NODEV, DWPA_E_HIP, DWPA_E_ARG, DWPA_E_NOMEM, DWPA_E_IO, DWPA_E_OVERFLOW, DWPA_E_RULE = -10, -11, -12, -13, -14, -15, -16
 DWPA_RC_CRACKED, DWPA_RC_EXHAUSTED, DWPA_RC_ERROR = 0, 1, -1
 DWPA_NC_PHP, DWPA_NC_HASHCAT = 0, 1
+DWPA_NC_MAX = 65536  # the largest nc / nonce_error_corrections taken (include/dwpa22000.h)
 DWPA_DICT_OK, DWPA_DICT_DAMAGED = 0, 1  # dwpa_crack_files_ex per-dictionary status (or DWPA_E_IO)
 DWPA_RULES_DEFAULT, DWPA_RULES_HASHCAT, DWPA_RULES_FULL = 0, 1, 2  # dwpa_config.rule_mode
 

@@ -197,6 +197,10 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
         for (size_t i = 0; i < ndicts; i++) dict_status[i] = DWPA_DICT_OK;
     if (!hash_file || !out_file || (!dicts && ndicts)) return DWPA_RC_ERROR;
     if (cfg && cfg->struct_size && cfg->struct_size < offsetof(dwpa_config, batch)) return DWPA_RC_ERROR;
+    if (nec > DWPA_NC_MAX) {
+        fprintf(stderr, "[dwpa] --nonce-error-corrections=%d is above the supported %d\n", nec, DWPA_NC_MAX);
+        return DWPA_RC_ERROR;
+    }
     // hashcat refuses to start when a wordlist cannot be opened; so does this call, before touching a device, and it
     // names the file (DWPA_E_IO in dict_status): a deterministic input error, which help_crack's drop-in does not retry
     bool unreadable = false;
@@ -331,7 +335,7 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
                     }
                     WorkItem it;
                     if (sh.stop || !items.next(it)) break;
-                    const int r = stage_shard(w, *it.chunk, it.b, it.e, slot);
+                    const int r = guarded([&] { return stage_shard(w, *it.chunk, it.b, it.e, slot); });
                     if (r < 0) {
                         fail(r);
                         break;
@@ -361,7 +365,7 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
                         w.ready.pop_front();
                         it = w.slot_item[slot];
                     }
-                    const int r = scan_shard(w, sh, *it.chunk, it.b, it.e, rp, slot);
+                    const int r = guarded([&] { return scan_shard(w, sh, *it.chunk, it.b, it.e, rp, slot); });
                     w.items++;
                     w.words += it.e - it.b;
                     {
@@ -591,13 +595,17 @@ extern "C" {
 
 int dwpa_rules_expand_file(int device, const char* rules_file, const char* const* sources, size_t nsources,
                            const char* out_path, int gzip_level, uint64_t* words_out, uint64_t* cands_out) {
-    return dwpa::rules_expand_file_impl(device, rules_file, sources, nsources, out_path, gzip_level, words_out,
-                                        cands_out);
+    return dwpa::guarded([&]() -> int {
+        return dwpa::rules_expand_file_impl(device, rules_file, sources, nsources, out_path, gzip_level, words_out,
+                                            cands_out);
+    });
 }
 
 int dwpa_crack_files(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,
                      int nonce_error_corrections, const char* out_file, const dwpa_config* cfg) {
-    return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg, nullptr);
+    return dwpa::guarded([&]() -> int {
+        return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg, nullptr);
+    }, DWPA_RC_ERROR, DWPA_RC_ERROR);
 }
 
 int dwpa_crack_last_stats(dwpa_crack_stats* out) {
@@ -609,7 +617,9 @@ int dwpa_crack_last_stats(dwpa_crack_stats* out) {
 int dwpa_crack_files_ex(const char* hash_file, const char* const* dicts, size_t ndicts, const char* rules_file,
                         int nonce_error_corrections, const char* out_file, const dwpa_config* cfg,
                         int32_t* dict_status) {
-    return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg, dict_status);
+    return dwpa::guarded([&]() -> int {
+        return dwpa::crack_impl(hash_file, dicts, ndicts, rules_file, nonce_error_corrections, out_file, cfg, dict_status);
+    }, DWPA_RC_ERROR, DWPA_RC_ERROR);
 }
 
 // md5 over fields 1..7 of the hashline (web/common.php:310-315); a tiny host MD5 keeps this dependency-free.
@@ -658,17 +668,19 @@ static void md5_host(const uint8_t* msg, size_t len, uint8_t out[16]) {
 }
 
 int dwpa_hash_m22000(const char* line, size_t line_len, uint8_t out[16]) {
-    if (!line || !out) return DWPA_E_ARG;
-    const char* f[9];
-    size_t fl[9], cnt = 0, st = 0;
-    for (size_t i = 0; i < line_len && cnt < 8; i++)
-        if (line[i] == '*') { f[cnt] = line + st; fl[cnt] = i - st; cnt++; st = i + 1; }
-    f[cnt] = line + st; fl[cnt] = line_len - st; cnt++;
-    if (cnt != 9) return DWPA_E_FORMAT;
-    std::string cat;
-    for (int i = 1; i <= 7; i++) cat.append(f[i], fl[i]);
-    md5_host((const uint8_t*)cat.data(), cat.size(), out);
-    return 0;
+    return dwpa::guarded([&]() -> int {
+        if (!line || !out) return DWPA_E_ARG;
+        const char* f[9];
+        size_t fl[9], cnt = 0, st = 0;
+        for (size_t i = 0; i < line_len && cnt < 8; i++)
+            if (line[i] == '*') { f[cnt] = line + st; fl[cnt] = i - st; cnt++; st = i + 1; }
+        f[cnt] = line + st; fl[cnt] = line_len - st; cnt++;
+        if (cnt != 9) return DWPA_E_FORMAT;
+        std::string cat;
+        for (int i = 1; i <= 7; i++) cat.append(f[i], fl[i]);
+        md5_host((const uint8_t*)cat.data(), cat.size(), out);
+        return 0;
+    });
 }
 
 }  // extern "C"

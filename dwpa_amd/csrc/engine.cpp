@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <deque>
+#include <exception>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -424,20 +425,44 @@ class HostPool {
         static HostPool* pool = new HostPool();  // never destroyed: workers may outlive static destructors
         return *pool;
     }
+    // fn(0..T-1), part 0 on the calling thread.  An exception of any part (std::bad_alloc on a huge input) is
+    // rethrown here once every part has ended -- the queued parts reference this frame -- so that it reaches the
+    // entry point's guarded() instead of terminating a worker thread.
     template <typename F>
     void run(size_t T, const F& fn) {
         std::atomic<size_t> left{T - 1};
+        std::exception_ptr err;
+        std::mutex err_mu;
+        auto part = [&](size_t t) {
+            try {
+                fn(t);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(err_mu);
+                if (!err) err = std::current_exception();
+            }
+        };
+        size_t queued = 0;
         {
             std::lock_guard<std::mutex> lk(mu_);
-            grow_locked(T - 1);
-            for (size_t t = 1; t < T; t++)
-                q_.push_back([&fn, &left, t] {
-                    fn(t);
-                    left.fetch_sub(1, std::memory_order_acq_rel);
-                });
+            try {
+                grow_locked(T - 1);
+            } catch (...) {  // fewer workers: the caller runs what they do not take
+            }
+            try {
+                for (; queued + 1 < T; queued++)
+                    q_.push_back([&part, &left, t = queued + 1] {
+                        part(t);
+                        left.fetch_sub(1, std::memory_order_acq_rel);
+                    });
+            } catch (...) {  // the parts that could not be queued run below
+            }
         }
         cv_.notify_all();
-        fn(0);
+        part(0);
+        for (size_t t = queued + 1; t < T; t++) {
+            part(t);
+            left.fetch_sub(1, std::memory_order_acq_rel);
+        }
         while (left.load(std::memory_order_acquire)) {
             std::function<void()> task;
             {
@@ -450,6 +475,7 @@ class HostPool {
             if (task) task();
             else std::this_thread::yield();
         }
+        if (err) std::rethrow_exception(err);
     }
 
     size_t workers() {
@@ -985,6 +1011,10 @@ static int check_batch_body(Device& d, const dwpa_job* jobs, size_t njobs, dwpa_
             rcs[j] = DWPA_MISS;
             cs.job_pmk[j] = jobs[j].pmk;
             if (!line_can_match(pl)) continue;  // PMKID/MIC shorter than 16 bytes never verifies
+            if (pl.kind == LINE_EAPOL && jobs[j].nc > DWPA_NC_MAX) {  // attempt tables beyond the documented bound
+                rcs[j] = DWPA_E_ARG;
+                continue;
+            }
             if (jobs[j].nkeys > UINT32_MAX) {      // key indices are 32-bit (SlotTable::kidx)
                 rcs[j] = DWPA_E_ARG;
                 continue;
@@ -1255,7 +1285,7 @@ static hipStream_t as_stream(void* s) { return (hipStream_t)s; }
 int scan_create(int device, const char* const* lines, const size_t* lens, size_t nlines, int nc, int nc_mode,
                 uint32_t batch, dwpa_scan** out) {
     RCHK(ensure_init());
-    if (device < 0 || device >= g_ndev || !out || batch == 0) return DWPA_E_ARG;
+    if (device < 0 || device >= g_ndev || !out || batch == 0 || nc > DWPA_NC_MAX) return DWPA_E_ARG;
     HIPCHK(hipSetDevice(device));
     auto sc = std::make_unique<dwpa_scan>();
     sc->device = device;
@@ -1532,16 +1562,20 @@ extern "C" {
 int dwpa_abi_version(void) { return DWPA_ABI_VERSION; }
 
 int dwpa_init(const dwpa_config* cfg) {
-    if (cfg && cfg->struct_size && cfg->struct_size < sizeof(uint32_t) * 3) return DWPA_E_ARG;
-    if (DWPA_CFG_HAS(cfg, rule_mode) && (cfg->rule_mode < DWPA_RULES_DEFAULT || cfg->rule_mode > DWPA_RULES_FULL))
-        return DWPA_E_ARG;
-    std::lock_guard<std::mutex> lk(g_mu);
-    return init_locked(cfg);
+    return guarded([&]() -> int {
+        if (cfg && cfg->struct_size && cfg->struct_size < sizeof(uint32_t) * 3) return DWPA_E_ARG;
+        if (DWPA_CFG_HAS(cfg, rule_mode) && (cfg->rule_mode < DWPA_RULES_DEFAULT || cfg->rule_mode > DWPA_RULES_FULL))
+            return DWPA_E_ARG;
+        std::lock_guard<std::mutex> lk(g_mu);
+        return init_locked(cfg);
+    });
 }
 
 int dwpa_device_count(void) {
-    int r = ensure_init();
-    return r < 0 ? r : g_ndev;
+    return guarded([&]() -> int {
+        int r = ensure_init();
+        return r < 0 ? r : g_ndev;
+    });
 }
 
 const char* dwpa_strerror(int code) {
@@ -1601,31 +1635,37 @@ void dwpa_shutdown(void) {
 
 int dwpa_check_m22000(const char* line, size_t line_len, const dwpa_bytes* keys, size_t nkeys, const uint8_t* pmk,
                       int nc, dwpa_result* out) {
-    if (!line || (!keys && nkeys) || !out) return DWPA_E_ARG;
-    dwpa_job j{line, line_len, keys, nkeys, pmk, nc};
-    int rc = 0;
-    int r = check_batch_impl(&j, 1, out, &rc);
-    return r < 0 ? r : rc;
+    return guarded([&]() -> int {
+        if (!line || (!keys && nkeys) || !out) return DWPA_E_ARG;
+        dwpa_job j{line, line_len, keys, nkeys, pmk, nc};
+        int rc = 0;
+        int r = check_batch_impl(&j, 1, out, &rc);
+        return r < 0 ? r : rc;
+    });
 }
 
 int dwpa_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs) {
-    if ((!jobs || !out || !rcs) && njobs) return DWPA_E_ARG;
-    if (njobs == 0) return 0;
-    return check_batch_impl(jobs, njobs, out, rcs);
+    return guarded([&]() -> int {
+        if ((!jobs || !out || !rcs) && njobs) return DWPA_E_ARG;
+        if (njobs == 0) return 0;
+        return check_batch_impl(jobs, njobs, out, rcs);
+    });
 }
 
 int dwpa_resource_stats(dwpa_resources* out) {
-    if (!out) return DWPA_E_ARG;
-    memset(out, 0, sizeof(*out));
-    out->device_bytes = g_dev_bytes.load();
-    out->pinned_host_bytes = g_pinned_bytes.load();
-    out->host_pool_threads = (uint32_t)HostPool::get().workers();
-    std::lock_guard<std::mutex> lk(g_mu);
-    out->devices = (uint32_t)g_ndev;
-    for (auto& d : g_dev)
-        if (d->used.load(std::memory_order_acquire)) out->call_contexts_used++;
-    out->call_contexts = (uint32_t)g_dev.size();
-    return 0;
+    return guarded([&]() -> int {
+        if (!out) return DWPA_E_ARG;
+        memset(out, 0, sizeof(*out));
+        out->device_bytes = g_dev_bytes.load();
+        out->pinned_host_bytes = g_pinned_bytes.load();
+        out->host_pool_threads = (uint32_t)HostPool::get().workers();
+        std::lock_guard<std::mutex> lk(g_mu);
+        out->devices = (uint32_t)g_ndev;
+        for (auto& d : g_dev)
+            if (d->used.load(std::memory_order_acquire)) out->call_contexts_used++;
+        out->call_contexts = (uint32_t)g_dev.size();
+        return 0;
+    });
 }
 
 int dwpa_check_last_stats(dwpa_check_stats* out) {
@@ -1635,47 +1675,56 @@ int dwpa_check_last_stats(dwpa_check_stats* out) {
 }
 
 int dwpa_pbkdf2_pmk(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* pmks_out) {
-    if ((!keys && nkeys) || (!essid && essid_len) || (!pmks_out && nkeys)) return DWPA_E_ARG;
-    if (nkeys == 0) return 0;
-    return pbkdf2_impl(keys, nkeys, essid, essid_len, pmks_out);
+    return guarded([&]() -> int {
+        if ((!keys && nkeys) || (!essid && essid_len) || (!pmks_out && nkeys)) return DWPA_E_ARG;
+        if (nkeys == 0) return 0;
+        return pbkdf2_impl(keys, nkeys, essid, essid_len, pmks_out);
+    });
 }
 
 int dwpa_parse_m22000(const char* line, size_t line_len, int nc, int nc_mode, dwpa_line_info* out) {
-    if (!line || !out) return DWPA_E_ARG;
-    memset(out, 0, sizeof(*out));
-    ParsedLine p = parse_m22000(line, line_len);
-    if (p.status) return p.status;
-    TableBuilder tb;
-    const uint32_t li = tb.add_line(p, nc, nc_mode, nc);
-    const LineDev& L = tb.lines[li];
-    out->type = p.kind;
-    out->keyver = p.keyver;
-    out->essid_len = (uint32_t)p.essid.size();
-    out->mac_ap_len = (uint32_t)p.mac_ap.size();
-    out->mac_sta_len = (uint32_t)p.mac_sta.size();
-    out->target_len = (uint32_t)(p.kind == LINE_PMKID ? p.pmkid.size() : p.keymic.size());
-    out->attempts = p.kind == LINE_PMKID ? 1 : L.natt;
-    out->lists = p.kind == LINE_PMKID ? 1 : L.nlists;
-    out->never_matches = tb.never[li];
-    memcpy(out->essid, p.essid.data(), std::min<size_t>(32, p.essid.size()));
-    memcpy(out->mac_ap, p.mac_ap.data(), std::min<size_t>(16, p.mac_ap.size()));
-    memcpy(out->mac_sta, p.mac_sta.data(), std::min<size_t>(16, p.mac_sta.size()));
-    dwpa_hash_m22000(line, line_len, out->hash_m22000);
-    return 0;
+    return guarded([&]() -> int {
+        if (!line || !out) return DWPA_E_ARG;
+        memset(out, 0, sizeof(*out));
+        ParsedLine p = parse_m22000(line, line_len);
+        if (p.status) return p.status;
+        if (p.kind == LINE_EAPOL && nc > DWPA_NC_MAX) return DWPA_E_ARG;
+        TableBuilder tb;
+        const uint32_t li = tb.add_line(p, nc, nc_mode, nc);
+        const LineDev& L = tb.lines[li];
+        out->type = p.kind;
+        out->keyver = p.keyver;
+        out->essid_len = (uint32_t)p.essid.size();
+        out->mac_ap_len = (uint32_t)p.mac_ap.size();
+        out->mac_sta_len = (uint32_t)p.mac_sta.size();
+        out->target_len = (uint32_t)(p.kind == LINE_PMKID ? p.pmkid.size() : p.keymic.size());
+        out->attempts = p.kind == LINE_PMKID ? 1 : L.natt;
+        out->lists = p.kind == LINE_PMKID ? 1 : L.nlists;
+        out->never_matches = tb.never[li];
+        memcpy(out->essid, p.essid.data(), std::min<size_t>(32, p.essid.size()));
+        memcpy(out->mac_ap, p.mac_ap.data(), std::min<size_t>(16, p.mac_ap.size()));
+        memcpy(out->mac_sta, p.mac_sta.data(), std::min<size_t>(16, p.mac_sta.size()));
+        dwpa_hash_m22000(line, line_len, out->hash_m22000);
+        return 0;
+    });
 }
 
 int dwpa_hc_unhex(const uint8_t* in, size_t in_len, uint8_t* out, size_t* out_len) {
-    if ((!in && in_len) || !out || !out_len) return DWPA_E_ARG;
-    std::string r = hc_unhex(std::string((const char*)in, in_len));
-    memcpy(out, r.data(), r.size());
-    *out_len = r.size();
-    return 0;
+    return guarded([&]() -> int {
+        if ((!in && in_len) || !out || !out_len) return DWPA_E_ARG;
+        std::string r = hc_unhex(std::string((const char*)in, in_len));
+        memcpy(out, r.data(), r.size());
+        *out_len = r.size();
+        return 0;
+    });
 }
 
 int dwpa_scan_create(int device, const char* const* lines, const size_t* line_lens, size_t nlines, int nc,
                      int nc_mode, uint32_t batch, dwpa_scan** out) {
-    if ((!lines || !line_lens) && nlines) return DWPA_E_ARG;
-    return scan_create(device, lines, line_lens, nlines, nc, nc_mode, batch, out);
+    return guarded([&]() -> int {
+        if ((!lines || !line_lens) && nlines) return DWPA_E_ARG;
+        return scan_create(device, lines, line_lens, nlines, nc, nc_mode, batch, out);
+    });
 }
 int dwpa_scan_num_groups(const dwpa_scan* scan) { return scan ? (int)scan->groups.size() : DWPA_E_ARG; }
 int dwpa_scan_line_status(const dwpa_scan* scan, size_t line) {
@@ -1684,30 +1733,44 @@ int dwpa_scan_line_status(const dwpa_scan* scan, size_t line) {
 }
 int dwpa_scan_load_dict(dwpa_scan* scan, const uint64_t* d_offsets, const uint8_t* d_bytes, uint64_t first,
                         uint32_t count, uint32_t minlen, uint32_t maxlen, void* hip_stream) {
-    return scan_load_dict(scan, d_offsets, d_bytes, first, count, minlen, maxlen, hip_stream);
+    return guarded([&]() -> int {
+        return scan_load_dict(scan, d_offsets, d_bytes, first, count, minlen, maxlen, hip_stream);
+    });
 }
 int dwpa_scan_load_numeric(dwpa_scan* scan, uint64_t first, uint32_t count, uint32_t digits, void* hip_stream) {
-    return scan_load_numeric(scan, first, count, digits, hip_stream);
+    return guarded([&]() -> int {
+        return scan_load_numeric(scan, first, count, digits, hip_stream);
+    });
 }
-int dwpa_scan_pbkdf2(dwpa_scan* scan, int group, void* hip_stream) { return scan_pbkdf2(scan, group, hip_stream); }
-int dwpa_scan_verify(dwpa_scan* scan, int group, void* hip_stream) { return scan_verify(scan, group, hip_stream); }
-int dwpa_scan_run(dwpa_scan* scan, void* hip_stream) { return scan_run(scan, hip_stream); }
+int dwpa_scan_pbkdf2(dwpa_scan* scan, int group, void* hip_stream) {
+    return guarded([&]() -> int { return scan_pbkdf2(scan, group, hip_stream); });
+}
+int dwpa_scan_verify(dwpa_scan* scan, int group, void* hip_stream) {
+    return guarded([&]() -> int { return scan_verify(scan, group, hip_stream); });
+}
+int dwpa_scan_run(dwpa_scan* scan, void* hip_stream) {
+    return guarded([&]() -> int { return scan_run(scan, hip_stream); });
+}
 int dwpa_scan_hits(dwpa_scan* scan, dwpa_hit* out, size_t cap, size_t* nhits, void* hip_stream) {
-    if (!scan || !nhits || (!out && cap)) return DWPA_E_ARG;
-    std::vector<HitDev> raw;
-    RCHK(scan_hits_raw(scan, raw, hip_stream));
-    *nhits = raw.size();
-    for (size_t i = 0; i < raw.size() && i < cap; i++) hit_to_public(scan, raw[i], out[i]);
-    return raw.size() > cap ? DWPA_E_OVERFLOW : 0;
+    return guarded([&]() -> int {
+        if (!scan || !nhits || (!out && cap)) return DWPA_E_ARG;
+        std::vector<HitDev> raw;
+        RCHK(scan_hits_raw(scan, raw, hip_stream));
+        *nhits = raw.size();
+        for (size_t i = 0; i < raw.size() && i < cap; i++) hit_to_public(scan, raw[i], out[i]);
+        return raw.size() > cap ? DWPA_E_OVERFLOW : 0;
+    });
 }
 int dwpa_scan_loaded(dwpa_scan* scan, uint32_t* count, void* hip_stream) {
-    if (!scan || !count) return DWPA_E_ARG;
-    HIPCHK(hipSetDevice(scan->device));
-    hipStream_t s = as_stream(hip_stream);
-    HIPCHK(hipMemcpyAsync(count, scan->batch.counters.p, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    if (*count > scan->batch_cap) *count = scan->batch_cap;
-    return 0;
+    return guarded([&]() -> int {
+        if (!scan || !count) return DWPA_E_ARG;
+        HIPCHK(hipSetDevice(scan->device));
+        hipStream_t s = as_stream(hip_stream);
+        HIPCHK(hipMemcpyAsync(count, scan->batch.counters.p, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (*count > scan->batch_cap) *count = scan->batch_cap;
+        return 0;
+    });
 }
 void dwpa_scan_destroy(dwpa_scan* scan) { scan_destroy(scan); }
 
@@ -1718,33 +1781,43 @@ static int set_dev(int device) {
     return 0;
 }
 int dwpa_dev_alloc(int device, size_t bytes, void** out) {
-    if (!out) return DWPA_E_ARG;
-    RCHK(set_dev(device));
-    if (hipMalloc(out, bytes ? bytes : 16) != hipSuccess) return DWPA_E_NOMEM;
-    return 0;
+    return guarded([&]() -> int {
+        if (!out) return DWPA_E_ARG;
+        RCHK(set_dev(device));
+        if (hipMalloc(out, bytes ? bytes : 16) != hipSuccess) return DWPA_E_NOMEM;
+        return 0;
+    });
 }
 int dwpa_dev_free(int device, void* p) {
-    RCHK(set_dev(device));
-    if (p) HIPCHK(hipFree(p));
-    return 0;
+    return guarded([&]() -> int {
+        RCHK(set_dev(device));
+        if (p) HIPCHK(hipFree(p));
+        return 0;
+    });
 }
 int dwpa_dev_upload(int device, void* dst, const void* src, size_t bytes) {
-    RCHK(set_dev(device));
-    if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-    return 0;
+    return guarded([&]() -> int {
+        RCHK(set_dev(device));
+        if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        return 0;
+    });
 }
 int dwpa_dev_download(int device, void* dst, const void* src, size_t bytes) {
-    RCHK(set_dev(device));
-    if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
-    return 0;
+    return guarded([&]() -> int {
+        RCHK(set_dev(device));
+        if (bytes) HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+        return 0;
+    });
 }
 int dwpa_stream_create(int device, void** out) {
-    if (!out) return DWPA_E_ARG;
-    RCHK(set_dev(device));
-    hipStream_t s;
-    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    *out = (void*)s;
-    return 0;
+    return guarded([&]() -> int {
+        if (!out) return DWPA_E_ARG;
+        RCHK(set_dev(device));
+        hipStream_t s;
+        HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        *out = (void*)s;
+        return 0;
+    });
 }
 int dwpa_stream_sync(void* stream) {
     HIPCHK(hipStreamSynchronize((hipStream_t)stream));
@@ -1755,12 +1828,14 @@ int dwpa_stream_destroy(void* stream) {
     return 0;
 }
 int dwpa_event_create(int device, void** out) {
-    if (!out) return DWPA_E_ARG;
-    RCHK(set_dev(device));
-    hipEvent_t e;
-    HIPCHK(hipEventCreate(&e));
-    *out = (void*)e;
-    return 0;
+    return guarded([&]() -> int {
+        if (!out) return DWPA_E_ARG;
+        RCHK(set_dev(device));
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        *out = (void*)e;
+        return 0;
+    });
 }
 int dwpa_event_record(void* event, void* stream) {
     HIPCHK(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));

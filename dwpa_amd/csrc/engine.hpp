@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <new>
+#include <stdexcept>
 #include <vector>
 
 #include "dwpa22000.h"
@@ -31,6 +33,23 @@ struct Batch {
 // later fields at their documented defaults).  struct_size 0 = the full current struct.
 #define DWPA_CFG_HAS(cfg, field) \
     ((cfg) && (!(cfg)->struct_size || (cfg)->struct_size >= offsetof(dwpa_config, field) + sizeof((cfg)->field)))
+
+// No C++ exception crosses the C ABI (a PHP-FPM worker or a Python process would be aborted): every entry point that
+// allocates host memory runs its body through guarded(), which maps std::bad_alloc / std::length_error (a host table
+// for an input too large for the machine) to `nomem` and any other exception to `other`.  Locks, call contexts and
+// in-flight device work are held by RAII objects in the bodies, so an unwound call leaves the library usable.
+template <class F>
+inline int guarded(F&& body, int nomem = DWPA_E_NOMEM, int other = DWPA_E_ARG) noexcept {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        return nomem;
+    } catch (const std::length_error&) {
+        return nomem;
+    } catch (...) {
+        return other;
+    }
+}
 
 int engine_init();
 // Rule-file loader mode of the process: dwpa_init's cfg->rule_mode when given, else DWPA_RULE_MODE=full|hashcat

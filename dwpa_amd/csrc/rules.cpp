@@ -263,31 +263,35 @@ void scan_rules_drop(const dwpa_scan* scan) {
 }  // namespace dwpa
 
 extern "C" int dwpa_scan_set_rules(dwpa_scan* scan, const char* rules_text, size_t rules_len) {
-    using namespace dwpa;
-    if (!scan || (!rules_text && rules_len)) return DWPA_E_ARG;
-    scan_rules_drop(scan);
-    auto sr = std::make_unique<ScanRules>();
-    sr->set.load_text(rules_text, rules_len);
-    if (sr->set.size() == 0) return DWPA_E_RULE;
-    int rc = rules_upload(scan_device(scan), sr->set, &sr->dev);
-    if (rc < 0) return rc;
-    const int n = (int)sr->set.size();
-    std::lock_guard<std::mutex> lk(g_rules_mu);
-    g_scan_rules[scan] = std::move(sr);
-    return n;
+    return dwpa::guarded([&]() -> int {
+        using namespace dwpa;
+        if (!scan || (!rules_text && rules_len)) return DWPA_E_ARG;
+        scan_rules_drop(scan);
+        auto sr = std::make_unique<ScanRules>();
+        sr->set.load_text(rules_text, rules_len);
+        if (sr->set.size() == 0) return DWPA_E_RULE;
+        int rc = rules_upload(scan_device(scan), sr->set, &sr->dev);
+        if (rc < 0) return rc;
+        const int n = (int)sr->set.size();
+        std::lock_guard<std::mutex> lk(g_rules_mu);
+        g_scan_rules[scan] = std::move(sr);
+        return n;
+    });
 }
 
 extern "C" int dwpa_scan_load_rules(dwpa_scan* scan, const uint64_t* d_offsets, const uint8_t* d_bytes,
                                     uint64_t first_word, uint32_t nwords, void* hip_stream) {
-    using namespace dwpa;
-    ScanRules* sr = nullptr;
-    {
-        std::lock_guard<std::mutex> lk(g_rules_mu);
-        auto it = g_scan_rules.find(scan);
-        if (it != g_scan_rules.end()) sr = it->second.get();
-    }
-    if (!sr) return DWPA_E_RULE;
-    return rules_load(scan, &sr->dev, d_offsets, d_bytes, first_word, nwords, (hipStream_t)hip_stream);
+    return dwpa::guarded([&]() -> int {
+        using namespace dwpa;
+        ScanRules* sr = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_rules_mu);
+            auto it = g_scan_rules.find(scan);
+            if (it != g_scan_rules.end()) sr = it->second.get();
+        }
+        if (!sr) return DWPA_E_RULE;
+        return rules_load(scan, &sr->dev, d_offsets, d_bytes, first_word, nwords, (hipStream_t)hip_stream);
+    });
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -296,85 +300,91 @@ extern "C" int dwpa_scan_load_rules(dwpa_scan* scan, const uint64_t* d_offsets, 
 // ---------------------------------------------------------------------------------------------------------
 extern "C" int dwpa_rules_count(const char* rules_text, size_t rules_len, uint32_t* nrules_present,
                                 uint32_t* nrules_parsed, uint32_t* first_skipped_line) {
-    using namespace dwpa;
-    if (!rules_text && rules_len) return DWPA_E_ARG;
-    RuleSet rs;
-    rs.quiet = true;
-    rs.load_text(rules_text, rules_len);
-    if (nrules_present) *nrules_present = rs.present;
-    if (nrules_parsed) *nrules_parsed = (uint32_t)rs.size();
-    if (first_skipped_line)
-        *first_skipped_line = rs.skipped_lines.empty() ? 0 : rs.skipped_lines[0];
-    return 0;
+    return dwpa::guarded([&]() -> int {
+        using namespace dwpa;
+        if (!rules_text && rules_len) return DWPA_E_ARG;
+        RuleSet rs;
+        rs.quiet = true;
+        rs.load_text(rules_text, rules_len);
+        if (nrules_present) *nrules_present = rs.present;
+        if (nrules_parsed) *nrules_parsed = (uint32_t)rs.size();
+        if (first_skipped_line)
+            *first_skipped_line = rs.skipped_lines.empty() ? 0 : rs.skipped_lines[0];
+        return 0;
+    });
 }
 
 extern "C" int dwpa_rules_count_ex(const char* rules_text, size_t rules_len, dwpa_rules_counts* out) {
-    using namespace dwpa;
-    if ((!rules_text && rules_len) || !out) return DWPA_E_ARG;
-    RuleSet full;  // the interpreter's load; the hashcat loader keeps its parsed lines without reject / memory ones
-    full.quiet = true;
-    full.load_text(rules_text, rules_len);
-    RuleSet hc;
-    hc.quiet = true;
-    hc.mode = DWPA_RULES_HASHCAT;
-    hc.load_text(rules_text, rules_len);
-    memset(out, 0, sizeof(*out));
-    out->present = full.present;
-    out->parsed = (uint32_t)full.size();
-    out->loaded_hashcat = (uint32_t)hc.size();
-    out->rejmem = hc.rejmem;
-    out->invalid = (uint32_t)full.skipped.size();
-    out->first_invalid_line = full.skipped_lines.empty() ? 0 : full.skipped_lines[0];
-    for (size_t i = 0; i < hc.skipped_lines.size() && !out->first_rejmem_line; i++)
-        if (std::find(full.skipped_lines.begin(), full.skipped_lines.end(), hc.skipped_lines[i]) ==
-            full.skipped_lines.end())
-            out->first_rejmem_line = hc.skipped_lines[i];
-    return 0;
+    return dwpa::guarded([&]() -> int {
+        using namespace dwpa;
+        if ((!rules_text && rules_len) || !out) return DWPA_E_ARG;
+        RuleSet full;  // the interpreter's load; the hashcat loader keeps its parsed lines without reject / memory ones
+        full.quiet = true;
+        full.load_text(rules_text, rules_len);
+        RuleSet hc;
+        hc.quiet = true;
+        hc.mode = DWPA_RULES_HASHCAT;
+        hc.load_text(rules_text, rules_len);
+        memset(out, 0, sizeof(*out));
+        out->present = full.present;
+        out->parsed = (uint32_t)full.size();
+        out->loaded_hashcat = (uint32_t)hc.size();
+        out->rejmem = hc.rejmem;
+        out->invalid = (uint32_t)full.skipped.size();
+        out->first_invalid_line = full.skipped_lines.empty() ? 0 : full.skipped_lines[0];
+        for (size_t i = 0; i < hc.skipped_lines.size() && !out->first_rejmem_line; i++)
+            if (std::find(full.skipped_lines.begin(), full.skipped_lines.end(), hc.skipped_lines[i]) ==
+                full.skipped_lines.end())
+                out->first_rejmem_line = hc.skipped_lines[i];
+        return 0;
+    });
 }
 
 extern "C" int dwpa_rules_expand(int device, const char* rules_text, size_t rules_len, const dwpa_bytes* words,
                                  size_t nwords, uint8_t* out /* nwords*nrules*256 */, uint32_t* out_len,
                                  uint32_t* nrules_out) {
-    using namespace dwpa;
-    if ((!words && nwords) || !nrules_out || (!rules_text && rules_len)) return DWPA_E_ARG;
-    RuleSet rs;
-    rs.quiet = true;  // callers report skipped lines once per file through dwpa_rules_count, not per chunk
-    rs.load_text(rules_text, rules_len);
-    *nrules_out = (uint32_t)rs.size();
-    if (!out || !out_len) return 0;
-    if (rs.size() == 0 || nwords == 0) return 0;
-    int rc = engine_init();
-    if (rc < 0) return rc;
-    if (hipSetDevice(device) != hipSuccess) return DWPA_E_NODEV;
-    std::vector<uint64_t> off(nwords + 1, 0);
-    std::string bytes;
-    for (size_t i = 0; i < nwords; i++) {
-        off[i] = bytes.size();
-        if (words[i].ptr) bytes.append((const char*)words[i].ptr, words[i].len);
-    }
-    off[nwords] = bytes.size();
-    bytes.append(16, '\0');
-    DevRules dr;
-    if ((rc = rules_upload(device, rs, &dr)) < 0) return rc;
-    const size_t ncand = nwords * rs.size();
-    void *d_off = nullptr, *d_bytes = nullptr, *d_out = nullptr, *d_len = nullptr;
-    rc = 0;
-    if (hipMalloc(&d_off, off.size() * 8) || hipMalloc(&d_bytes, bytes.size()) || hipMalloc(&d_out, ncand * 256) ||
-        hipMalloc(&d_len, ncand * 4))
-        rc = DWPA_E_NOMEM;
-    if (!rc && (hipMemcpy(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice) ||
-                hipMemcpy(d_bytes, bytes.data(), bytes.size(), hipMemcpyHostToDevice)))
-        rc = DWPA_E_HIP;
-    if (!rc && launch_rules_expand((const uint64_t*)d_off, (const uint8_t*)d_bytes, (uint32_t)nwords,
-                                   (const uint32_t*)dr.offs, (const uint32_t*)dr.code, dr.nrules, (uint8_t*)d_out,
-                                   (uint32_t*)d_len, nullptr) != hipSuccess)
-        rc = DWPA_E_HIP;
-    if (!rc && (hipMemcpy(out, d_out, ncand * 256, hipMemcpyDeviceToHost) ||
-                hipMemcpy(out_len, d_len, ncand * 4, hipMemcpyDeviceToHost)))
-        rc = DWPA_E_HIP;
-    (void)hipFree(d_off); (void)hipFree(d_bytes); (void)hipFree(d_out); (void)hipFree(d_len);
-    rules_release(&dr);
-    return rc;
+    return dwpa::guarded([&]() -> int {
+        using namespace dwpa;
+        if ((!words && nwords) || !nrules_out || (!rules_text && rules_len)) return DWPA_E_ARG;
+        RuleSet rs;
+        rs.quiet = true;  // callers report skipped lines once per file through dwpa_rules_count, not per chunk
+        rs.load_text(rules_text, rules_len);
+        *nrules_out = (uint32_t)rs.size();
+        if (!out || !out_len) return 0;
+        if (rs.size() == 0 || nwords == 0) return 0;
+        int rc = engine_init();
+        if (rc < 0) return rc;
+        if (hipSetDevice(device) != hipSuccess) return DWPA_E_NODEV;
+        std::vector<uint64_t> off(nwords + 1, 0);
+        std::string bytes;
+        for (size_t i = 0; i < nwords; i++) {
+            off[i] = bytes.size();
+            if (words[i].ptr) bytes.append((const char*)words[i].ptr, words[i].len);
+        }
+        off[nwords] = bytes.size();
+        bytes.append(16, '\0');
+        DevRules dr;
+        if ((rc = rules_upload(device, rs, &dr)) < 0) return rc;
+        const size_t ncand = nwords * rs.size();
+        void *d_off = nullptr, *d_bytes = nullptr, *d_out = nullptr, *d_len = nullptr;
+        rc = 0;
+        if (hipMalloc(&d_off, off.size() * 8) || hipMalloc(&d_bytes, bytes.size()) || hipMalloc(&d_out, ncand * 256) ||
+            hipMalloc(&d_len, ncand * 4))
+            rc = DWPA_E_NOMEM;
+        if (!rc && (hipMemcpy(d_off, off.data(), off.size() * 8, hipMemcpyHostToDevice) ||
+                    hipMemcpy(d_bytes, bytes.data(), bytes.size(), hipMemcpyHostToDevice)))
+            rc = DWPA_E_HIP;
+        if (!rc && launch_rules_expand((const uint64_t*)d_off, (const uint8_t*)d_bytes, (uint32_t)nwords,
+                                       (const uint32_t*)dr.offs, (const uint32_t*)dr.code, dr.nrules, (uint8_t*)d_out,
+                                       (uint32_t*)d_len, nullptr) != hipSuccess)
+            rc = DWPA_E_HIP;
+        if (!rc && (hipMemcpy(out, d_out, ncand * 256, hipMemcpyDeviceToHost) ||
+                    hipMemcpy(out_len, d_len, ncand * 4, hipMemcpyDeviceToHost)))
+            rc = DWPA_E_HIP;
+        (void)hipFree(d_off); (void)hipFree(d_bytes); (void)hipFree(d_out); (void)hipFree(d_len);
+        rules_release(&dr);
+        return rc;
+    });
 }
 
 // Host-only application of rule `rule_index` (0-based among the rules of rules_text that parse) to one word: the
@@ -382,18 +392,20 @@ extern "C" int dwpa_rules_expand(int device, const char* rules_text, size_t rule
 // 0xFFFFFFFF when it is rejected.  For parity tests without a device and for reporting a hit's PSK.
 extern "C" int dwpa_rules_apply_host(const char* rules_text, size_t rules_len, uint32_t rule_index, const uint8_t* word,
                                      size_t word_len, uint8_t* out /* 256 bytes */, uint32_t* out_len) {
-    using namespace dwpa;
-    if ((!rules_text && rules_len) || (!word && word_len) || !out || !out_len) return DWPA_E_ARG;
-    RuleSet rs;
-    rs.quiet = true;
-    rs.load_text(rules_text, rules_len);
-    if (rule_index >= rs.size()) return DWPA_E_RULE;
-    std::string cand;
-    if (!rs.apply_host(rule_index, std::string((const char*)word, word_len), &cand)) {
-        *out_len = 0xFFFFFFFFu;
+    return dwpa::guarded([&]() -> int {
+        using namespace dwpa;
+        if ((!rules_text && rules_len) || (!word && word_len) || !out || !out_len) return DWPA_E_ARG;
+        RuleSet rs;
+        rs.quiet = true;
+        rs.load_text(rules_text, rules_len);
+        if (rule_index >= rs.size()) return DWPA_E_RULE;
+        std::string cand;
+        if (!rs.apply_host(rule_index, std::string((const char*)word, word_len), &cand)) {
+            *out_len = 0xFFFFFFFFu;
+            return 0;
+        }
+        memcpy(out, cand.data(), cand.size());
+        *out_len = (uint32_t)cand.size();
         return 0;
-    }
-    memcpy(out, cand.data(), cand.size());
-    *out_len = (uint32_t)cand.size();
-    return 0;
+    });
 }

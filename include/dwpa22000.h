@@ -67,6 +67,10 @@ extern "C" {
 #define DWPA_NC_PHP 0          /* common.php:250-300: N+0, then V+k,V-k,N+k,N-k for k = 1..(nc>>1)+1, $n mutated */
 #define DWPA_NC_HASHCAT 1      /* hashcat --nonce-error-corrections=N: N+0, then +-k, k = 1..N, message_pair bits
                                   0x10 (no NC), 0x20 (LE only), 0x40 (BE only) honoured (third-party semantics)   */
+#define DWPA_NC_MAX 65536      /* the largest nc / nonce_error_corrections taken (PHP mode: 131,077 attempts per key;
+                                  the reference's call sites pass <= ~2 x nets.nc + 128).  A larger one on an EAPOL
+                                  line is DWPA_E_ARG for that job, so the PHP wrapper runs the original
+                                  check_key_m22000 for it; dwpa_scan_create / dwpa_crack_files refuse it.          */
 
 typedef struct {
     const uint8_t *ptr;        /* NULL = PHP null key (skipped, common.php:172,240) */

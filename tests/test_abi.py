@@ -106,3 +106,47 @@ def test_php_ffi_cdef_matches_header():
         return re.sub(r"\s+([,);])", r"\1", s)
     for proto in re.findall(r"^\s*((?:int|const char \*)\s*dwpa_\w+\(.*?\);)", cdef, flags=re.M | re.S):
         assert norm(proto) in norm(hdr), proto
+
+
+def test_nc_bound():
+    """DWPA_NC_MAX: the header's bound, what it admits, and DWPA_E_ARG above it for EAPOL lines only (PHP ignores nc
+    for PMKID lines); the PHP wrapper answers such a job with the original check_key_m22000 (codes <= -10)."""
+    from dwpa_amd import m22000 as M
+    hdr = open(L.HEADER).read()
+    assert re.search(r"#define DWPA_NC_MAX (\d+)", hdr).group(1) == str(L.DWPA_NC_MAX)
+    pmkid, eapol = S.CHALLENGE_LINES
+    info = M.parse_m22000(eapol, L.DWPA_NC_MAX)
+    assert info["attempts"] == 1 + 4 * ((L.DWPA_NC_MAX >> 1) + 1)
+    assert M.parse_m22000(eapol, L.DWPA_NC_MAX, L.DWPA_NC_HASHCAT)["attempts"] == 1 + 4 * L.DWPA_NC_MAX
+    assert M.parse_m22000(eapol, L.DWPA_NC_MAX + 1) == L.DWPA_E_ARG
+    assert M.parse_m22000(eapol, 2**31 - 1, L.DWPA_NC_HASHCAT) == L.DWPA_E_ARG
+    assert M.parse_m22000(eapol, -(2**31))["attempts"] == 1
+    assert M.parse_m22000(pmkid, 2**31 - 1)["attempts"] == 1
+    assert L.DWPA_E_ARG <= -10  # so php/dwpa22000.php falls back, never answers False
+
+
+_NOMEM_CHILD = r"""
+import ctypes, resource, sys
+sys.path.insert(0, sys.argv[1])
+from dwpa_amd import _lib as L
+lib = L.load()
+text = b":\n" * 20_000_000  # 40 MB of rules: the parsed set needs several times that
+c = L.RulesCounts()
+soft, hard = resource.getrlimit(resource.RLIMIT_AS)
+vm = int([l for l in open("/proc/self/status") if l.startswith("VmSize")][0].split()[1]) * 1024
+resource.setrlimit(resource.RLIMIT_AS, (vm + (64 << 20), hard))
+rc = lib.dwpa_rules_count_ex(text, len(text), ctypes.byref(c))
+print(rc)
+"""
+
+
+def test_no_exception_crosses_the_c_abi():
+    """A host allocation that fails inside the library (std::bad_alloc) comes back as DWPA_E_NOMEM instead of
+    aborting the caller's process (a PHP-FPM worker, help_crack): the child caps its address space, then asks the
+    library to parse a rules text whose tables do not fit."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _NOMEM_CHILD, root], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip() == str(L.DWPA_E_NOMEM), (r.stdout, r.stderr[-2000:])
