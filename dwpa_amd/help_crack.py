@@ -140,6 +140,9 @@ def run_cracker(conf: dict, dictlist, nonce_error_corrections: int = NONCE_ERROR
     rules_file, mask, nec = _parse_options(conf.get("rules", ""), conf.get("coptions", ""))
     if nec is not None:
         nonce_error_corrections = nec
+    if nonce_error_corrections > L.DWPA_NC_MAX:  # deterministic: the library refuses it on every attempt
+        pprint(f"--nonce-error-corrections={nonce_error_corrections} is above the supported {L.DWPA_NC_MAX}", "FAIL")
+        raise L.DwpaError(L.DWPA_E_ARG, f"nonce_error_corrections {nonce_error_corrections} > {L.DWPA_NC_MAX}")
     key_file = conf["key_file"]
     dictlist = list(dictlist)
     tries = 0

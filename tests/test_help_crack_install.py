@@ -178,3 +178,16 @@ def test_coptions_nonce_error_corrections(standin, monkeypatch, co, exp):
     open("help_crack.hash", "w").write("x\n")
     hc.conf["coptions"] = co
     assert hc.run_cracker(["a.gz"]) == 1 and seen == [exp]
+
+
+def test_coptions_nonce_error_corrections_above_the_bound(standin, monkeypatch):
+    """A -co value above DWPA_NC_MAX is refused at once (DWPA_E_ARG), not retried forever by the failure loop."""
+    calls = []
+    monkeypatch.setattr(H.M, "crack_files_ex", lambda *a, **k: calls.append(a) or (1, []))
+    H.install(standin.HelpCrack)
+    hc = standin.HelpCrack()
+    open("help_crack.hash", "w").write("x\n")
+    hc.conf["coptions"] = f"--nonce-error-corrections={L.DWPA_NC_MAX + 1}"
+    with pytest.raises(L.DwpaError) as e:
+        hc.run_cracker(["a.gz"])
+    assert e.value.code == L.DWPA_E_ARG and not calls
