@@ -321,12 +321,12 @@ class DictReader {
             while (p < end && c.words() < max_words && c.bytes.size() < max_bytes) {
                 const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
                 if (!nl) {
-                    partial_.append(p, (size_t)(end - p));
+                    keep_partial(p, (size_t)(end - p));
                     p = end;
                     break;
                 }
                 if (!partial_.empty()) {
-                    partial_.append(p, (size_t)(nl - p));
+                    keep_partial(p, (size_t)(nl - p));
                     emit(c, partial_.data(), partial_.size());
                     partial_.clear();
                 } else {
@@ -343,8 +343,18 @@ class DictReader {
     // The reader reached the end of every file: nothing was cut short by a cancel or an error.
     bool complete() { return finished_ && src_.complete(); }
 
+    // A line is kept up to MAX_LINE bytes: every consumer rejects a word that long (the 8..63 PSK filter, the rule
+    // engine's 256-byte words, hashcat's --stdout), a $HEX[] form cut short no longer decodes and stays as long, and
+    // the line still counts as one word -- but a file of binary garbage without a '\n' no longer needs its whole
+    // size in host memory.
+    static constexpr size_t MAX_LINE = 1u << 20;
+
   private:
+    void keep_partial(const char* p, size_t k) {
+        if (partial_.size() < MAX_LINE) partial_.append(p, std::min(k, MAX_LINE - partial_.size()));
+    }
     static void emit(Chunk& c, const char* p, size_t k) {
+        k = std::min(k, MAX_LINE);
         if (k && p[k - 1] == '\r') k--;
         if (k > 5 && p[0] == '$' && starts_hex((const uint8_t*)p, k)) c.bytes += hc_unhex(std::string(p, k));
         else c.bytes.append(p, k);

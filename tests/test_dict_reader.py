@@ -190,3 +190,21 @@ def test_item_queue_covers_every_word_and_balances_workers(tmp_path):
             w = [x["words"] for x in d["workers"]]
             if workers > 1 and path == plain:
                 assert max(w) <= 2 * n / workers, (workers, w)
+
+
+def test_reader_caps_overlong_lines(tmp_path):
+    """A line longer than the reader's 1 MiB cap (binary garbage without a '\\n', a runaway line) is still one word,
+    kept to its first MiB -- every consumer rejects a word that long -- and the next line comes through intact, in
+    plain and gzip files, across the 4 MiB inflate blocks."""
+    subprocess.run(["make", "-s", "-C", ROOT, "tools/bin/inflate_bench"], check=True)
+    cap = 1 << 20
+    hexline = b"$HEX[" + b"41" * (3 * cap) + b"]"
+    data = b"first\n" + b"\x00" * (5 * cap) + b"\nnext\r\n" + hexline + b"\nlast"
+    plain, gz = tmp_path / "long.txt", tmp_path / "long.txt.gz"
+    plain.write_bytes(data)
+    with gzip.open(gz, "wb", compresslevel=1) as f:
+        f.write(data)
+    r = subprocess.run([TOOL, "--dump", str(plain), str(gz)], capture_output=True, check=True)
+    got = [bytes.fromhex(l) for l in r.stdout.decode().split("\n")[:-1]]
+    one = [b"first", b"\x00" * cap, b"next", hexline[:cap], b"last"]
+    assert got == one + one
