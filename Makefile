@@ -59,7 +59,7 @@ clean:
 
 tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
        tools/bin/inflate_check tools/bin/item_queue_check tools/bin/rules_fuzz_asan tools/bin/clock_idle \
-       tools/bin/inflate_check_tsan tools/bin/tail_placement
+       tools/bin/inflate_check_tsan tools/bin/tail_placement tools/bin/parse_fuzz_asan
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -98,6 +98,11 @@ tools/bin/rules_fuzz_asan: tools/rules_fuzz.cpp $(SRC)/rules.cpp $(SRC)/rules.hp
 	@mkdir -p tools/bin
 	$(HIPCC) -O1 -g -std=c++17 -Iinclude -I$(SRC) -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
 	    -o $@ tools/rules_fuzz.cpp $(SRC)/rules.cpp
+
+tools/bin/parse_fuzz_asan: tools/parse_fuzz.cpp $(SRC)/m22000_host.cpp $(SRC)/m22000_host.hpp $(SRC)/tables.hpp
+	@mkdir -p tools/bin
+	$(HIPCC) -O1 -g -std=c++17 -Iinclude -I$(SRC) -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+	    -o $@ tools/parse_fuzz.cpp $(SRC)/m22000_host.cpp
 
 tools/bin/clock_idle: tools/clock_idle.hip
 	@mkdir -p tools/bin
