@@ -40,6 +40,8 @@ final class Dwpa22000
     /* a cold worker sends a derive to the GPU only from this many keys on: PHP's ~1.1 ms per key then costs about what
      * the first call does (~0.2-0.3 s for a worker started alone, up to ~0.7 s in a start-up storm of 16) */
     const COLD_MIN_KEYS = 256;
+    /* DWPA_NC_MAX: the largest nc the library takes; the ABI's nc is an int32 */
+    const NC_MAX = 65536;
 
     public static function ffi()
     {
@@ -71,8 +73,17 @@ CDEF;
         if (function_exists('check_key_m22000_php')) {
             return check_key_m22000_php($hashline, $keys, $pmk, $nc);
         }
-        $msg = $rc === null ? 'caller PMK is not 32 bytes' : FFI::string(self::ffi()->dwpa_strerror($rc));
+        $msg = $rc === null ? 'caller PMK is not 32 bytes, or nc is out of range'
+                            : FFI::string(self::ffi()->dwpa_strerror($rc));
         throw new Dwpa22000Error("libdwpa22000: $msg (rc $rc)");
+    }
+
+    /* an $nc the library reads as PHP does: FFI would wrap a PHP int outside int32, and the library refuses one
+     * above DWPA_NC_MAX (an EAPOL job; PHP ignores $nc for PMKID lines, but such calls are left to PHP as well) */
+    public static function nc_ok($nc)
+    {
+        $v = (int) $nc;
+        return $v >= -2147483648 && $v <= self::NC_MAX;
     }
 
     /* a caller PMK the ABI can take: `if (!$pmk)` (common.php:178) means derive; otherwise exactly 32 bytes */
@@ -136,7 +147,7 @@ CDEF;
 
 function check_key_m22000_gpu($hashline, $keys, $pmk = False, $nc = 128)
 {
-    if (!Dwpa22000::pmk_ok($pmk)) {
+    if (!Dwpa22000::pmk_ok($pmk) || !Dwpa22000::nc_ok($nc)) {
         return Dwpa22000::fallback(null, $hashline, $keys, $pmk, $nc);
     }
     $ffi = Dwpa22000::ffi();
@@ -168,7 +179,7 @@ function check_keys_m22000_gpu_batch($jobs)
     $gpu = [];                                       // indices of the jobs the library checks
     foreach ($jobs as $i => $job) {
         $args[$i] = $job + [null, [], False, 128];
-        if (Dwpa22000::pmk_ok($args[$i][2])) {
+        if (Dwpa22000::pmk_ok($args[$i][2]) && Dwpa22000::nc_ok($args[$i][3])) {
             $gpu[] = $i;
         }
     }
@@ -210,7 +221,7 @@ function check_keys_m22000_gpu_batch($jobs)
         }
     }
     foreach ($args as $i => $a) {
-        if (!Dwpa22000::pmk_ok($a[2])) {
+        if (!Dwpa22000::pmk_ok($a[2]) || !Dwpa22000::nc_ok($a[3])) {
             $res[$i] = Dwpa22000::fallback(null, $a[0], $a[1], $a[2], $a[3]);
         }
     }

@@ -80,7 +80,8 @@ def test_single_check_code_map():
     body = _function(_src(), "check_key_m22000_gpu")
     steps, tail = _decide(body)
     assert steps == [
-        ("!Dwpa22000::pmk_ok($pmk)", "Dwpa22000::fallback(null, $hashline, $keys, $pmk, $nc)"),
+        ("!Dwpa22000::pmk_ok($pmk) || !Dwpa22000::nc_ok($nc)",
+         "Dwpa22000::fallback(null, $hashline, $keys, $pmk, $nc)"),
         ("$rc == Dwpa22000::HIT", "Dwpa22000::result($vals, $res)"),
         ("Dwpa22000::is_device_error($rc)", "Dwpa22000::fallback($rc, $hashline, $keys, $pmk, $nc)"),
     ]
@@ -95,8 +96,10 @@ def test_batch_code_map():
     assert re.search(r"if \(\$jrc == Dwpa22000::HIT\) \{\s*\$res\[\$i\] = Dwpa22000::result", body)
     assert re.search(r"elseif \(\$rc < 0 \|\| Dwpa22000::is_device_error\(\$jrc\)\) \{.*?Dwpa22000::fallback\(\$jrc,",
                      body, flags=re.S)
-    # jobs whose PMK the ABI cannot take go to the PHP check, not to the library
-    assert re.search(r"if \(!Dwpa22000::pmk_ok\(\$a\[2\]\)\) \{\s*\$res\[\$i\] = Dwpa22000::fallback\(null,", body)
+    # jobs whose PMK or nc the ABI cannot take go to the PHP check, not to the library
+    assert "if (Dwpa22000::pmk_ok($args[$i][2]) && Dwpa22000::nc_ok($args[$i][3])) {" in body
+    assert re.search(r"if \(!Dwpa22000::pmk_ok\(\$a\[2\]\) \|\| !Dwpa22000::nc_ok\(\$a\[3\]\)\) \{\s*"
+                     r"\$res\[\$i\] = Dwpa22000::fallback\(null,", body)
 
 
 def test_pmk_is_never_padded_or_truncated():
@@ -134,3 +137,13 @@ def test_routed_check_accounts_for_the_cold_first_call():
     assert line.split("*")[3:6] == ["020000000001", "020000000002", "7761726d7570"]
     import dwpa_amd
     assert dwpa_amd.parse_m22000(line)["type"] == 1  # the warm-up line is a valid PMKID line
+
+
+def test_nc_outside_the_abi_goes_to_php():
+    """A PHP int outside int32 would be wrapped by FFI, and one above DWPA_NC_MAX is refused by the library: such an
+    $nc goes to the original check (the result stays PHP's), for single and batch calls alike."""
+    src = _src()
+    hdr = open(L.HEADER).read()
+    assert _const(src, "NC_MAX") == int(re.search(r"#define DWPA_NC_MAX (\d+)", hdr).group(1)) == L.DWPA_NC_MAX
+    ok = _function(src, "nc_ok")
+    assert "$v = (int) $nc;" in ok and "return $v >= -2147483648 && $v <= self::NC_MAX;" in ok
