@@ -80,6 +80,14 @@ def _result(keys, r: L.Result):
     return [key, int(r.nc), _ENDIAN[int(r.endian)], pmk]
 
 
+def _nc(nc) -> int:
+    """The ABI's nc is an int32: a value outside it would be wrapped by ctypes into a different window."""
+    v = int(nc)
+    if not -2**31 <= v < 2**31:
+        raise L.DwpaError(L.DWPA_E_ARG, f"nc {v} is outside int32")
+    return v
+
+
 def check_key_m22000(hashline, keys, pmk=False, nc: int = 128):
     """Drop-in for PHP check_key_m22000($hashline, $keys, $pmk=False, $nc=128)."""
     h = _b(hashline)
@@ -89,7 +97,7 @@ def check_key_m22000(hashline, keys, pmk=False, nc: int = 128):
     pm = bytes(pmk) if pmk else None  # PHP: `if (!$pmk)` -- False/''/None all mean "derive"
     if pm is not None and len(pm) != 32:
         raise ValueError("pmk must be 32 bytes")
-    rc = L.check(L.load().dwpa_check_m22000(h, len(h), arr, len(keys), pm, int(nc), ctypes.byref(res)),
+    rc = L.check(L.load().dwpa_check_m22000(h, len(h), arr, len(keys), pm, _nc(nc), ctypes.byref(res)),
                  "check_m22000")
     if rc != L.DWPA_HIT:
         return False
@@ -115,7 +123,7 @@ class BatchJobs:
             c = self.carr[i]
             c.line, c.line_len = h, len(h)
             c.keys, c.nkeys = ctypes.cast(arr, ctypes.POINTER(L.Bytes)), len(keys)
-            c.pmk, c.nc = pm, int(nc)
+            c.pmk, c.nc = pm, _nc(nc)
         self.nkeys = sum(len(k) for k in self.key_lists)
         self.out = (L.Result * max(1, n))()
         self.rcs = (ctypes.c_int * max(1, n))()

@@ -150,3 +150,15 @@ def test_no_exception_crosses_the_c_abi():
     r = subprocess.run([sys.executable, "-c", _NOMEM_CHILD, root], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip() == str(L.DWPA_E_NOMEM), (r.stdout, r.stderr[-2000:])
+
+
+def test_python_nc_outside_int32_is_refused():
+    """ctypes would wrap an nc outside int32 into a different window; the Python API refuses it before any call."""
+    import dwpa_amd
+    pmkid = S.CHALLENGE_LINES[0]
+    for nc in (2**31, -2**31 - 1, 2**40 + 8):
+        with pytest.raises(L.DwpaError) as e:
+            dwpa_amd.check_key_m22000(pmkid, [b"aaaa1234"], False, nc)
+        assert e.value.code == L.DWPA_E_ARG
+        with pytest.raises(L.DwpaError):
+            dwpa_amd.check_batch([(pmkid, [b"aaaa1234"], False, nc)])
