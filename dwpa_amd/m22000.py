@@ -259,7 +259,7 @@ def crack_files_ex(hash_file, dicts, rules_file=None, nonce_error_corrections: i
     darr = (ctypes.c_char_p * max(1, len(dl)))(*dl)
     st = (ctypes.c_int32 * max(1, len(dl)))()
     rc = L.load().dwpa_crack_files_ex(_b(hash_file), darr, len(dl), _b(rules_file) if rules_file else None,
-                                      int(nonce_error_corrections), _b(out_file), ctypes.byref(cfg), st)
+                                      _nc(nonce_error_corrections), _b(out_file), ctypes.byref(cfg), st)
     return rc, [int(st[i]) for i in range(len(dl))]
 
 
@@ -287,7 +287,7 @@ class Scan:
         lp = (ctypes.c_char_p * max(1, n))(*self.lines)
         ll = (ctypes.c_size_t * max(1, n))(*[len(x) for x in self.lines])
         h = ctypes.c_void_p()
-        L.check(self._lib.dwpa_scan_create(device, lp, ll, n, int(nc), int(nc_mode), int(batch), ctypes.byref(h)),
+        L.check(self._lib.dwpa_scan_create(device, lp, ll, n, _nc(nc), int(nc_mode), int(batch), ctypes.byref(h)),
                 "scan_create")
         self._h = h
         self.batch = (int(batch) + 63) & ~63
