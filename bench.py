@@ -450,13 +450,19 @@ def spawn_ranks(args) -> int:
     return 0
 
 
-def check_device(local: int, rank: int) -> None:
-    """Fail loudly when this rank's GPU is not visible (a node with fewer GPUs than --gpus)."""
+def check_device(local: int, rank: int) -> int:
+    """This rank's device index.  LOCAL_RANK when every GPU is visible; 0 when the launcher gave the rank its own GPU
+    (HIP/ROCR/CUDA_VISIBLE_DEVICES naming exactly one); otherwise fail loudly (a node with fewer GPUs than --gpus)."""
     import dwpa_amd
     n = dwpa_amd.device_count()
-    if local >= n:
-        raise SystemExit(f"bench.py rank {rank}: device {local} not visible ({n} gfx950 devices); "
-                         "DWPA_BENCH_ONE_DEVICE=1 rehearses N ranks on one GPU")
+    if local < n:
+        return local
+    vis = next((os.environ[v] for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+                if os.environ.get(v)), None)
+    if n == 1 and vis is not None and len(vis.split(",")) == 1:
+        return 0
+    raise SystemExit(f"bench.py rank {rank}: device {local} not visible ({n} gfx950 devices); "
+                     "DWPA_BENCH_ONE_DEVICE=1 rehearses N ranks on one GPU")
 
 
 def main():
@@ -484,7 +490,7 @@ def main():
         local = 0  # rehearsal of the N>1 control path with every rank on one GPU (not a scaling measurement)
     if args.dry_run:
         return main_dry(args, world, rank)
-    check_device(local, rank)
+    local = check_device(local, rank)
     if args.workload in ("c1", "c5"):
         return main_ffi(args, world, rank, local)
     if args.workload == "c2files":

@@ -119,3 +119,23 @@ def test_ranks_die_with_the_parent():
         time.sleep(0.2)
     alive = [k for k in kids if os.path.exists(f"/proc/{k}") and open(f"/proc/{k}/stat").read().split()[2] != "Z"]
     assert not alive, alive
+
+
+def test_rank_device_index(monkeypatch):
+    """A rank uses its LOCAL_RANK as the device index; when the launcher gave it its own GPU (one device visible and
+    HIP/ROCR/CUDA_VISIBLE_DEVICES naming one), index 0; with fewer GPUs than ranks and no such variable it fails."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import dwpa_amd
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setattr(dwpa_amd, "device_count", lambda: 8)
+    assert bench.check_device(5, 5) == 5
+    monkeypatch.setattr(dwpa_amd, "device_count", lambda: 1)
+    with pytest.raises(SystemExit):
+        bench.check_device(5, 5)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "5")
+    assert bench.check_device(5, 5) == 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "4,5")
+    with pytest.raises(SystemExit):
+        bench.check_device(5, 5)
