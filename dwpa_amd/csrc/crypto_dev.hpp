@@ -137,32 +137,66 @@ __device__ __forceinline__ Sha1Mid sha1_mid(const uint32_t h[5]) {
 constexpr bool w84_var(int s) { return s >= 16 || s <= 4; }
 constexpr uint32_t w84_const(int s) { return s == 5 ? 0x80000000u : s == 15 ? 672u : 0u; }
 
-// W[T] before the rotate: XOR of the variable sources plus the folded constant, fewest VALU ops.
+// W[T]: the recurrence applied 2^j times -- for T >= 16 * 2^j,
+//   W[T] = rotl(W[T - 3s] ^ W[T - 8s] ^ W[T - 14s] ^ W[T - 16s], s),  s = 2^j
+// (j = 0 is the schedule's definition; j = 1 and j = 2 follow by substituting it into itself).  Each form costs one
+// rotate; the XORs depend on how many of its four sources are variable.  The 84-byte message's zero words W6..W14
+// make the j = 1 form cheaper for T = 34..46 and the j = 2 form for T = 64..78: 84 instead of 112 XOR-type ops per
+// compression, at the price of keeping W0..W4 and W16..W22 live longer.  DWPA_SCHED_WIDE is the largest j used
+// (0 = the plain recurrence).
+#ifndef DWPA_SCHED_WIDE
+#define DWPA_SCHED_WIDE 1
+#endif
+constexpr uint32_t sched84_const(int T, int j) {
+    const int sh = 1 << j;
+    return (w84_var(T - 3 * sh) ? 0u : w84_const(T - 3 * sh)) ^ (w84_var(T - 8 * sh) ? 0u : w84_const(T - 8 * sh)) ^
+           (w84_var(T - 14 * sh) ? 0u : w84_const(T - 14 * sh)) ^ (w84_var(T - 16 * sh) ? 0u : w84_const(T - 16 * sh));
+}
+constexpr int sched84_nv(int T, int j) {
+    const int sh = 1 << j;
+    return (int)w84_var(T - 3 * sh) + (int)w84_var(T - 8 * sh) + (int)w84_var(T - 14 * sh) + (int)w84_var(T - 16 * sh);
+}
+// XOR-type ops of form j: a 3-input op takes two more terms, the folded constant counts as one term
+constexpr int sched84_cost(int T, int j) { return (sched84_nv(T, j) + (sched84_const(T, j) != 0u ? 1 : 0)) / 2; }
+#ifndef DWPA_SCHED_J2_MIN
+#define DWPA_SCHED_J2_MIN 64
+#endif
+constexpr int sched84_form(int T) {
+    int best = 0;
+    for (int j = 1; j <= DWPA_SCHED_WIDE; j++)
+        if (T >= (16 << j) && (j < 2 || T >= DWPA_SCHED_J2_MIN) && sched84_cost(T, j) < sched84_cost(T, best))
+            best = j;
+    return best;
+}
+
+// W[T] (T >= 16) from the full message array w[0..T-1] (compile-time indices: registers, not memory).
 template <int T>
-__device__ __forceinline__ uint32_t sched84(const uint32_t w[16]) {
-    constexpr int s0 = T - 3, s1 = T - 8, s2 = T - 14, s3 = T - 16;
-    constexpr uint32_t K = (w84_var(s0) ? 0u : w84_const(s0)) ^ (w84_var(s1) ? 0u : w84_const(s1)) ^
-                           (w84_var(s2) ? 0u : w84_const(s2)) ^ (w84_var(s3) ? 0u : w84_const(s3));
-    constexpr int nv = (int)w84_var(s0) + (int)w84_var(s1) + (int)w84_var(s2) + (int)w84_var(s3);
+__device__ __forceinline__ uint32_t sched84(const uint32_t w[80]) {
+    constexpr int j = sched84_form(T), sh = 1 << j;
+    constexpr int s0 = T - 3 * sh, s1 = T - 8 * sh, s2 = T - 14 * sh, s3 = T - 16 * sh;
+    constexpr uint32_t K = sched84_const(T, j);
+    constexpr int nv = sched84_nv(T, j);
     uint32_t v[4] = {0, 0, 0, 0};
     int n = 0;
-    if constexpr (w84_var(s0)) v[n++] = w[s0 & 15];
-    if constexpr (w84_var(s1)) v[n++] = w[s1 & 15];
-    if constexpr (w84_var(s2)) v[n++] = w[s2 & 15];
-    if constexpr (w84_var(s3)) v[n++] = w[s3 & 15];
-    if constexpr (nv == 4) return xor3(v[0], v[1], v[2]) ^ v[3];
+    if constexpr (w84_var(s0)) v[n++] = w[s0];
+    if constexpr (w84_var(s1)) v[n++] = w[s1];
+    if constexpr (w84_var(s2)) v[n++] = w[s2];
+    if constexpr (w84_var(s3)) v[n++] = w[s3];
+    uint32_t x;
+    if constexpr (nv == 4) x = xor3(v[0], v[1], v[2]) ^ v[3];
     else if constexpr (nv == 3) {
-        if constexpr (K == 0) return xor3(v[0], v[1], v[2]);
-        else return xor3(v[0], v[1], v[2]) ^ K;
+        if constexpr (K == 0) x = xor3(v[0], v[1], v[2]);
+        else x = xor3(v[0], v[1], v[2]) ^ K;
     } else if constexpr (nv == 2) {
-        if constexpr (K == 0) return v[0] ^ v[1];
-        else return xor3s(v[0], v[1], K);
+        if constexpr (K == 0) x = v[0] ^ v[1];
+        else x = xor3s(v[0], v[1], K);
     } else if constexpr (nv == 1) {
-        if constexpr (K == 0) return v[0];
-        else return v[0] ^ K;
+        if constexpr (K == 0) x = v[0];
+        else x = v[0] ^ K;
     } else {
-        return K;
+        x = K;
     }
+    return rotl(x, (uint32_t)sh);
 }
 
 // Issue-slot spacer.  On gfx950 a wave whose VALU stream mixes 4-cycle ops (alignbit, add3) with 2-cycle ops
@@ -174,7 +208,7 @@ __device__ __forceinline__ void spacer() {
 }
 
 template <int T, int NOP = 0>
-__device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[16]) {
+__device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[80]) {
     uint32_t f;
     if constexpr (T < 20) f = ch3(b, c, d);
     else if constexpr (T < 40) f = xor3(b, c, d);
@@ -187,9 +221,9 @@ __device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, ui
         uint32_t wt;
         if constexpr (T < 16) wt = w[T];
         else {
-            wt = rotl(sched84<T>(w), 1);
+            wt = sched84<T>(w);
             spacer<NOP, 1>();
-            w[T & 15] = wt;
+            w[T] = wt;
         }
         t = rotl(a, 5) + f + e + sha1_k<T>() + wt;
     }
@@ -199,14 +233,14 @@ __device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, ui
 }
 
 template <int NOP, int T0, int... Ts>
-__device__ __forceinline__ void steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[16],
+__device__ __forceinline__ void steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[80],
                                         std::integer_sequence<int, T0, Ts...>) {
     step84<T0, NOP>(a, b, c, d, e, w);
     if constexpr (sizeof...(Ts) > 0) steps84<NOP>(a, b, c, d, e, w, std::integer_sequence<int, Ts...>{});
 }
 template <int Lo, int NOP, int... Is>
 __device__ __forceinline__ void run_steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
-                                            uint32_t w[16], std::integer_sequence<int, Is...>) {
+                                            uint32_t w[80], std::integer_sequence<int, Is...>) {
     steps84<NOP>(a, b, c, d, e, w, std::integer_sequence<int, (Lo + Is)...>{});
 }
 
@@ -215,7 +249,7 @@ __device__ __forceinline__ void run_steps84(uint32_t& a, uint32_t& b, uint32_t& 
 // rounds 2-79 use the constant-folded message schedule above.
 template <int NOP = 0>
 __device__ __forceinline__ void sha1_84(const Sha1Mid& M, const uint32_t in[5], uint32_t out[5]) {
-    uint32_t w[16];
+    uint32_t w[80];
     w[0] = in[0]; w[1] = in[1]; w[2] = in[2]; w[3] = in[3]; w[4] = in[4];
 #pragma unroll
     for (int i = 5; i < 16; i++) w[i] = w84_const(i);
