@@ -31,12 +31,13 @@ NC = 8          # nonce-error-corrections of the client (help_crack.py:773); the
 NC_MODE = 1     # DWPA_NC_HASHCAT: N+0 then +-1..+-8 in both endians = 33 attempts per candidate
 # Roofline.  Work unit: 16,388 SHA-1 compressions per PMK (north_star).  Bound: integer
 # VALU issue.  Measured on gfx950 (tools/valu_peak, profiles/r01/valu_issue_costs.json): xor/bitop3/add_u32 take
-# 2 SIMD cycles per wave64 instruction, alignbit (rotate) and add3 take 4, so the cheapest HMAC inner-loop
-# compression costs C_MIN = 1878.5 SIMD-cycles per wave (64 lanes; derivation in DESIGN.md section 4).
+# 2 SIMD cycles per wave64 instruction, alignbit (rotate) and add3 take 4, so the cheapest known HMAC inner-loop
+# compression costs C_MIN = 1822.5 SIMD-cycles per wave (64 lanes; derivation in DESIGN.md section 4 and
+# tools/cmin.py: with the schedule identities of round 5; rounds 1-4 priced it at 1878.5 with the plain recurrence).
 COMPRESSIONS_PER_PMK = 16388
 SIMDS, CLOCK_HZ = 256 * 4, 2.4e9
 from tools.cmin import c_min  # noqa: E402  (the C_min model; tools/regen_peak.sh re-measures its inputs)
-C_MIN_CYCLES = c_min()  # 1878.5 at full rate 2 / half rate 4 SIMD-cycles per wave instruction
+C_MIN_CYCLES = c_min()  # 1822.5 at full rate 2 / half rate 4 SIMD-cycles per wave instruction
 PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
 # HBM traffic per PMK of the kernel each workload's roofline names, from the PMC passes of tools/profile_traffic.sh
 # over that workload's bench command (FETCH_SIZE doubled as MI355X_MICROARCH.md "HBM [CDNA4]" prescribes, plus
@@ -60,10 +61,11 @@ TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950_q, profiles/r05/pmc_final",
 ALGO_BYTES_PER_PMK = 40 + 32
 # Guide view (MI355X_MICROARCH.md: 4 SIMD-32 per CU, one VALU per 2 cycles = 128 int32 lane-ops/clk/CU at 2.4 GHz,
 # every op full rate).  Reported beside the issue-cost roofline, with SURVEY.md 8(d)'s ideal 617 ops per compression
-# and with the 575.5 VALU the kernel issues per compression (4,714,742 per wave / 8,192 compressions, PMC).  Not
+# and with the 562.5 VALU the kernel issues per compression (1,125 per loop iteration of two compressions, round 5's
+# schedule identities; 575.5 before them, 4,714,742 per wave / 8,192 compressions in PMC).  Not
 # attainable on gfx950, where v_alignbit/v_add3/v_bfi issue at half rate (profiles/r01/valu_issue_costs.json).
 SURVEY_OPS_PER_COMPRESSION = 617
-ISSUED_OPS_PER_COMPRESSION = 575.5
+ISSUED_OPS_PER_COMPRESSION = 562.5
 PEAK_LANE_OPS = 256 * 128 * CLOCK_HZ
 
 

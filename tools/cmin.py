@@ -7,11 +7,15 @@ half-rate cost (v_alignbit / v_add3), the cheapest HMAC inner-loop compression o
     78 rounds x (rotl5 h + rotl30 h + f() f + 4 adds min(4f, 2h))
   - one add in each of the 14 rounds whose K+W or e+K is loop-invariant      (-14 f)
   + rounds 0-1 folded into midstate invariants                                (5 f)
-  + schedule: 64 rotl1 + 112 xor/bitop3                                       (64 h + 112 f)
+  + schedule: 64 rotates + SCHED_XORS xor/bitop3                             (64 h + SCHED_XORS f)
   + digest adds                                                               (5 f)
   + T ^= U, 5 xors per two compressions (one of them folded)                  (1.25 f)
 
-SIMD-cycles per wave per compression; C_min = 1,878.5 at f = 2, h = 4.  Peak = SIMDs x clock x 64 / C_min.
+SCHED_XORS is the schedule's XOR-type op count (tools/sched_identities.py).  The plain recurrence needs 112; rounds 1-4
+priced the model on that, C_min = 1,878.5.  Round 5 found that the recurrence applied 2^j times reaches the message's
+zero words: 99 ops with j <= 1, which is what the kernel runs (DWPA_SCHED_WIDE=1, 61 VGPRs), and 84 with j <= 2, whose
+longer live ranges spill at 8 waves.  The model takes the cheapest known form, 84: C_min = 1,822.5 at f = 2, h = 4.
+Peak = SIMDs x clock x 64 / C_min.
 
     python tools/cmin.py profiles/r02/valu_issue_costs.json     # prints the peak from a fresh measurement
 """
@@ -25,8 +29,11 @@ HALF_OPS = ("v_alignbit_b32", "v_add3_u32")
 SIMDS, CLOCK_HZ, COMPRESSIONS_PER_PMK = 1024, 2.4e9, 16388
 
 
-def c_min(f: float = 2.0, h: float = 4.0) -> float:
-    return 78 * (2 * h + f + min(4 * f, 2 * h)) - 14 * f + 5 * f + (64 * h + 112 * f) + 5 * f + 1.25 * f
+SCHED_XORS = 84  # the cheapest known schedule (j <= 2); the kernel's j <= 1 form has 99
+
+
+def c_min(f: float = 2.0, h: float = 4.0, sched_xors: int = SCHED_XORS) -> float:
+    return 78 * (2 * h + f + min(4 * f, 2 * h)) - 14 * f + 5 * f + (64 * h + sched_xors * f) + 5 * f + 1.25 * f
 
 
 def from_costs(path: str) -> dict:
