@@ -9,7 +9,7 @@ HDRS := $(wildcard $(SRC)/*.hpp) include/dwpa22000.h
 OBJS := $(OBJ)/kernels.o $(OBJ)/rules_dev.o $(OBJ)/engine.o $(OBJ)/m22000_host.o $(OBJ)/crack.o $(OBJ)/rules.o \
         $(OBJ)/pbkdf2_module.o $(OBJ)/pbkdf2_hsaco.o
 LLVM := /opt/rocm/lib/llvm/bin
-ISSUE_RULE ?= before_half
+ISSUE_RULE ?= sched=1:alt,before_half
 
 all: $(LIB) oracle
 
@@ -26,7 +26,7 @@ build/pbkdf2/pbkdf2_gfx950.s: $(SRC)/pbkdf2_gfx950.hip $(SRC)/pbkdf2_dev.hpp $(S
 	@mkdir -p build/pbkdf2
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 --cuda-device-only -S $< -o $@
 
-build/pbkdf2/pbkdf2_issue.s: build/pbkdf2/pbkdf2_gfx950.s $(SRC)/gen/issue_pass.py
+build/pbkdf2/pbkdf2_issue.s: build/pbkdf2/pbkdf2_gfx950.s $(SRC)/gen/issue_pass.py Makefile
 	python3 $(SRC)/gen/issue_pass.py $< $@ k_pbkdf2_gfx950+k_pbkdf2_gfx950_ms+k_pbkdf2_gfx950_mg+k_pbkdf2_gfx950_p+k_pbkdf2_gfx950_ms_p+k_pbkdf2_gfx950_mg_p+k_pbkdf2_gfx950_q+k_pbkdf2_gfx950_mg_q $(ISSUE_RULE)
 
 build/pbkdf2/pbkdf2_gfx950.hsaco: build/pbkdf2/pbkdf2_issue.s
