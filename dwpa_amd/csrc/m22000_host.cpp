@@ -22,13 +22,6 @@ namespace dwpa {
 static bool is_xd(uint8_t c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
 static int hv(uint8_t c) { return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10; }
 
-// valid_hex(), common.php:28-36 (ctype_xdigit("") is false)
-static bool valid_hex(const char* s, size_t n) {
-    if (n == 0 || (n & 1)) return false;
-    for (size_t i = 0; i < n; i++)
-        if (!is_xd((uint8_t)s[i])) return false;
-    return true;
-}
 static void hex2bin_into(const char* s, size_t n, std::string& o) {
     o.resize(n / 2);
     for (size_t i = 0; i < n / 2; i++) o[i] = (char)(hv((uint8_t)s[2 * i]) << 4 | hv((uint8_t)s[2 * i + 1]));
