@@ -170,7 +170,11 @@ def nopify(lines, kernel, rules):
     for r in rules:
         if r.startswith("sched="):
             arg = r.split("=", 1)[1].split(":")
-            body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:], "group" in arg[1:])
+            try:
+                body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:], "group" in arg[1:])
+            except ValueError as err:  # e.g. a hazard s_nop of another compiler: keep its order, spacers still apply
+                sys.stderr.write(f"issue_pass: {kernel}: {r} skipped ({err})\n")
+                continue
             lines = lines[:h + 1] + body + lines[e:]
             e = h + 1 + len(body)
     if "split_add3" in rules:
