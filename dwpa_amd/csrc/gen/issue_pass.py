@@ -21,10 +21,11 @@ Rules (comma-separated, applied in the loop body only):
   nop1            use s_nop 1 instead of s_nop 0
   split_add3      rewrite every v_add3_u32 as two v_add_u32_e32 (same adds, mod 2^32; 4-cycle op -> two 2-cycle
                   ops), applied before the nop rules (A/B: fewer half-rate ops in the stream)
-  sched=D[:alt|:group]  list-schedule the loop body again (VGPR/SGPR/SCC dependences kept, registers unchanged) so
-                  that an instruction issues at least D VALU slots after the producers of its operands where the
-                  dependences allow; `alt` also prefers alternating 2-/4-cycle ops, `group` runs of one rate (fewer
-                  2 <-> 4-cycle transitions, for lone waves).  Applied before the nop rules (A/B)
+  sched=D[:alt|:group][:orig]  list-schedule the loop body again (VGPR/SGPR/SCC dependences kept, registers
+                  unchanged) so that an instruction issues at least D VALU slots after the producers of its operands
+                  where the dependences allow; `alt` also prefers alternating 2-/4-cycle ops, `group` runs of one
+                  rate (fewer 2 <-> 4-cycle transitions, for lone waves); ties go to the longest remaining critical
+                  path, or with `orig` to the compiler's order.  Applied before the nop rules (A/B)
   none            copy through
 """
 import re
@@ -103,7 +104,7 @@ def _defs_uses(line):
     raise ValueError(f"unexpected instruction in the loop body: {line!r}")
 
 
-def reschedule(body, dmin, alt, group=False):
+def reschedule(body, dmin, alt, group=False, orig=False):
     """Greedy list schedule of a straight-line loop body (see the sched rule)."""
     ins = []
     for l in body:
@@ -150,7 +151,7 @@ def reschedule(body, dmin, alt, group=False):
             dist = min((len(order) - pos[j] for j in raw[i]), default=dmin)
             half = ins[i][1].replace("_e32", "").replace("_e64", "") in HALF
             return (min(dist, dmin), alt and prev_half is not None and half != prev_half,
-                    group and prev_half is not None and half == prev_half, cp[i], -i)
+                    group and prev_half is not None and half == prev_half, *((-i, cp[i]) if orig else (cp[i], -i)))
         i = max(ready, key=key)
         ready.discard(i)
         pos[i] = len(order)
@@ -171,7 +172,7 @@ def nopify(lines, kernel, rules):
         if r.startswith("sched="):
             arg = r.split("=", 1)[1].split(":")
             try:
-                body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:], "group" in arg[1:])
+                body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:], "group" in arg[1:], "orig" in arg[1:])
             except ValueError as err:  # e.g. a hazard s_nop of another compiler: keep its order, spacers still apply
                 sys.stderr.write(f"issue_pass: {kernel}: {r} skipped ({err})\n")
                 continue
