@@ -6,7 +6,7 @@ EVERY instruction at the 4-cycle rate, even with 8 waves per SIMD; homogeneous s
 scalar `s_nop 0` in front of each 4-cycle op restores near-additive issue: the PBKDF2 loop goes from 3.9 to ~3.4
 SIMD-cycles per VALU instruction (+15.7 % PMK/s) with the instruction stream otherwise unchanged.  Source-level
 `asm volatile("s_nop 0")` cannot do this -- LLVM hoists the register-only VALU ops over it -- hence the pass on
-the compiler's assembly.  The product rule (the Makefile's ISSUE_RULE) is `sched=1:alt,before_half` since round 5
+the compiler's assembly.  The product rule (the Makefile's ISSUE_RULE) is `sched=1:alt:orig,before_half` since round 5
 (`before_half` before it; profiles/r05/issue_rules_sched/).
 
 Rules (comma-separated, applied in the loop body only):
