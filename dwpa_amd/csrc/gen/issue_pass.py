@@ -21,11 +21,12 @@ Rules (comma-separated, applied in the loop body only):
   nop1            use s_nop 1 instead of s_nop 0
   split_add3      rewrite every v_add3_u32 as two v_add_u32_e32 (same adds, mod 2^32; 4-cycle op -> two 2-cycle
                   ops), applied before the nop rules (A/B: fewer half-rate ops in the stream)
-  sched=D[:alt|:group][:orig]  list-schedule the loop body again (VGPR/SGPR/SCC dependences kept, registers
+  sched=D[:alt|:group][:orig][:asmnop]  list-schedule the loop body again (VGPR/SGPR/SCC dependences kept, registers
                   unchanged) so that an instruction issues at least D VALU slots after the producers of its operands
                   where the dependences allow; `alt` also prefers alternating 2-/4-cycle ops, `group` runs of one
                   rate (fewer 2 <-> 4-cycle transitions, for lone waves); ties go to the longest remaining critical
-                  path, or with `orig` to the compiler's order.  Applied before the nop rules (A/B)
+                  path, or with `orig` to the compiler's order; `asmnop` first drops the s_nop LLVM places after
+                  inline-asm blocks (the loop's v_bitop3 ops).  Applied before the nop rules (A/B)
   none            copy through
 """
 import re
@@ -171,8 +172,14 @@ def nopify(lines, kernel, rules):
     for r in rules:
         if r.startswith("sched="):
             arg = r.split("=", 1)[1].split(":")
+            body = lines[h + 1:e]
+            if "asmnop" in arg[1:]:
+                # LLVM puts an `s_nop 0` after an inline-asm block it cannot see into; after the loop's
+                # v_bitop3_b32 blocks (VGPR in, VGPR out, no hazard between VALU ops) it is dead weight
+                body = [l for k, l in enumerate(body)
+                        if not (l.strip() == "s_nop 0" and k and body[k - 1].strip() == ";;#ASMEND")]
             try:
-                body = reschedule(lines[h + 1:e], int(arg[0]), "alt" in arg[1:], "group" in arg[1:], "orig" in arg[1:])
+                body = reschedule(body, int(arg[0]), "alt" in arg[1:], "group" in arg[1:], "orig" in arg[1:])
             except ValueError as err:  # e.g. a hazard s_nop of another compiler: keep its order, spacers still apply
                 sys.stderr.write(f"issue_pass: {kernel}: {r} skipped ({err})\n")
                 continue
