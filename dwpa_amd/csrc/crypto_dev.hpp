@@ -143,7 +143,9 @@ constexpr uint32_t w84_const(int s) { return s == 5 ? 0x80000000u : s == 15 ? 67
 // rotate; the XORs depend on how many of its four sources are variable.  The 84-byte message's zero words W6..W14
 // make the j = 1 form cheaper for T = 34..46 and the j = 2 form for T = 64..78: 84 instead of 112 XOR-type ops per
 // compression, at the price of keeping W0..W4 and W16..W22 live longer.  DWPA_SCHED_WIDE is the largest j used
-// (0 = the plain recurrence).
+// (0 = the plain recurrence) and DWPA_SCHED_J2_MIN the first t that may use j = 2: j <= 1 by default (the lone-wave
+// kernels of kernels.hip), j = 2 from t = 73 in the issue-pass kernels, which define both at the top of
+// pbkdf2_gfx950.hip (profiles/r05/sched_identities/).
 #ifndef DWPA_SCHED_WIDE
 #define DWPA_SCHED_WIDE 1
 #endif
