@@ -133,57 +133,74 @@ __device__ __forceinline__ Sha1Mid sha1_mid(const uint32_t h[5]) {
     return m;
 }
 
-// Message words of the 84-byte HMAC inner/outer message: W0..W4 variable, W5 = 0x80000000, W6..W14 = 0, W15 = 672.
-constexpr bool w84_var(int s) { return s >= 16 || s <= 4; }
-constexpr uint32_t w84_const(int s) { return s == 5 ? 0x80000000u : s == 15 ? 672u : 0u; }
+// Message layouts with compile-time words: var(s) says whether W[s] (s < 16) is a run-time value, cst(s) is its value
+// otherwise.  Words past 15 are schedule words (run-time).
+// Msg84: the 84-byte HMAC inner/outer message (a 20-byte digest after a 64-byte pad block): W0..W4 variable,
+// W5 = 0x80000000, W6..W14 = 0, W15 = 672.
+struct Msg84 {
+    static constexpr bool var(int s) { return s >= 16 || s <= 4; }
+    static constexpr uint32_t cst(int s) { return s == 5 ? 0x80000000u : s == 15 ? 672u : 0u; }
+};
+// MsgKey<NV, P>: an HMAC key pad block of a key of NV words (PMK: 8, KCK: 4): W[s] = key[s] ^ P for s < NV, P after.
+template <int NV, uint32_t P>
+struct MsgKey {
+    static constexpr bool var(int s) { return s >= 16 || s < NV; }
+    static constexpr uint32_t cst(int s) { return s >= NV && s < 16 ? P : 0u; }
+};
+constexpr bool w84_var(int s) { return Msg84::var(s); }
+constexpr uint32_t w84_const(int s) { return Msg84::cst(s); }
 
 // W[T]: the recurrence applied 2^j times -- for T >= 16 * 2^j,
 //   W[T] = rotl(W[T - 3s] ^ W[T - 8s] ^ W[T - 14s] ^ W[T - 16s], s),  s = 2^j
 // (j = 0 is the schedule's definition; j = 1 and j = 2 follow by substituting it into itself).  Each form costs one
-// rotate; the XORs depend on how many of its four sources are variable.  The 84-byte message's zero words W6..W14
-// make the j = 1 form cheaper for T = 34..46 and the j = 2 form for T = 64..78: 84 instead of 112 XOR-type ops per
-// compression, at the price of keeping W0..W4 and W16..W22 live longer.  DWPA_SCHED_WIDE is the largest j used
-// (0 = the plain recurrence) and DWPA_SCHED_J2_MIN the first t that may use j = 2: j <= 1 by default (the lone-wave
-// kernels of kernels.hip), j = 2 from t = 73 in the issue-pass kernels, which define both at the top of
-// pbkdf2_gfx950.hip (profiles/r05/sched_identities/).
+// rotate; the XORs depend on how many of its four sources are variable (compile-time words fold into one constant).
+// The 84-byte message's zero words W6..W14 make the j = 1 form cheaper for T = 34..46 and the j = 2 form for
+// T = 64..78: 84 instead of 112 XOR-type ops per compression, at the price of keeping W0..W4 and W16..W22 live
+// longer.  DWPA_SCHED_WIDE is the largest j used (0 = the plain recurrence) and DWPA_SCHED_J2_MIN the first t that may
+// use j = 2: j <= 1 by default (the lone-wave kernels of kernels.hip), j = 2 from t = 73 in the issue-pass kernels,
+// which define both at the top of pbkdf2_gfx950.hip (profiles/r05/sched_identities/).
 #ifndef DWPA_SCHED_WIDE
 #define DWPA_SCHED_WIDE 1
 #endif
-constexpr uint32_t sched84_const(int T, int j) {
+template <class M>
+constexpr uint32_t sched_const(int T, int j) {
     const int sh = 1 << j;
-    return (w84_var(T - 3 * sh) ? 0u : w84_const(T - 3 * sh)) ^ (w84_var(T - 8 * sh) ? 0u : w84_const(T - 8 * sh)) ^
-           (w84_var(T - 14 * sh) ? 0u : w84_const(T - 14 * sh)) ^ (w84_var(T - 16 * sh) ? 0u : w84_const(T - 16 * sh));
+    return (M::var(T - 3 * sh) ? 0u : M::cst(T - 3 * sh)) ^ (M::var(T - 8 * sh) ? 0u : M::cst(T - 8 * sh)) ^
+           (M::var(T - 14 * sh) ? 0u : M::cst(T - 14 * sh)) ^ (M::var(T - 16 * sh) ? 0u : M::cst(T - 16 * sh));
 }
-constexpr int sched84_nv(int T, int j) {
+template <class M>
+constexpr int sched_nv(int T, int j) {
     const int sh = 1 << j;
-    return (int)w84_var(T - 3 * sh) + (int)w84_var(T - 8 * sh) + (int)w84_var(T - 14 * sh) + (int)w84_var(T - 16 * sh);
+    return (int)M::var(T - 3 * sh) + (int)M::var(T - 8 * sh) + (int)M::var(T - 14 * sh) + (int)M::var(T - 16 * sh);
 }
 // XOR-type ops of form j: a 3-input op takes two more terms, the folded constant counts as one term
-constexpr int sched84_cost(int T, int j) { return (sched84_nv(T, j) + (sched84_const(T, j) != 0u ? 1 : 0)) / 2; }
+template <class M>
+constexpr int sched_cost(int T, int j) { return (sched_nv<M>(T, j) + (sched_const<M>(T, j) != 0u ? 1 : 0)) / 2; }
 #ifndef DWPA_SCHED_J2_MIN
 #define DWPA_SCHED_J2_MIN 64
 #endif
-constexpr int sched84_form(int T) {
+template <class M>
+constexpr int sched_form(int T) {
     int best = 0;
     for (int j = 1; j <= DWPA_SCHED_WIDE; j++)
-        if (T >= (16 << j) && (j < 2 || T >= DWPA_SCHED_J2_MIN) && sched84_cost(T, j) < sched84_cost(T, best))
+        if (T >= (16 << j) && (j < 2 || T >= DWPA_SCHED_J2_MIN) && sched_cost<M>(T, j) < sched_cost<M>(T, best))
             best = j;
     return best;
 }
 
-// W[T] (T >= 16) from the full message array w[0..T-1] (compile-time indices: registers, not memory).
-template <int T>
-__device__ __forceinline__ uint32_t sched84(const uint32_t w[80]) {
-    constexpr int j = sched84_form(T), sh = 1 << j;
+// W[T] (T >= 16) of layout M from the full message array w[0..T-1] (compile-time indices: registers, not memory).
+template <class M, int T>
+__device__ __forceinline__ uint32_t sched_w(const uint32_t w[80]) {
+    constexpr int j = sched_form<M>(T), sh = 1 << j;
     constexpr int s0 = T - 3 * sh, s1 = T - 8 * sh, s2 = T - 14 * sh, s3 = T - 16 * sh;
-    constexpr uint32_t K = sched84_const(T, j);
-    constexpr int nv = sched84_nv(T, j);
+    constexpr uint32_t K = sched_const<M>(T, j);
+    constexpr int nv = sched_nv<M>(T, j);
     uint32_t v[4] = {0, 0, 0, 0};
     int n = 0;
-    if constexpr (w84_var(s0)) v[n++] = w[s0];
-    if constexpr (w84_var(s1)) v[n++] = w[s1];
-    if constexpr (w84_var(s2)) v[n++] = w[s2];
-    if constexpr (w84_var(s3)) v[n++] = w[s3];
+    if constexpr (M::var(s0)) v[n++] = w[s0];
+    if constexpr (M::var(s1)) v[n++] = w[s1];
+    if constexpr (M::var(s2)) v[n++] = w[s2];
+    if constexpr (M::var(s3)) v[n++] = w[s3];
     uint32_t x;
     if constexpr (nv == 4) x = xor3(v[0], v[1], v[2]) ^ v[3];
     else if constexpr (nv == 3) {
@@ -209,21 +226,21 @@ __device__ __forceinline__ void spacer() {
     if constexpr ((NOP & WHERE) != 0) asm volatile("s_nop 0");
 }
 
-template <int T, int NOP = 0>
-__device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[80]) {
+template <class M, int T, int NOP = 0>
+__device__ __forceinline__ void step_m(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[80]) {
     uint32_t f;
     if constexpr (T < 20) f = ch3(b, c, d);
     else if constexpr (T < 40) f = xor3(b, c, d);
     else if constexpr (T < 60) f = maj3(b, c, d);
     else f = xor3(b, c, d);
     uint32_t t;
-    if constexpr (T < 16 && !w84_var(T)) {
-        t = rotl(a, 5) + f + e + (sha1_k<T>() + w84_const(T));
+    if constexpr (T < 16 && !M::var(T)) {
+        t = rotl(a, 5) + f + e + (sha1_k<T>() + M::cst(T));
     } else {
         uint32_t wt;
         if constexpr (T < 16) wt = w[T];
         else {
-            wt = sched84<T>(w);
+            wt = sched_w<M, T>(w);
             spacer<NOP, 1>();
             w[T] = wt;
         }
@@ -234,16 +251,16 @@ __device__ __forceinline__ void step84(uint32_t& a, uint32_t& b, uint32_t& c, ui
     spacer<NOP, 4>();
 }
 
-template <int NOP, int T0, int... Ts>
-__device__ __forceinline__ void steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[80],
+template <class M, int NOP, int T0, int... Ts>
+__device__ __forceinline__ void steps_m(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e, uint32_t w[80],
                                         std::integer_sequence<int, T0, Ts...>) {
-    step84<T0, NOP>(a, b, c, d, e, w);
-    if constexpr (sizeof...(Ts) > 0) steps84<NOP>(a, b, c, d, e, w, std::integer_sequence<int, Ts...>{});
+    step_m<M, T0, NOP>(a, b, c, d, e, w);
+    if constexpr (sizeof...(Ts) > 0) steps_m<M, NOP>(a, b, c, d, e, w, std::integer_sequence<int, Ts...>{});
 }
-template <int Lo, int NOP, int... Is>
-__device__ __forceinline__ void run_steps84(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
+template <class M, int Lo, int NOP, int... Is>
+__device__ __forceinline__ void run_steps_m(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d, uint32_t& e,
                                             uint32_t w[80], std::integer_sequence<int, Is...>) {
-    steps84<NOP>(a, b, c, d, e, w, std::integer_sequence<int, (Lo + Is)...>{});
+    steps_m<M, NOP>(a, b, c, d, e, w, std::integer_sequence<int, (Lo + Is)...>{});
 }
 
 // out <- SHA1_compress(M, in[0..4] || 0x80 || 0.. || bitlen(64+20)): the PBKDF2/HMAC inner-loop compression
@@ -258,7 +275,7 @@ __device__ __forceinline__ void sha1_84(const Sha1Mid& M, const uint32_t in[5], 
     uint32_t a1 = M.c0 + w[0];
     uint32_t a2 = rotl(a1, 5) + M.c1 + w[1];
     uint32_t a = a2, b = a1, c = M.r0, d = M.r1, e = M.h2;
-    run_steps84<2, NOP>(a, b, c, d, e, w, std::make_integer_sequence<int, 78>{});
+    run_steps_m<Msg84, 2, NOP>(a, b, c, d, e, w, std::make_integer_sequence<int, 78>{});
     out[0] = M.h0 + a; out[1] = M.h1 + b; out[2] = M.h2 + c; out[3] = M.h3 + d; out[4] = M.h4 + e;
 }
 
@@ -286,6 +303,27 @@ __device__ __forceinline__ void sha1_compress_kw(uint32_t st[5], const uint32_t*
 
 __device__ __forceinline__ void sha1_iv(uint32_t st[5]) {
     st[0] = SHA1_IV0; st[1] = SHA1_IV1; st[2] = SHA1_IV2; st[3] = SHA1_IV3; st[4] = SHA1_IV4;
+}
+
+// SHA1_compress(IV, key ^ P || P..P) for a key of NV words: an HMAC ipad (P = 0x36363636) or opad (0x5c5c5c5c)
+// midstate, with the pad words folded into the schedule (MsgKey).  The verifiers' PMK (8 words) and KCK (4 words).
+template <int NV, uint32_t P>
+__device__ __forceinline__ void sha1_keypad(const uint32_t* key, uint32_t out[5]) {
+    uint32_t w[80];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = i < NV ? key[i] ^ P : P;
+    uint32_t a = SHA1_IV0, b = SHA1_IV1, c = SHA1_IV2, d = SHA1_IV3, e = SHA1_IV4;
+    run_steps_m<MsgKey<NV, P>, 0, 0>(a, b, c, d, e, w, std::make_integer_sequence<int, 80>{});
+    out[0] = SHA1_IV0 + a; out[1] = SHA1_IV1 + b; out[2] = SHA1_IV2 + c; out[3] = SHA1_IV3 + d; out[4] = SHA1_IV4 + e;
+}
+// HMAC-SHA1 midstates of a 32-byte key (the PMK).
+__device__ __forceinline__ void sha1_hmac_mid_pmk(const uint32_t p[8], uint32_t ipad[5], uint32_t opad[5]) {
+    sha1_keypad<8, 0x36363636u>(p, ipad);
+    sha1_keypad<8, 0x5c5c5c5cu>(p, opad);
+}
+// HMAC outer hash over a 20-byte inner digest: the 84-byte message's folded schedule (sha1_84) from the opad state.
+__device__ __forceinline__ void sha1_outer20(const uint32_t opad[5], const uint32_t in[5], uint32_t out[5]) {
+    sha1_84(sha1_mid(opad), in, out);
 }
 
 // HMAC-SHA1 key block (<= 64 bytes, big-endian words, zero padded) -> ipad / opad midstates.

@@ -214,14 +214,6 @@ __device__ __forceinline__ void md5_blocks_km(uint32_t st[4], const uint32_t* __
     for (uint32_t b = 0; b < nblk; b++) md5_compress_km(st, km + b * MD5_KM_WORDS);
 }
 
-// HMAC outer hash over a 20-byte inner digest (generic state, no invariant folding).
-__device__ __forceinline__ void sha1_outer20(const uint32_t opad[5], const uint32_t in[5], uint32_t out[5]) {
-    uint32_t m[16] = {in[0], in[1], in[2], in[3], in[4], 0x80000000u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 672u};
-#pragma unroll
-    for (int k = 0; k < 5; k++) out[k] = opad[k];
-    sha1_compress(out, m);
-}
-
 // Block b of an attempt's PRF stream: shared words with the attempt's two patched words substituted
 // (LineDev.patch_w0/_w1; NO_PATCH never matches, so explicit per-attempt blocks pass through unchanged).
 __device__ __forceinline__ void att_block(const uint32_t* __restrict__ w, uint32_t b, uint32_t pw0, uint32_t pw1,
@@ -272,16 +264,16 @@ template <uint32_t VC>
 __device__ __forceinline__ void eapol_key(const LineDev& L, const uint32_t* __restrict__ pool, const uint32_t p[8],
                                           EapolKey& K) {
     constexpr bool has12 = (VC & (VC_KV1 | VC_KV2)) != 0, has3 = (VC & VC_KV3) != 0;
-    uint32_t kb[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
     if (has12 && (!has3 || L.keyver != 3)) {
         uint32_t ip1[5];
-        sha1_hmac_mid(kb, ip1, K.op1);
+        sha1_hmac_mid_pmk(p, ip1, K.op1);
 #pragma unroll
         for (int k = 0; k < 5; k++) K.pre1[k] = ip1[k];
         sha1_blocks_kw(K.pre1, pool + L.pre_off, L.pre_nblk);
     } else if constexpr (has3) {
+        uint32_t kb[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
         uint32_t ip2[8];
         sha256_hmac_mid(kb, ip2, K.op2);
 #pragma unroll
@@ -321,16 +313,10 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         if (has2 && (!has1 || L.keyver == 2)) {
             // HMAC-SHA1(KCK, EAPOL): the opad midstate is computed after the inner hash so that the two key-pad
             // compressions are not live at the same time (keeps this class inside 64 VGPRs)
-            uint32_t blk[16], mi[5], mo[5];
-#pragma unroll
-            for (int k = 0; k < 16; k++) blk[k] = (k < 4 ? ptk[k] : 0u) ^ 0x36363636u;
-            sha1_iv(mi);
-            sha1_compress(mi, blk);
+            uint32_t mi[5], mo[5];
+            sha1_keypad<4, 0x36363636u>(ptk, mi);
             sha1_blocks_kw(mi, pool + L.mic_off, L.mic_nblk);
-#pragma unroll
-            for (int k = 0; k < 16; k++) blk[k] = (k < 4 ? ptk[k] : 0u) ^ 0x5c5c5c5cu;
-            sha1_iv(mo);
-            sha1_compress(mo, blk);
+            sha1_keypad<4, 0x5c5c5c5cu>(ptk, mo);
             uint32_t o[5];
             sha1_outer20(mo, mi, o);
             mic[0] = o[0]; mic[1] = o[1]; mic[2] = o[2]; mic[3] = o[3];
@@ -502,11 +488,8 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
 
     constexpr bool has_pmkid = (VC & VC_PMKID) != 0, has_eapol = (VC & ~VC_PMKID) != 0;
     if (has_pmkid && (!has_eapol || L.kind == LINE_PMKID)) {
-        uint32_t kb[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) kb[k] = k < 8 ? p[k] : 0u;
         uint32_t ip[5], op[5], st[5], out[5];
-        sha1_hmac_mid(kb, ip, op);
+        sha1_hmac_mid_pmk(p, ip, op);
 #pragma unroll
         for (int k = 0; k < 5; k++) st[k] = ip[k];
         sha1_blocks_kw(st, pool + L.msg_off, L.msg_nblk);

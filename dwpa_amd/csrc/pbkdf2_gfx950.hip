@@ -2,7 +2,7 @@
 // VALU issue pass (gen/issue_pass.py, the Makefile's ISSUE_RULE), assembled to a code object and embedded in
 // libdwpa22000.so (see Makefile); launched with hipModuleLaunchKernel (pbkdf2_module.cpp).
 //
-// These multi-wave kernels take the j = 2 schedule forms from round 73 on (crypto_dev.hpp sched84: 1,116 VALU per
+// These multi-wave kernels take the j = 2 schedule forms from round 73 on (crypto_dev.hpp sched_w: 1,116 VALU per
 // loop iteration, 64 VGPRs, no spill): with the issue pass's list scheduler they measured -0.9 % at 8 waves per SIMD
 // and -0.3 % at 6 against j <= 1 (profiles/r05/sched_identities/).  The lone-wave kernels in kernels.hip keep
 // j <= 1, which is faster there (one-key call 8.17 against 8.29 ms).

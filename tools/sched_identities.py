@@ -2,7 +2,7 @@
 W5 = 0x80000000, W6..W14 = 0, W15 = 672) when W[t] may use the recurrence applied 2^j times:
 W[t] = rotl(W[t-3s] ^ W[t-8s] ^ W[t-14s] ^ W[t-16s], s), s = 2^j, t >= 16s.  A 3-input XOR takes two more terms,
 the folded constant counts as one term.  python3 tools/sched_identities.py -> per max-j totals and the t that change
-(crypto_dev.hpp sched84; profiles/r05/sched_identities/)."""
+(crypto_dev.hpp sched_w; profiles/r05/sched_identities/)."""
 KIND = ["v"] * 5 + ["c"] + ["z"] * 9 + ["c"]
 
 
