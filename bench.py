@@ -61,11 +61,11 @@ TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950_q, profiles/r05/pmc_final",
 ALGO_BYTES_PER_PMK = 40 + 32
 # Guide view (MI355X_MICROARCH.md: 4 SIMD-32 per CU, one VALU per 2 cycles = 128 int32 lane-ops/clk/CU at 2.4 GHz,
 # every op full rate).  Reported beside the issue-cost roofline, with SURVEY.md 8(d)'s ideal 617 ops per compression
-# and with the 562.5 VALU the kernel issues per compression (1,125 per loop iteration of two compressions, round 5's
-# schedule identities; 575.5 before them, 4,714,742 per wave / 8,192 compressions in PMC).  Not
+# and with the 558 VALU the kernel issues per compression (1,116 per loop iteration of two compressions with round 5's
+# schedule identities in k_pbkdf2_gfx950_q; 575.5 before them, 4,714,742 per wave / 8,192 compressions in PMC).  Not
 # attainable on gfx950, where v_alignbit/v_add3/v_bfi issue at half rate (profiles/r01/valu_issue_costs.json).
 SURVEY_OPS_PER_COMPRESSION = 617
-ISSUED_OPS_PER_COMPRESSION = 562.5
+ISSUED_OPS_PER_COMPRESSION = 558
 PEAK_LANE_OPS = 256 * 128 * CLOCK_HZ
 
 
