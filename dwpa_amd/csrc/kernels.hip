@@ -99,7 +99,11 @@ __global__ __launch_bounds__(256) void k_pbkdf2(const uint32_t* __restrict__ mid
 }
 
 // Lanes [live, count) of a padded launch (lone_pad below) repeat slot live-1's derivation and store nothing.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_ms(
+// DWPA_LONE_WPE: the occupancy bound of this lone-wave kernel (A/B builds may lift it).
+#ifndef DWPA_LONE_WPE
+#define DWPA_LONE_WPE __attribute__((amdgpu_waves_per_eu(8, 8)))
+#endif
+__global__ __launch_bounds__(256) DWPA_LONE_WPE void k_pbkdf2_ms(
     const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
     const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, uint32_t live) {
     const uint32_t blk = blockIdx.y;
