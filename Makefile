@@ -59,7 +59,7 @@ clean:
 
 tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
        tools/bin/inflate_check tools/bin/item_queue_check tools/bin/rules_fuzz_asan tools/bin/clock_idle \
-       tools/bin/inflate_check_tsan tools/bin/tail_placement tools/bin/parse_fuzz_asan
+       tools/bin/inflate_check_tsan tools/bin/tail_placement tools/bin/parse_fuzz_asan tools/bin/vgpr_bank
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -105,6 +105,10 @@ tools/bin/parse_fuzz_asan: tools/parse_fuzz.cpp $(SRC)/m22000_host.cpp $(SRC)/m2
 	    -o $@ tools/parse_fuzz.cpp $(SRC)/m22000_host.cpp
 
 tools/bin/clock_idle: tools/clock_idle.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
+
+tools/bin/vgpr_bank: tools/vgpr_bank.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -o $@ $<
 

@@ -6,8 +6,8 @@ EVERY instruction at the 4-cycle rate, even with 8 waves per SIMD; homogeneous s
 scalar `s_nop 0` in front of each 4-cycle op restores near-additive issue: the PBKDF2 loop goes from 3.9 to ~3.4
 SIMD-cycles per VALU instruction (+15.7 % PMK/s) with the instruction stream otherwise unchanged.  Source-level
 `asm volatile("s_nop 0")` cannot do this -- LLVM hoists the register-only VALU ops over it -- hence the pass on
-the compiler's assembly.  The product rule (the Makefile's ISSUE_RULE) is `sched=1:alt:orig,before_half` since round 5
-(`before_half` before it; profiles/r05/issue_rules_sched/).
+the compiler's assembly.  The product rule (the Makefile's ISSUE_RULE) is `sched=1:alt:orig:asmnop,before_half`
+since round 5 (`before_half` before it; profiles/r05/issue_rules_sched/, profiles/r05/sched_identities/).
 
 Rules (comma-separated, applied in the loop body only):
   after_half      s_nop after every 4-cycle VALU (alignbit, add3, xad, bfi, ...)
@@ -26,7 +26,9 @@ Rules (comma-separated, applied in the loop body only):
                   where the dependences allow; `alt` also prefers alternating 2-/4-cycle ops, `group` runs of one
                   rate (fewer 2 <-> 4-cycle transitions, for lone waves); ties go to the longest remaining critical
                   path, or with `orig` to the compiler's order; `asmnop` first drops the s_nop LLVM places after
-                  inline-asm blocks (the loop's v_bitop3 ops).  Applied before the nop rules (A/B)
+                  inline-asm blocks (the loop's v_bitop3 ops); `bank` then renames loop-local values so that fewer
+                  v_bitop3_b32 read sources from one VGPR bank (bank_rename; A/B only, profiles/r05/vgpr_bank/).
+                  Applied before the nop rules (A/B)
   none            copy through
 """
 import re
@@ -167,6 +169,120 @@ def reschedule(body, dmin, alt, group=False, orig=False):
     return [ins[i][0] for i in order + salu]
 
 
+def _bop3_conflicts(srcs):
+    """Source VGPR pairs of one v_bitop3_b32 that share a bank (v % 4)."""
+    vs = [int(s[1:]) for s in srcs if _vgpr(s)]
+    return sum(1 for a in range(len(vs)) for b in range(a + 1, len(vs)) if vs[a] % 4 == vs[b] % 4 and vs[a] != vs[b])
+
+
+def bank_rename(body, maxv):
+    """Rename loop-local VGPR values so that fewer v_bitop3_b32 read two sources from one bank.  Measured with
+    tools/vgpr_bank.hip (profiles/r05/vgpr_bank/): a v_bitop3_b32 whose three sources all sit in one bank (v % 4)
+    issues at the half rate; two in one bank cost nothing extra.  Cutting the pairs (99 -> 36 in the q kernel) also
+    cuts those triples (4 -> 1); the C2 kernel gained 0.08 %, so this stays an A/B option.  A value is local when the body
+    writes its register again later (so it dies inside the body); it moves to a register in [0, maxv] that no
+    instruction touches between the value's def and its last use and whose next access after that is a pure write.
+    Dependences between instructions only lose false (WAR/WAW) edges; the order is unchanged."""
+    if any("v[" in l for l in body):
+        raise ValueError("register tuples in the loop body")
+    ops = []  # per line: None, or [op, [operand tokens], text prefix]
+    for l in body:
+        m = re.match(r"(\s+)([vs]_\w+)(\s+)(.*)$", l)
+        if not m or _defs_uses(l) is None:
+            ops.append(None)
+            continue
+        parts = m.group(4).split(",")
+        ops.append([m.group(2), parts, m.group(1) + m.group(2) + m.group(3)])
+
+    def tok(p):
+        return p.strip().split()[0] if p.strip() else ""
+
+    def acc(k):  # (defs, uses) of VGPRs at line k
+        if ops[k] is None:
+            return set(), set()
+        op, parts, _ = ops[k]
+        ts = [tok(p) for p in parts]
+        if op.startswith("v_"):
+            return {ts[0]}, {t for t in ts[1:] if _vgpr(t)}
+        return set(), set()
+
+    def value_at(k, reg):
+        """(def line, use lines, next def line) of the value register reg gets at line k, or None if not local."""
+        uses = []
+        for j in range(k + 1, len(body)):
+            d, u = acc(j)
+            if reg in u:
+                uses.append(j)
+            if reg in d:
+                return k, uses, j
+        return None
+
+    def free(reg, a, b):
+        """reg holds nothing live over lines [a, b]: no access there, and its next access after b is a pure write."""
+        for j in range(a, len(body)):
+            d, u = acc(j)
+            if j <= b:
+                if reg in d or reg in u:
+                    return False
+            elif reg in u:
+                return False
+            elif reg in d:
+                return True
+        return False
+
+    def conflicts():
+        return sum(_bop3_conflicts([tok(p) for p in o[1][1:]]) for o in ops if o and o[0] == "v_bitop3_b32")
+
+    def rename(k, uses, old, new):
+        op, parts, pre = ops[k]
+        parts[0] = parts[0].replace(old, new, 1) if tok(parts[0]) == old else parts[0]
+        for j in uses:
+            p = ops[j][1]
+            for x in range(1, len(p)):
+                if tok(p[x]) == old:
+                    p[x] = p[x].replace(old, new, 1)
+
+    before = conflicts()
+    for k in range(len(body)):
+        o = ops[k]
+        if not o or o[0] != "v_bitop3_b32":
+            continue
+        srcs = [tok(p) for p in o[1][1:]]
+        if not _bop3_conflicts(srcs):
+            continue
+        # try to move one source value of a conflicting pair to a bank none of the other sources use
+        done = False
+        for s in srcs:
+            if done or not _vgpr(s):
+                continue
+            dl = max((j for j in range(k) if s in acc(j)[0]), default=None)
+            if dl is None:
+                continue
+            v = value_at(dl, s)
+            if v is None:
+                continue
+            _, uses, _ = v
+            last = max(uses)
+            others = {int(t[1:]) % 4 for t in srcs if _vgpr(t) and t != s}
+            for r in range(maxv + 1):
+                nr = f"v{r}"
+                if r % 4 in others or nr == s or not free(nr, dl, last):
+                    continue
+                # the move must not add conflicts at the value's other bitop3 readers
+                old_c = sum(_bop3_conflicts([tok(p) for p in ops[j][1][1:]]) for j in uses if ops[j][0] == "v_bitop3_b32")
+                saved = [(j, list(ops[j][1])) for j in [dl] + uses]
+                rename(dl, uses, s, nr)
+                new_c = sum(_bop3_conflicts([tok(p) for p in ops[j][1][1:]]) for j in uses if ops[j][0] == "v_bitop3_b32")
+                if new_c < old_c:
+                    done = True
+                    break
+                for j, p in saved:
+                    ops[j][1] = p
+    out = [l if ops[k] is None else ops[k][2] + ",".join(ops[k][1]) for k, l in enumerate(body)]
+    sys.stderr.write(f"issue_pass: bank: v_bitop3_b32 same-bank source pairs {before} -> {conflicts()}\n")
+    return out
+
+
 def nopify(lines, kernel, rules):
     h, e, nv = main_loop_range(lines, kernel)
     for r in rules:
@@ -183,6 +299,11 @@ def nopify(lines, kernel, rules):
             except ValueError as err:  # e.g. a hazard s_nop of another compiler: keep its order, spacers still apply
                 sys.stderr.write(f"issue_pass: {kernel}: {r} skipped ({err})\n")
                 continue
+            if "bank" in arg[1:]:
+                start = next(i for i, l in enumerate(lines) if l.startswith(kernel + ":"))
+                end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+                maxv = max(int(x) for l in lines[start:end] for x in re.findall(r"\bv(\d+)\b", l))
+                body = bank_rename(body, maxv)
             lines = lines[:h + 1] + body + lines[e:]
             e = h + 1 + len(body)
     if "split_add3" in rules:
