@@ -7,7 +7,7 @@ OBJ := build/obj
 LIB := dwpa_amd/lib/libdwpa22000.so
 HDRS := $(wildcard $(SRC)/*.hpp) include/dwpa22000.h
 OBJS := $(OBJ)/kernels.o $(OBJ)/rules_dev.o $(OBJ)/engine.o $(OBJ)/m22000_host.o $(OBJ)/crack.o $(OBJ)/rules.o \
-        $(OBJ)/pbkdf2_module.o $(OBJ)/pbkdf2_hsaco.o
+        $(OBJ)/pbkdf2_module.o $(OBJ)/pbkdf2_hsaco.o $(OBJ)/host_crypto.o $(OBJ)/host_check.o
 LLVM := /opt/rocm/lib/llvm/bin
 ISSUE_RULE ?= sched=1:alt:orig:asmnop,before_half
 

@@ -11,9 +11,9 @@ this package is its Python host side:
 """
 from ._lib import DwpaError, load  # noqa: F401
 from .m22000 import (BatchJobs, check_batch, check_key_m22000, crack_files, device_count, group_by_essid,  # noqa: F401
-                     check_stats, hash_m22000, hc_unhex, parse_m22000, pbkdf2_pmk, rules_count, rules_count_ex,
+                     check_stats, hash_m22000, hc_unhex, init, parse_m22000, pbkdf2_pmk, rules_count, rules_count_ex,
                      rules_expand, Scan)
 
 __all__ = ["DwpaError", "load", "BatchJobs", "check_key_m22000", "check_batch", "pbkdf2_pmk", "hc_unhex", "hash_m22000",
            "crack_files", "rules_count", "rules_count_ex", "check_stats", "rules_expand", "device_count", "Scan",
-           "parse_m22000", "group_by_essid"]
+           "parse_m22000", "group_by_essid", "init"]

@@ -1,7 +1,9 @@
 """ctypes binding of libdwpa22000.so (include/dwpa22000.h).
 
-There is no CPU fallback: importing works anywhere (so the CPU test suite can check exports), but every compute
-entry point returns DWPA_E_NODEV without a gfx950 device and the wrappers raise ``DwpaError`` -- loudly.
+Importing works anywhere.  The check path and PBKDF2 run on the gfx950 device, or on the library's own host backend
+for small calls and -- only when asked for (dwpa_config.allow_cpu_fallback, DWPA_CPU_FALLBACK=1) -- without a device;
+otherwise a call without a device returns DWPA_E_NODEV and the wrappers raise ``DwpaError``, loudly.  The client
+path (crack_files, scans, rule expansion) is device-only.
 """
 from __future__ import annotations
 
@@ -17,9 +19,10 @@ DWPA_E_FORMAT, DWPA_E_HEX, DWPA_E_TYPE, DWPA_E_KEYVER = -1, -2, -3, -4
 DWPA_E_NODEV, DWPA_E_HIP, DWPA_E_ARG, DWPA_E_NOMEM, DWPA_E_IO, DWPA_E_OVERFLOW, DWPA_E_RULE = -10, -11, -12, -13, -14, -15, -16
 DWPA_RC_CRACKED, DWPA_RC_EXHAUSTED, DWPA_RC_ERROR = 0, 1, -1
 DWPA_NC_PHP, DWPA_NC_HASHCAT = 0, 1
-DWPA_NC_MAX = 65536  # the largest nc / nonce_error_corrections taken (include/dwpa22000.h)
+DWPA_NC_MAX = 65664  # the largest nc / nonce_error_corrections taken (include/dwpa22000.h)
 DWPA_DICT_OK, DWPA_DICT_DAMAGED = 0, 1  # dwpa_crack_files_ex per-dictionary status (or DWPA_E_IO)
 DWPA_RULES_DEFAULT, DWPA_RULES_HASHCAT, DWPA_RULES_FULL = 0, 1, 2  # dwpa_config.rule_mode
+DWPA_BACKEND_DEVICE, DWPA_BACKEND_HOST_SMALL, DWPA_BACKEND_HOST_FALLBACK = 0, 1, 2  # dwpa_check_stats.backend
 
 
 class DwpaError(RuntimeError):
@@ -44,7 +47,8 @@ class Job(ctypes.Structure):
 
 class Config(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("device_mask", ctypes.c_uint32), ("batch", ctypes.c_uint32),
-                ("nc_mode", ctypes.c_int32), ("rule_mode", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("nc_mode", ctypes.c_int32), ("rule_mode", ctypes.c_int32), ("allow_cpu_fallback", ctypes.c_int32),
+                ("host_max_pmks", ctypes.c_int32), ("reserved", ctypes.c_int32 * 1)]
 
 
 class CrackStats(ctypes.Structure):
@@ -56,7 +60,7 @@ class CrackStats(ctypes.Structure):
 class CheckStats(ctypes.Structure):
     _fields_ = [("jobs", ctypes.c_uint32), ("slots", ctypes.c_uint32), ("pmks", ctypes.c_uint32),
                 ("tail_pmks", ctypes.c_uint32), ("tail_waves", ctypes.c_uint32), ("tail_waves_raised", ctypes.c_uint32),
-                ("hits", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("seconds", ctypes.c_double)]
+                ("hits", ctypes.c_uint32), ("backend", ctypes.c_uint32), ("seconds", ctypes.c_double)]
 
 
 class Resources(ctypes.Structure):

@@ -237,6 +237,14 @@ static int g_ndev = 0;
 static uint32_t g_mask = 0;
 static uint32_t g_batch = 0;
 static int g_rule_mode = DWPA_RULES_DEFAULT;  // dwpa_init's cfg->rule_mode
+static int g_cpu_fallback = 0;                // dwpa_init's cfg->allow_cpu_fallback (0: DWPA_CPU_FALLBACK)
+static int g_host_max = 0;                    // dwpa_init's cfg->host_max_pmks (0: DWPA_HOST_MAX_PMKS, else default)
+static bool g_nodev = false;                  // hipGetDeviceCount found no device (not asked again)
+// A device call has completed in this process.  Until then the small-call threshold is COLD_FACTOR times larger:
+// the first device call also starts the HIP runtime, loads the code objects and creates the call context (0.2-0.7 s
+// in a fresh PHP-FPM worker, profiles/r05/c1cold/), which a few hundred host PBKDF2s undercut.
+static std::atomic<bool> g_device_warm{false};
+constexpr double COLD_FACTOR = 8.0;
 static std::vector<std::unique_ptr<Device>> g_dev;  // call contexts: [device * calls_per_device() + k]
 
 // Head fence of one physical device: concurrent calls launch their PBKDF2 heads one after another (each head
@@ -270,10 +278,16 @@ static int init_locked(const dwpa_config* cfg) {
         g_mask = cfg->device_mask;
         g_batch = cfg->batch;
         if (DWPA_CFG_HAS(cfg, rule_mode)) g_rule_mode = cfg->rule_mode;
+        if (DWPA_CFG_HAS(cfg, allow_cpu_fallback)) g_cpu_fallback = cfg->allow_cpu_fallback;
+        if (DWPA_CFG_HAS(cfg, host_max_pmks)) g_host_max = cfg->host_max_pmks;
     }
     if (g_init) return 0;
+    if (g_nodev) return DWPA_E_NODEV;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DWPA_E_NODEV;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        g_nodev = true;
+        return DWPA_E_NODEV;
+    }
     g_ndev = n;
     g_dev.clear();
     g_fence.clear();
@@ -291,6 +305,37 @@ static int init_locked(const dwpa_config* cfg) {
 static int ensure_init() {
     std::lock_guard<std::mutex> lk(g_mu);
     return init_locked(nullptr);
+}
+
+// Host backend switches (host_check.cpp).  allow_cpu_fallback: dwpa_init's value when set (1 on, -1 off), else
+// DWPA_CPU_FALLBACK=1 from the environment; off by default, so a box without a device says DWPA_E_NODEV unless the
+// caller asked for the host backend.  host_max_pmks: calls of at most this many PMK-equivalents with at least one
+// PBKDF2 derive run on the host (dwpa_init's value, else DWPA_HOST_MAX_PMKS, else 24; <= 0 from either = never).
+static bool cpu_fallback_on() {
+    int v;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        v = g_cpu_fallback;
+    }
+    if (v) return v > 0;
+    const char* e = getenv("DWPA_CPU_FALLBACK");
+    return e && *e == '1';
+}
+static double host_max_pmks() {
+    int v;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        v = g_host_max;
+    }
+    if (v) return v < 0 ? 0.0 : (double)v;
+    const char* e = getenv("DWPA_HOST_MAX_PMKS");
+    if (e && *e) return std::max(0.0, atof(e));
+    return 24.0;
+}
+// Device-side failures a call may retry on the host backend (allow_cpu_fallback): no device, a HIP error, a device or
+// pinned allocation that failed, a hit buffer that overflowed.
+static bool host_retry_code(int rc) {
+    return rc == DWPA_E_NODEV || rc == DWPA_E_HIP || rc == DWPA_E_NOMEM || rc == DWPA_E_OVERFLOW;
 }
 
 // Devices selected by `mask` (0 = the dwpa_init() mask; that one 0 = every visible device).
@@ -517,6 +562,9 @@ static void parallel_for(size_t T, const F& fn) {
     }
     HostPool::get().run(T, fn);
 }
+
+size_t host_threads_for(size_t n, size_t min_per_thread) { return host_threads(n, min_per_thread); }
+void host_parallel(size_t T, const std::function<void(size_t)>& fn) { parallel_for(T, fn); }
 
 // A typed view of pinned staging memory.
 template <typename T>
@@ -964,10 +1012,20 @@ static thread_local bool g_have_check_stats = false;
 static int check_batch_body(Device& d, const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs,
                             DrainOnExit& drain);
 
-static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs) {
-    const auto t0 = std::chrono::steady_clock::now();
-    g_check_stats = dwpa_check_stats{};
-    g_have_check_stats = true;
+// The host backend answers the whole call (backend DWPA_BACKEND_HOST_SMALL or _HOST_FALLBACK).
+static int check_batch_host(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs, uint32_t backend,
+                            std::chrono::steady_clock::time_point t0) {
+    dwpa_check_stats st{};
+    st.jobs = (uint32_t)std::min<size_t>(njobs, UINT32_MAX);
+    st.backend = backend;
+    const int rc = host_check_batch(jobs, njobs, out, rcs, st);
+    g_check_stats = st;
+    g_check_stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+static int check_batch_device(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs,
+                              std::chrono::steady_clock::time_point t0) {
     RCHK(ensure_init());
     Device* dp = pick_device();
     if (!dp) return DWPA_E_NODEV;
@@ -976,9 +1034,28 @@ static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out
     Device& d = *dp;
     d.stats = dwpa_check_stats{};
     d.stats.jobs = (uint32_t)std::min<size_t>(njobs, UINT32_MAX);
+    d.stats.backend = DWPA_BACKEND_DEVICE;
     const int rc = check_batch_body(d, jobs, njobs, out, rcs, drain);
+    if (rc >= 0) g_device_warm.store(true, std::memory_order_relaxed);
     g_check_stats = d.stats;
     g_check_stats.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return rc;
+}
+
+// Routing: a small call (at least one PBKDF2 derive, at most host_max_pmks PMK-equivalents) runs on the host without
+// touching the device; every other call on the device, and on the host after a device-side failure when
+// allow_cpu_fallback is on.
+static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs) {
+    const auto t0 = std::chrono::steady_clock::now();
+    g_check_stats = dwpa_check_stats{};
+    g_have_check_stats = true;
+    const HostCost hc = host_cost(jobs, njobs);
+    const double thr = host_max_pmks() * (g_device_warm.load(std::memory_order_relaxed) ? 1.0 : COLD_FACTOR);
+    if (hc.derives && hc.pmk_equiv <= thr)
+        return check_batch_host(jobs, njobs, out, rcs, DWPA_BACKEND_HOST_SMALL, t0);
+    const int rc = check_batch_device(jobs, njobs, out, rcs, t0);
+    if (host_retry_code(rc) && cpu_fallback_on())
+        return check_batch_host(jobs, njobs, out, rcs, DWPA_BACKEND_HOST_FALLBACK, t0);
     return rc;
 }
 
@@ -1197,7 +1274,20 @@ static int check_batch_body(Device& d, const dwpa_job* jobs, size_t njobs, dwpa_
     return 0;
 }
 
+static int pbkdf2_device(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out);
+
+// dwpa_pbkdf2_pmk: the check path's routing (a small derive on the host, the device otherwise, the host again after a
+// device-side failure when allow_cpu_fallback is on).
 static int pbkdf2_impl(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out) {
+    const double thr = host_max_pmks() * (g_device_warm.load(std::memory_order_relaxed) ? 1.0 : COLD_FACTOR);
+    if ((double)nkeys <= thr) return host_pbkdf2(keys, nkeys, essid, essid_len, out);
+    const int rc = pbkdf2_device(keys, nkeys, essid, essid_len, out);
+    if (rc >= 0) g_device_warm.store(true, std::memory_order_relaxed);
+    if (host_retry_code(rc) && cpu_fallback_on()) return host_pbkdf2(keys, nkeys, essid, essid_len, out);
+    return rc;
+}
+
+static int pbkdf2_device(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out) {
     RCHK(ensure_init());
     Device* dp = pick_device();
     if (!dp) return DWPA_E_NODEV;
@@ -1566,8 +1656,15 @@ int dwpa_init(const dwpa_config* cfg) {
         if (cfg && cfg->struct_size && cfg->struct_size < sizeof(uint32_t) * 3) return DWPA_E_ARG;
         if (DWPA_CFG_HAS(cfg, rule_mode) && (cfg->rule_mode < DWPA_RULES_DEFAULT || cfg->rule_mode > DWPA_RULES_FULL))
             return DWPA_E_ARG;
-        std::lock_guard<std::mutex> lk(g_mu);
-        return init_locked(cfg);
+        if (DWPA_CFG_HAS(cfg, allow_cpu_fallback) && (cfg->allow_cpu_fallback < -1 || cfg->allow_cpu_fallback > 1))
+            return DWPA_E_ARG;
+        int rc;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            rc = init_locked(cfg);
+        }
+        // no device: the library still answers check and PBKDF2 calls when the host backend may take them
+        return rc == DWPA_E_NODEV && cpu_fallback_on() ? 0 : rc;
     });
 }
 

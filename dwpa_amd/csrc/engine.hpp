@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <new>
 #include <stdexcept>
 #include <vector>
@@ -50,6 +51,22 @@ inline int guarded(F&& body, int nomem = DWPA_E_NOMEM, int other = DWPA_E_ARG) n
         return other;
     }
 }
+
+// The check path's host worker pool (engine.cpp HostPool): threads for n items of at least min_per_thread each (at
+// most DWPA_HOST_THREADS), and fn(0..T-1) with part 0 on the calling thread.
+size_t host_threads_for(size_t n, size_t min_per_thread);
+void host_parallel(size_t T, const std::function<void(size_t)>& fn);
+
+// Host (CPU) backend, host_check.cpp.  host_cost: the work of a check call in PMK-equivalents (PBKDF2 derives plus
+// the nonce-correction attempts' verify compressions / 16,388), estimated from the jobs without parsing them.
+struct HostCost {
+    uint64_t keys = 0;      // non-null keys
+    uint64_t derives = 0;   // keys whose PMK is derived (not the caller's $pmk)
+    double pmk_equiv = 0;   // derives + verify work
+};
+HostCost host_cost(const dwpa_job* jobs, size_t njobs);
+int host_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs, dwpa_check_stats& stats);
+int host_pbkdf2(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out);
 
 int engine_init();
 // Rule-file loader mode of the process: dwpa_init's cfg->rule_mode when given, else DWPA_RULE_MODE=full|hashcat

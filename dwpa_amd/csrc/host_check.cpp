@@ -1,0 +1,429 @@
+// host_check.cpp -- the host (CPU) backend behind the same C ABI ("the server may have no GPU, so the
+// CPU backend is mandatory behind the same ABI").
+//
+// It answers dwpa_check_m22000 / dwpa_check_batch / dwpa_pbkdf2_pmk on the host's cores, with the library's own
+// primitives (host_crypto.cpp: SHA-NI / AES-NI or scalar) -- never the oracle, never OpenSSL.  engine.cpp routes a
+// call here in two cases:
+//   * small calls: a call whose work is at most dwpa_config.host_max_pmks PMK-equivalents (put_work's one key per
+//     check_key_m22000 call, common.php:902) -- one PBKDF2 chain on a lone GPU wave takes ~8 ms, on a SHA-NI core
+//     well under one;
+//   * no usable gfx950 device, or a device call that failed, when dwpa_config.allow_cpu_fallback (or
+//     DWPA_CPU_FALLBACK=1) is set.
+// Every call reports which backend answered it (dwpa_check_stats.backend).
+//
+// The semantics are the device path's, built from the same host pieces: parse_m22000 (PHP acceptance rules), the
+// TableBuilder's attempt lists (common.php:237-300 nonce-correction order, PHP's $n mutation across attempts and
+// keys) in raw-block form, first key in input order then first attempt in PHP order (common.php:186,280-289), and the
+// caller's $pmk for the first non-null key only (:178,188,246,302).
+#include <string.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "dwpa22000.h"
+#include "engine.hpp"
+#include "host_crypto.hpp"
+#include "m22000_host.hpp"
+
+namespace dwpa {
+
+using namespace hostc;
+
+namespace {
+
+constexpr uint32_t NO_UID = 0xffffffffu;  // slot whose PMK is the caller's
+
+// HMAC midstates of a 32-byte PMK (key block = PMK || 0^32) for SHA-1 and SHA-256
+void pmk_mid_sha1(const uint32_t pmk[8], uint32_t ip[5], uint32_t op[5]) {
+    uint32_t wi[16], wo[16];
+    for (int t = 0; t < 16; t++) {
+        const uint32_t v = t < 8 ? pmk[t] : 0;
+        wi[t] = v ^ 0x36363636u;
+        wo[t] = v ^ 0x5c5c5c5cu;
+    }
+    memcpy(ip, SHA1_IV, 20);
+    memcpy(op, SHA1_IV, 20);
+    sha1_compress(ip, wi);
+    sha1_compress(op, wo);
+}
+void pmk_mid_sha256(const uint32_t pmk[8], uint32_t ip[8], uint32_t op[8]) {
+    uint32_t wi[16], wo[16];
+    for (int t = 0; t < 16; t++) {
+        const uint32_t v = t < 8 ? pmk[t] : 0;
+        wi[t] = v ^ 0x36363636u;
+        wo[t] = v ^ 0x5c5c5c5cu;
+    }
+    memcpy(ip, SHA256_IV, 32);
+    memcpy(op, SHA256_IV, 32);
+    sha256_compress(ip, wi);
+    sha256_compress(op, wo);
+}
+
+inline uint32_t bswap(uint32_t v) { return __builtin_bswap32(v); }
+
+// Block b of attempt `at`'s PRF blocks after the line's shared prefix, its two correction words patched in when the
+// line shares one stream between all attempts (tables.hpp LineDev.patch_w0/_w1).
+inline void att_block(const LineDev& L, const AttDev& at, const uint32_t* pool, uint32_t b, uint32_t w[16]) {
+    memcpy(w, pool + at.blk_off + 16 * (size_t)b, 64);
+    if (L.patch_w0 != NO_PATCH) {
+        const uint32_t lo = 16 * b;
+        if (L.patch_w0 >= lo && L.patch_w0 < lo + 16) w[L.patch_w0 - lo] = at.v0;
+        if (L.patch_w1 >= lo && L.patch_w1 < lo + 16) w[L.patch_w1 - lo] = at.v1;
+    }
+}
+
+// HMAC-SHA1 / HMAC-MD5 keyed with the 16-byte KCK (PTK words 0..3) over the EAPOL frame: the keyver 2 / 1 MIC
+// (common.php:264,268).  mic[4]: SHA-1 words (big-endian) or MD5 words (little-endian), as LineDev.target.
+void mic_sha1(const uint32_t kck[4], const uint32_t* blocks, uint32_t nblk, uint32_t mic[5]) {
+    uint32_t ki[16], ko[16], st[5], w[16];
+    for (int t = 0; t < 16; t++) {
+        const uint32_t v = t < 4 ? kck[t] : 0;
+        ki[t] = v ^ 0x36363636u;
+        ko[t] = v ^ 0x5c5c5c5cu;
+    }
+    memcpy(st, SHA1_IV, 20);
+    sha1_compress(st, ki);
+    for (uint32_t b = 0; b < nblk; b++) sha1_compress(st, blocks + 16 * (size_t)b);
+    memcpy(w, st, 20);
+    w[5] = 0x80000000u;
+    for (int t = 6; t < 15; t++) w[t] = 0;
+    w[15] = (64 + 20) * 8;
+    memcpy(mic, SHA1_IV, 20);
+    sha1_compress(mic, ko);
+    sha1_compress(mic, w);
+}
+void mic_md5(const uint32_t kck_be[4], const uint32_t* blocks, uint32_t nblk, uint32_t mic[4]) {
+    uint32_t ki[16], ko[16], st[4], w[16];
+    for (int t = 0; t < 16; t++) {
+        const uint32_t v = t < 4 ? bswap(kck_be[t]) : 0;  // the KCK's bytes as little-endian words
+        ki[t] = v ^ 0x36363636u;
+        ko[t] = v ^ 0x5c5c5c5cu;
+    }
+    memcpy(st, MD5_IV, 16);
+    md5_compress(st, ki);
+    for (uint32_t b = 0; b < nblk; b++) md5_compress(st, blocks + 16 * (size_t)b);
+    memcpy(w, st, 16);
+    w[4] = 0x80u;
+    for (int t = 5; t < 16; t++) w[t] = 0;
+    w[14] = (64 + 16) * 8;
+    memcpy(mic, MD5_IV, 16);
+    md5_compress(mic, ko);
+    md5_compress(mic, w);
+}
+
+// The first attempt of the line's list for key ordinal `ord` under which `pmk` verifies, or -1 (PMKID lines: 0 / -1).
+int64_t verify_pmk(const TableBuilder& tb, uint32_t li, uint32_t ord, const uint32_t pmk[8]) {
+    const LineDev& L = tb.lines[li];
+    if (tb.never[li]) return -1;
+    const uint32_t* pool = tb.pool.data();
+    if (L.kind == LINE_PMKID) {  // HMAC-SHA1(PMK, "PMK Name" || AP || STA)[0:16] (common.php:183-185)
+        uint32_t ip[5], op[5], w[16];
+        pmk_mid_sha1(pmk, ip, op);
+        for (uint32_t b = 0; b < L.msg_nblk; b++) sha1_compress(ip, pool + L.msg_off + 16 * (size_t)b);
+        memcpy(w, ip, 20);
+        w[5] = 0x80000000u;
+        for (int t = 6; t < 15; t++) w[t] = 0;
+        w[15] = (64 + 20) * 8;
+        sha1_compress(op, w);
+        return memcmp(op, L.target, 16) == 0 ? 0 : -1;
+    }
+    const uint32_t list = std::min(ord, L.nlists - 1);
+    const AttDev* at = tb.atts.data() + L.list_off + (size_t)list * L.natt;
+    uint32_t w[16];
+    if (L.keyver != 3) {
+        // PTK = HMAC-SHA1(PMK, "Pairwise key expansion\0" || m || n || "\0") (common.php:263,267)
+        uint32_t ip[5], op[5], pre[5];
+        pmk_mid_sha1(pmk, ip, op);
+        memcpy(pre, ip, 20);
+        for (uint32_t b = 0; b < L.pre_nblk; b++) sha1_compress(pre, pool + L.pre_off + 16 * (size_t)b);
+        for (uint32_t a = 0; a < L.natt; a++) {
+            uint32_t st[5], ptk[5], mic[5];
+            memcpy(st, pre, 20);
+            for (uint32_t b = 0; b < at[a].nblk; b++) {
+                att_block(L, at[a], pool, b, w);
+                sha1_compress(st, w);
+            }
+            memcpy(w, st, 20);
+            w[5] = 0x80000000u;
+            for (int t = 6; t < 15; t++) w[t] = 0;
+            w[15] = (64 + 20) * 8;
+            memcpy(ptk, op, 20);
+            sha1_compress(ptk, w);
+            if (L.keyver == 2) mic_sha1(ptk, pool + L.mic_off, L.mic_nblk, mic);
+            else mic_md5(ptk, pool + L.mic_off, L.mic_nblk, mic);
+            if (memcmp(mic, L.target, 16) == 0) return a;
+        }
+        return -1;
+    }
+    // keyver 3: PTK = HMAC-SHA256(PMK, "\1\0Pairwise key expansion" || m || n || "\x80\1"), MIC = AES-128-CMAC(KCK,
+    // EAPOL) (common.php:271-272)
+    uint32_t ip[8], op[8], pre[8];
+    pmk_mid_sha256(pmk, ip, op);
+    memcpy(pre, ip, 32);
+    for (uint32_t b = 0; b < L.pre_nblk; b++) sha256_compress(pre, pool + L.pre_off + 16 * (size_t)b);
+    std::vector<uint8_t> cm(16 * (size_t)L.mic_nblk);
+    for (size_t i = 0; i < 4 * (size_t)L.mic_nblk; i++) {
+        const uint32_t v = pool[L.mic_off + i];
+        cm[4 * i] = (uint8_t)(v >> 24);
+        cm[4 * i + 1] = (uint8_t)(v >> 16);
+        cm[4 * i + 2] = (uint8_t)(v >> 8);
+        cm[4 * i + 3] = (uint8_t)v;
+    }
+    uint8_t target[16];
+    for (int k = 0; k < 4; k++) {
+        target[4 * k] = (uint8_t)(L.target[k] >> 24);
+        target[4 * k + 1] = (uint8_t)(L.target[k] >> 16);
+        target[4 * k + 2] = (uint8_t)(L.target[k] >> 8);
+        target[4 * k + 3] = (uint8_t)L.target[k];
+    }
+    for (uint32_t a = 0; a < L.natt; a++) {
+        uint32_t st[8], ptk[8];
+        memcpy(st, pre, 32);
+        for (uint32_t b = 0; b < at[a].nblk; b++) {
+            att_block(L, at[a], pool, b, w);
+            sha256_compress(st, w);
+        }
+        memcpy(w, st, 32);
+        w[8] = 0x80000000u;
+        for (int t = 9; t < 15; t++) w[t] = 0;
+        w[15] = (64 + 32) * 8;
+        memcpy(ptk, op, 32);
+        sha256_compress(ptk, w);
+        uint8_t kck[16], mac[16];
+        for (int k = 0; k < 4; k++) {
+            kck[4 * k] = (uint8_t)(ptk[k] >> 24);
+            kck[4 * k + 1] = (uint8_t)(ptk[k] >> 16);
+            kck[4 * k + 2] = (uint8_t)(ptk[k] >> 8);
+            kck[4 * k + 3] = (uint8_t)ptk[k];
+        }
+        aes128_cmac(kck, cm.data(), L.mic_nblk, L.cmac_complete != 0, mac);
+        if (memcmp(mac, target, 16) == 0) return a;
+    }
+    return -1;
+}
+
+// One unique (ESSID, key) PMK to derive: its key bytes and its ESSID group's salt blocks.
+struct Derive {
+    const uint8_t* key;
+    size_t len;
+    uint32_t group;
+};
+
+// PBKDF2 of every entry of `dv` into pmk[i] (big-endian words), over up to host_threads() threads: chunks of
+// PBKDF2_CHAINS / 2 keys handed out through an atomic counter, so uneven keys (a 64 KiB one) do not stall a part.
+void derive_all(const std::vector<Derive>& dv, const std::vector<std::vector<uint32_t>>& salt,
+                const std::vector<uint32_t>& nblk, std::vector<std::array<uint32_t, 8>>& pmk) {
+    const size_t per = PBKDF2_CHAINS / 2, nchunks = (dv.size() + per - 1) / per;
+    pmk.resize(dv.size());
+    std::atomic<size_t> next{0};
+    host_parallel(host_threads_for(nchunks, 1), [&](size_t) {
+        uint32_t mid[PBKDF2_CHAINS / 2][10];
+        const uint32_t* sp[PBKDF2_CHAINS / 2];
+        uint32_t nb[PBKDF2_CHAINS / 2];
+        for (size_t c; (c = next.fetch_add(1, std::memory_order_relaxed)) < nchunks;) {
+            const size_t i0 = c * per, n = std::min(per, dv.size() - i0);
+            for (size_t k = 0; k < n; k++) {
+                const Derive& d = dv[i0 + k];
+                hmac_sha1_mid(d.key, d.len, mid[k], mid[k] + 5);
+                sp[k] = salt[d.group].data();
+                nb[k] = nblk[d.group];
+            }
+            pbkdf2_sha1(n, mid, sp, nb, (uint32_t(*)[8])pmk[i0].data());
+        }
+    });
+}
+
+void pmk_bytes_out(const uint32_t w[8], uint8_t out[32]) {
+    for (int k = 0; k < 8; k++) {
+        out[4 * k] = (uint8_t)(w[k] >> 24);
+        out[4 * k + 1] = (uint8_t)(w[k] >> 16);
+        out[4 * k + 2] = (uint8_t)(w[k] >> 8);
+        out[4 * k + 3] = (uint8_t)w[k];
+    }
+}
+
+}  // namespace
+
+HostCost host_cost(const dwpa_job* jobs, size_t njobs) {
+    HostCost c;
+    for (size_t j = 0; j < njobs; j++) {
+        const dwpa_job& J = jobs[j];
+        // the type field decides the verify work; a malformed line costs nothing (it fails the parse)
+        const bool eapol = J.line && J.line_len > 6 && memcmp(J.line, "WPA*02*", 7) == 0;
+        const int64_t nc = std::min<int64_t>(J.nc, DWPA_NC_MAX);
+        const double att = eapol ? (double)(1 + 4 * std::max<int64_t>(0, (nc >> 1) + 1)) : 1.0;
+        const double verify = eapol ? att * 9.0 : 4.0;  // compressions per key (PRF + MIC per attempt; PMKID)
+        uint64_t nn = 0;
+        for (size_t k = 0; k < J.nkeys; k++)
+            if (J.keys[k].ptr) nn++;
+        c.keys += nn;
+        c.derives += nn - (nn && J.pmk ? 1 : 0);
+        c.pmk_equiv += (double)nn * verify / 16388.0;
+    }
+    c.pmk_equiv += (double)c.derives;
+    return c;
+}
+
+int host_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs, dwpa_check_stats& stats) {
+    std::vector<ParsedLine> parsed(njobs);
+    std::vector<uint32_t> nnz(njobs, 0);
+    // parse (PHP acceptance rules) and count the non-null keys of every line that can match; the same per-job
+    // validation as the device path (engine.cpp check_batch_body)
+    const size_t TP = host_threads_for(njobs, 64);
+    host_parallel(TP, [&](size_t t) {
+        const size_t T = TP;
+        for (size_t j = njobs * t / T; j < njobs * (t + 1) / T; j++) {
+            out[j].key_index = -1;
+            out[j].nc = 0;
+            out[j].endian = 0;
+            out[j].nc_valid = 0;
+            memset(out[j].pmk, 0, 32);
+            ParsedLine& pl = parsed[j];
+            parse_m22000_into(jobs[j].line, jobs[j].line_len, pl);
+            rcs[j] = pl.status;
+            if (pl.status) continue;
+            rcs[j] = DWPA_MISS;
+            if (!line_can_match(pl)) continue;
+            if ((pl.kind == LINE_EAPOL && jobs[j].nc > DWPA_NC_MAX) || jobs[j].nkeys > UINT32_MAX) {
+                rcs[j] = DWPA_E_ARG;
+                continue;
+            }
+            uint32_t c = 0;
+            for (size_t k = 0; k < jobs[j].nkeys; k++)
+                if (jobs[j].keys[k].ptr) c++;
+            nnz[j] = c;
+        }
+    });
+
+    // ESSID groups (first-seen order) with their salt blocks; the line tables (raw blocks, PHP nonce order)
+    std::unordered_map<std::string_view, uint32_t> essid_id;
+    std::vector<uint32_t> gid(njobs, 0), job_line(njobs, 0), jslot(njobs, 0);
+    std::vector<std::vector<uint32_t>> salt;
+    std::vector<uint32_t> nblk;
+    TableBuilder tb;
+    tb.raw = true;
+    size_t nslots = 0;
+    for (size_t j = 0; j < njobs; j++) {
+        if (!nnz[j]) continue;
+        auto ins = essid_id.try_emplace(std::string_view(parsed[j].essid), (uint32_t)salt.size());
+        if (ins.second) {
+            salt.emplace_back();
+            nblk.push_back(build_salt_blocks(parsed[j].essid, salt.back()));
+        }
+        gid[j] = ins.first->second;
+        job_line[j] = tb.add_line(parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
+        jslot[j] = (uint32_t)nslots;
+        nslots += nnz[j];
+    }
+    stats.slots = (uint32_t)std::min<size_t>(nslots, UINT32_MAX);
+    if (!nslots) return 0;
+
+    // slots: the job's non-null keys in order ($HEX[] decoded); unique (ESSID, key) pairs derived once
+    std::vector<uint32_t> sjob(nslots), sord(nslots), skidx(nslots), suid(nslots);
+    std::vector<std::string> dec;  // decoded $HEX[] keys (stable storage for the views below)
+    size_t ndec = 0;
+    for (size_t j = 0; j < njobs; j++)
+        if (nnz[j])
+            for (size_t k = 0; k < jobs[j].nkeys; k++)
+                if (jobs[j].keys[k].ptr && starts_hex(jobs[j].keys[k].ptr, jobs[j].keys[k].len)) ndec++;
+    dec.reserve(ndec);
+    std::vector<std::unordered_map<std::string_view, uint32_t>> uniq(salt.size());
+    std::vector<Derive> dv;
+    for (size_t j = 0; j < njobs; j++) {
+        if (!nnz[j]) continue;
+        size_t s = jslot[j];
+        uint32_t o = 0;
+        for (size_t k = 0; k < jobs[j].nkeys; k++) {
+            const dwpa_bytes& kb = jobs[j].keys[k];
+            if (!kb.ptr) continue;  // is_null($key): skipped (common.php:172,240)
+            sjob[s] = (uint32_t)j;
+            sord[s] = o;
+            skidx[s] = (uint32_t)k;
+            if (o == 0 && jobs[j].pmk) {
+                suid[s] = NO_UID;  // the caller's $pmk (common.php:178,246)
+            } else {
+                std::string_view key((const char*)kb.ptr, kb.len);
+                if (starts_hex(kb.ptr, kb.len)) {
+                    dec.push_back(hc_unhex(std::string(key)));
+                    key = dec.back();
+                }
+                auto ins = uniq[gid[j]].try_emplace(key, (uint32_t)dv.size());
+                if (ins.second) dv.push_back(Derive{(const uint8_t*)key.data(), key.size(), gid[j]});
+                suid[s] = ins.first->second;
+            }
+            s++;
+            o++;
+        }
+    }
+    stats.pmks = (uint32_t)dv.size();
+    std::vector<std::array<uint32_t, 8>> pmk;
+    derive_all(dv, salt, nblk, pmk);
+
+    // verify every slot; a job's slots beyond its first hit (in key order) are skipped once the hit is known
+    std::vector<std::atomic<uint32_t>> best(njobs);
+    for (auto& b : best) b.store(UINT32_MAX, std::memory_order_relaxed);
+    std::vector<int32_t> satt(nslots, -1);
+    std::vector<std::array<uint32_t, 8>> caller(njobs);
+    for (size_t j = 0; j < njobs; j++)
+        if (nnz[j] && jobs[j].pmk)
+            for (int k = 0; k < 8; k++)
+                caller[j][k] = (uint32_t)jobs[j].pmk[4 * k] << 24 | (uint32_t)jobs[j].pmk[4 * k + 1] << 16 |
+                               (uint32_t)jobs[j].pmk[4 * k + 2] << 8 | jobs[j].pmk[4 * k + 3];
+    const size_t chunk = 16, nchunks = (nslots + chunk - 1) / chunk;
+    std::atomic<size_t> next{0};
+    host_parallel(host_threads_for(nchunks, 1), [&](size_t) {
+        for (size_t c; (c = next.fetch_add(1, std::memory_order_relaxed)) < nchunks;)
+            for (size_t s = c * chunk; s < std::min(nslots, (c + 1) * chunk); s++) {
+                const uint32_t j = sjob[s];
+                if (sord[s] > best[j].load(std::memory_order_relaxed)) continue;
+                const uint32_t* pw = suid[s] == NO_UID ? caller[j].data() : pmk[suid[s]].data();
+                const int64_t a = verify_pmk(tb, job_line[j], sord[s], pw);
+                if (a < 0) continue;
+                satt[s] = (int32_t)a;
+                uint32_t cur = best[j].load(std::memory_order_relaxed);
+                while (sord[s] < cur && !best[j].compare_exchange_weak(cur, sord[s], std::memory_order_relaxed)) {
+                }
+            }
+    });
+
+    // first key in input order wins, then the first attempt in PHP order (common.php:186,280-289)
+    for (size_t j = 0; j < njobs; j++) {
+        const uint32_t o = best[j].load(std::memory_order_relaxed);
+        if (o == UINT32_MAX) continue;
+        const size_t s = jslot[j] + o;
+        const LineDev& L = tb.lines[job_line[j]];
+        rcs[j] = DWPA_HIT;
+        stats.hits++;
+        out[j].key_index = (int32_t)skidx[s];
+        pmk_bytes_out(suid[s] == NO_UID ? caller[j].data() : pmk[suid[s]].data(), out[j].pmk);
+        if (L.kind == LINE_PMKID) {
+            out[j].nc_valid = 0;
+        } else {
+            const uint32_t list = std::min(o, L.nlists - 1);
+            const AttDev& at = tb.atts[L.list_off + (size_t)list * L.natt + (size_t)satt[s]];
+            out[j].nc_valid = 1;
+            out[j].nc = at.nc;
+            out[j].endian = (int8_t)at.endian;
+        }
+    }
+    return 0;
+}
+
+int host_pbkdf2(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out) {
+    std::vector<std::vector<uint32_t>> salt(1);
+    std::vector<uint32_t> nblk{build_salt_blocks(std::string((const char*)essid, essid_len), salt[0])};
+    std::vector<Derive> dv(nkeys);
+    for (size_t i = 0; i < nkeys; i++)  // a null key derives as the empty key (as the device path)
+        dv[i] = Derive{keys[i].ptr, keys[i].ptr ? keys[i].len : 0, 0};
+    std::vector<std::array<uint32_t, 8>> pmk;
+    derive_all(dv, salt, nblk, pmk);
+    for (size_t i = 0; i < nkeys; i++) pmk_bytes_out(pmk[i].data(), out + 32 * i);
+    return 0;
+}
+
+}  // namespace dwpa

@@ -239,10 +239,15 @@ static void md5_km(const uint32_t* m, std::vector<uint32_t>& out) {
     }
 }
 
-enum class Kw { Sha1, Sha256, Md5 };
-// Append blocks [b0, b1) of the 16-word-block stream w to the pool as KW blocks; returns their word offset.
+enum class Kw { Sha1, Sha256, Md5, Raw };
+// Append blocks [b0, b1) of the 16-word-block stream w to the pool as KW blocks (Kw::Raw: as they are, 16 words
+// each -- TableBuilder::raw); returns their word offset.
 static uint32_t push_kw(std::vector<uint32_t>& pool, const uint32_t* w, size_t b0, size_t b1, Kw alg) {
     const uint32_t off = (uint32_t)pool.size();
+    if (alg == Kw::Raw) {
+        pool.insert(pool.end(), w + 16 * b0, w + 16 * b1);
+        return off;
+    }
     for (size_t b = b0; b < b1; b++) {
         if (alg == Kw::Sha1) sha1_kw(w + 16 * b, pool);
         else if (alg == Kw::Sha256) sha256_kw(w + 16 * b, pool);
@@ -338,7 +343,7 @@ static void add_explicit_attempts(TableBuilder& tb, LineDev& L, const std::vecto
         if (!same) break;
         prefix++;
     }
-    L.pre_off = push_kw(tb.pool, ref.data(), 0, prefix, alg);
+    L.pre_off = push_kw(tb.pool, ref.data(), 0, prefix, tb.raw ? Kw::Raw : alg);
     L.pre_nblk = (uint32_t)prefix;
     L.list_off = (uint32_t)tb.atts.size();
     L.nlists = (uint32_t)lists.size();
@@ -367,7 +372,7 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
         std::string msg = std::string("PMK Name") + p.mac_ap + p.mac_sta;
         std::vector<uint32_t> w = md_stream_be(msg, 64);
         L.msg_nblk = (uint32_t)(w.size() / 16);
-        L.msg_off = push_kw(pool, w.data(), 0, L.msg_nblk, Kw::Sha1);
+        L.msg_off = push_kw(pool, w.data(), 0, L.msg_nblk, raw ? Kw::Raw : Kw::Sha1);
         const bool ok = p.pmkid.size() >= 16;  // strncmp(20-byte digest, $pmkid, 16) needs >= 16 bytes
         for (int k = 0; k < 4; k++) L.target[k] = ok ? be32(p.pmkid, 4 * k) : 0;
         lines.push_back(L);
@@ -414,7 +419,7 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
     L.patch_w0 = L.patch_w1 = NO_PATCH;
     L.natt = (uint32_t)order.size();
     const Kw prf_alg = kv3 ? Kw::Sha256 : Kw::Sha1;
-    const bool att_kw = att_kw_all || L.natt < ATT_PARALLEL_MIN;
+    const bool att_kw = !raw && (att_kw_all || L.natt < ATT_PARALLEL_MIN);
     if (n0.size() >= patch + 4) {
         // Every attempt rewrites exactly bytes [patch, patch+4) of $n (common.php:255-259) and never changes its
         // length, so all attempts of all keys share one message apart from those 4 bytes: one list, one shared
@@ -424,7 +429,7 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
         const std::vector<uint32_t> w = md_stream_be(base, 64);
         const uint32_t W0 = (uint32_t)(o >> 2), W1 = (uint32_t)((o + 3) >> 2);
         const uint32_t prefix = W0 / 16;
-        L.pre_off = push_kw(pool, w.data(), 0, prefix, prf_alg);
+        L.pre_off = push_kw(pool, w.data(), 0, prefix, raw ? Kw::Raw : prf_alg);
         L.pre_nblk = prefix;
         const uint32_t blk_off = (uint32_t)pool.size();
         pool.insert(pool.end(), w.begin() + 16 * prefix, w.end());
@@ -473,7 +478,7 @@ uint32_t TableBuilder::add_line(const ParsedLine& p, int nc, int nc_mode, int ne
     if (p.keyver == 1 || p.keyver == 2) {
         std::vector<uint32_t> w = p.keyver == 1 ? md5_stream_le(p.eapol, 64) : md_stream_be(p.eapol, 64);
         L.mic_nblk = (uint32_t)(w.size() / 16);
-        L.mic_off = push_kw(pool, w.data(), 0, L.mic_nblk, p.keyver == 1 ? Kw::Md5 : Kw::Sha1);
+        L.mic_off = push_kw(pool, w.data(), 0, L.mic_nblk, raw ? Kw::Raw : p.keyver == 1 ? Kw::Md5 : Kw::Sha1);
     } else {
         const size_t len = p.eapol.size();
         const size_t nb = (len + 15) / 16;

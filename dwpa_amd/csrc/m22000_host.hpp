@@ -40,6 +40,9 @@ struct TableBuilder {
     // KW blocks of every attempt's PRF blocks for the key-parallel verifier: always (att_kw_all, scan API), else
     // only for lines with fewer than ATT_PARALLEL_MIN attempts (the check path verifies the others attempt-parallel).
     bool att_kw_all = false;
+    // Host backend (host_check.cpp): every block stays a raw 16-word block -- the PMKID message, the PRF prefix and
+    // the MIC blocks are not expanded to KW form, and no attempt gets KW blocks.
+    bool raw = false;
 
     // Adds a parsed (status 0) line; returns its index.
     uint32_t add_line(const ParsedLine& p, int nc, int nc_mode, int nec);

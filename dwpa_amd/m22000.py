@@ -3,7 +3,8 @@
 ``check_key_m22000`` keeps the exact call signature and return shape of the PHP function it replaces
 (web/common.php:157-307): ``False`` or ``[PSK, NC, endian, PMK]`` with ``NC``/``endian`` ``None`` for PMKID
 lines, ``endian`` in ``{None, 'BE', 'LE'}``, ``PSK`` after ``$HEX[]`` decoding and ``PMK`` as 32 raw bytes.
-All arithmetic runs on the GPU through the C ABI; without a device the calls raise ``DwpaError``.
+The arithmetic runs in libdwpa22000.so: on the GPU, or on the library's host backend for small calls and (only when
+asked for, ``init(allow_cpu_fallback=1)``) without a device; otherwise a call without a device raises ``DwpaError``.
 """
 from __future__ import annotations
 
@@ -22,6 +23,16 @@ def _b(x) -> bytes:
 
 def device_count() -> int:
     return L.check(L.load().dwpa_device_count(), "device_count")
+
+
+def init(device_mask: int = 0, batch: int = 0, rule_mode: int = L.DWPA_RULES_DEFAULT, allow_cpu_fallback: int = 0,
+         host_max_pmks: int = 0) -> int:
+    """dwpa_init: the process's device selection, check batch, rule-file mode and host backend switches
+    (allow_cpu_fallback 1/-1/0 = on/off/DWPA_CPU_FALLBACK; host_max_pmks n/-1/0 = small-call threshold/never/
+    DWPA_HOST_MAX_PMKS or 24).  Returns 0 or raises (DWPA_E_NODEV without a device unless the fallback is on)."""
+    cfg = L.Config(ctypes.sizeof(L.Config), int(device_mask), int(batch), 0, int(rule_mode), int(allow_cpu_fallback),
+                   int(host_max_pmks))
+    return L.check(L.load().dwpa_init(ctypes.byref(cfg)), "init")
 
 
 def hc_unhex(key) -> bytes:
@@ -143,8 +154,8 @@ class BatchJobs:
 
 
 def check_stats():
-    """dwpa_check_last_stats: {jobs, slots, pmks, tail_pmks, tail_waves, tail_waves_raised, hits, seconds} of this
-    thread's last check call."""
+    """dwpa_check_last_stats: {jobs, slots, pmks, tail_pmks, tail_waves, tail_waves_raised, hits, backend, seconds}
+    of this thread's last check call (backend: DWPA_BACKEND_DEVICE / _HOST_SMALL / _HOST_FALLBACK)."""
     st = L.CheckStats()
     L.check(L.load().dwpa_check_last_stats(ctypes.byref(st)), "check_last_stats")
     return {k: getattr(st, k) for k, _ in L.CheckStats._fields_ if k != "reserved"}
@@ -166,7 +177,8 @@ def check_batch(jobs):
 
 
 def pbkdf2_pmk(keys, essid) -> list:
-    """PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes), on the GPU."""
+    """PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes): on the GPU, or on the host backend for
+    at most host_max_pmks keys."""
     keys = [_b(k) for k in keys]
     e = _b(essid)
     arr, keep = L.bytes_array(keys)

@@ -11,8 +11,17 @@
  *       help_crack/help_crack.py:765-802 (command line :773, rc handling :776-786, outfile parsed by get_key :804-879)
  *
  * Plain C types only.  The caller owns every buffer; the library keeps no caller pointer after a call returns and
- * returns no heap memory.  All entry points are thread-safe.  There is no CPU fallback: without a usable gfx950
- * device every compute entry point returns DWPA_E_NODEV.
+ * returns no heap memory.  All entry points are thread-safe.
+ *
+ * Two backends answer the check path (dwpa_check_m22000, dwpa_check_batch) and dwpa_pbkdf2_pmk:
+ *   - the gfx950 device (the hot path: PBKDF2 and the verifiers as hand-written HIP kernels);
+ *   - the library's host backend (its own SHA-1 / SHA-256 / MD5 / AES-128, with SHA-NI / AES-NI where the CPU has
+ *     them, over the host pool's threads), the same semantics and the same results, which answers
+ *       (a) small calls -- at least one PBKDF2 derive and at most dwpa_config.host_max_pmks PMK-equivalents (put_work
+ *           checks one key per call, common.php:902, and one PBKDF2 chain on a lone GPU wave takes ~8 ms), and
+ *       (b) every call, when no usable gfx950 device exists or a device call failed, if allow_cpu_fallback is on.
+ *   dwpa_check_last_stats().backend says which one answered a call.  The client path (dwpa_crack_files, dwpa_scan_*,
+ *   dwpa_rules_expand*) is device-only: without a device it returns DWPA_E_NODEV / DWPA_RC_ERROR.
  *
  * Concurrent check calls (dwpa_check_m22000 / dwpa_check_batch / dwpa_pbkdf2_pmk from several threads) run on up to
  * DWPA_CALLS_PER_DEVICE (default 2) call contexts per device at once and overlap on the GPU; more callers wait for
@@ -28,8 +37,9 @@
 extern "C" {
 #endif
 
-#define DWPA_ABI_VERSION 3   /* 2: dwpa_crack_stats.rules / rules_skipped, dwpa_rules_count; 3: dwpa_check_last_stats,
-                                dwpa_config.rule_mode, dwpa_rules_count_ex, dwpa_crack_stats.rules_rejmem */
+#define DWPA_ABI_VERSION 4   /* 2: dwpa_crack_stats.rules / rules_skipped, dwpa_rules_count; 3: dwpa_check_last_stats,
+                                dwpa_config.rule_mode, dwpa_rules_count_ex, dwpa_crack_stats.rules_rejmem; 4: the host
+                                backend -- dwpa_config.allow_cpu_fallback / host_max_pmks, dwpa_check_stats.backend */
 
 /* ---- return codes ------------------------------------------------------------------------------------------ */
 #define DWPA_MISS 0            /* no key matched (PHP: False)                                                 */
@@ -38,7 +48,7 @@ extern "C" {
 #define DWPA_E_HEX (-2)        /* a required field is not valid even-length hex       (common.php:28-36,162-195) */
 #define DWPA_E_TYPE (-3)       /* type field is neither 01 nor 02                     (common.php:167,190,306) */
 #define DWPA_E_KEYVER (-4)     /* EAPOL key version not 1/2/3 or EAPOL < 49 bytes     (common.php:274-276)     */
-#define DWPA_E_NODEV (-10)     /* no usable gfx950 device                                                      */
+#define DWPA_E_NODEV (-10)     /* no usable gfx950 device (and allow_cpu_fallback off)                         */
 #define DWPA_E_HIP (-11)       /* HIP runtime error                                                            */
 #define DWPA_E_ARG (-12)       /* invalid argument                                                             */
 #define DWPA_E_NOMEM (-13)     /* host or device allocation failed                                             */
@@ -67,10 +77,12 @@ extern "C" {
 #define DWPA_NC_PHP 0          /* common.php:250-300: N+0, then V+k,V-k,N+k,N-k for k = 1..(nc>>1)+1, $n mutated */
 #define DWPA_NC_HASHCAT 1      /* hashcat --nonce-error-corrections=N: N+0, then +-k, k = 1..N, message_pair bits
                                   0x10 (no NC), 0x20 (LE only), 0x40 (BE only) honoured (third-party semantics)   */
-#define DWPA_NC_MAX 65536      /* the largest nc / nonce_error_corrections taken (PHP mode: 131,077 attempts per key;
-                                  the reference's call sites pass <= ~2 x nets.nc + 128).  A larger one on an EAPOL
-                                  line is DWPA_E_ARG for that job, so the PHP wrapper runs the original
-                                  check_key_m22000 for it; dwpa_scan_create / dwpa_crack_files refuse it.          */
+#define DWPA_NC_MAX 65664      /* the largest nc / nonce_error_corrections taken (PHP mode: 131,333 attempts per key).
+                                  Every reference call site fits, nets.nc being a smallint (db/wpa.sql:165):
+                                  common.php:919 passes |nc| * 2 + 128 <= 65,664, :606 (|nc| << 1) + 1 <= 65,537.  A
+                                  larger one on an EAPOL line is DWPA_E_ARG for that job (the PHP wrapper then runs
+                                  the original check_key_m22000 if it is kept, else throws); dwpa_scan_create /
+                                  dwpa_crack_files refuse it.                                                      */
 
 typedef struct {
     const uint8_t *ptr;        /* NULL = PHP null key (skipped, common.php:172,240) */
@@ -101,7 +113,18 @@ typedef struct {
     uint32_t batch;            /* candidate slots per device per launch; 0 = auto */
     int32_t nc_mode;           /* DWPA_NC_PHP or DWPA_NC_HASHCAT (crack_files default: HASHCAT) */
     int32_t rule_mode;         /* DWPA_RULES_DEFAULT (0) / _HASHCAT / _FULL (ABI 3; was reserved[0]) */
-    int32_t reserved[3];
+    int32_t allow_cpu_fallback; /* ABI 4 (was reserved[1]), dwpa_init only: 1 = without a usable device, or after a
+                                  device call failed (DWPA_E_NODEV / _HIP / _NOMEM / _OVERFLOW), check and PBKDF2
+                                  calls run on the host backend; -1 = never; 0 = DWPA_CPU_FALLBACK=1 from the
+                                  environment, else never.  With it on, dwpa_init returns 0 on a box without a device */
+    int32_t host_max_pmks;     /* ABI 4 (was reserved[2]), dwpa_init only: a check call with at least one PBKDF2 derive
+                                  and at most this many PMK-equivalents (derives + nonce-correction verify work /
+                                  16,388 compressions) runs on the host backend, a dwpa_pbkdf2_pmk call of at most this
+                                  many keys too; -1 = never (every call on the device); 0 = DWPA_HOST_MAX_PMKS from
+                                  the environment (<= 0: never), else 24.  Until the process's first device call
+                                  completes the threshold is 8x this: that call also starts the HIP runtime (0.2-0.7 s
+                                  in a fresh PHP-FPM worker) */
+    int32_t reserved[1];
 } dwpa_config;
 
 typedef struct {
@@ -133,8 +156,9 @@ int dwpa_check_m22000(const char *line, size_t line_len, const dwpa_bytes *keys,
  * each (ESSID, key) PMK is derived once.  rcs[i] / out[i] as for dwpa_check_m22000.  Returns 0 or a
  * negative code if the whole batch failed (device error). */
 int dwpa_check_batch(const dwpa_job *jobs, size_t njobs, dwpa_result *out, int *rcs);
-/* What the calling thread's last dwpa_check_m22000 / dwpa_check_batch call did (ABI 3): its jobs, the non-null keys
- * of usable lines (slots), the (ESSID, key) PMKs derived after deduplication, how many of those the tail launch
+/* What the calling thread's last dwpa_check_m22000 / dwpa_check_batch call did (ABI 3): which backend answered it
+ * (ABI 4), its jobs, the non-null keys of usable lines (slots), the (ESSID, key) PMKs derived after deduplication (on
+ * the host backend: by it; the tail fields below stay 0 there), how many of those the tail launch
  * derived (the remainder under one wave per SIMD, run beside the head at low wave priority), the tail's waves and
  * how many of them saw the head end and raised their priority (DWPA_TAIL_PRIO), the hits, and the call's wall time.
  * Returns 0, or DWPA_E_ARG before any check call in this thread. */
@@ -146,9 +170,13 @@ typedef struct {
     uint32_t tail_waves;
     uint32_t tail_waves_raised;
     uint32_t hits;
-    uint32_t reserved;
+    uint32_t backend;          /* ABI 4: DWPA_BACKEND_* -- who answered the call */
     double seconds;
 } dwpa_check_stats;
+#define DWPA_BACKEND_DEVICE 0         /* the gfx950 device                                                    */
+#define DWPA_BACKEND_HOST_SMALL 1     /* the host backend: a small call (dwpa_config.host_max_pmks)           */
+#define DWPA_BACKEND_HOST_FALLBACK 2  /* the host backend: no usable device / a failed device call, with
+                                         allow_cpu_fallback on                                               */
 int dwpa_check_last_stats(dwpa_check_stats *out);
 /* What this process's copy of the library holds right now (ABI 3; host only, never initialises a device): device
  * buffers and pinned host memory of every call context, scan and crack call, the host pool's worker threads (grown
@@ -165,7 +193,8 @@ typedef struct {
 int dwpa_resource_stats(dwpa_resources *out);
 
 /* ---- primitives exposed for parity tests and wrappers ------------------------------------------------------ */
-/* PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes, no $HEX[] decoding). */
+/* PMK = PBKDF2-HMAC-SHA1(key, essid, 4096, 32) for every key (raw bytes, no $HEX[] decoding; a NULL key derives as
+ * the empty key).  At most host_max_pmks keys: on the host backend, as the check path routes. */
 int dwpa_pbkdf2_pmk(const dwpa_bytes *keys, size_t nkeys, const uint8_t *essid, size_t essid_len,
                     uint8_t *pmks_out /* nkeys * 32 */);
 /* hashcat $HEX[...] decoding as web/common.php:3-25; *out_len <= in_len. */

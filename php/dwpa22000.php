@@ -5,22 +5,28 @@
  * check_key_m22000_gpu() is a drop-in for check_key_m22000() (web/common.php:157-307): same arguments, same
  * return value (False or [PSK, NC, 'BE'|'LE'|Null, PMK]).  check_keys_m22000_gpu_batch() takes many
  * [hashline, keys, pmk, nc] jobs at once (put_work's loop, common.php:900-925; rkg.php:126,147) so every
- * (ESSID, key) PMK is derived once on the GPU.  Needs hc_unhex() from common.php for the returned PSK.
+ * (ESSID, key) PMK is derived once.  Needs hc_unhex() from common.php for the returned PSK.
+ *
+ * The library answers every call itself (ABI 4): on the GPU, or on its host backend -- its own SHA-1 / SHA-256 /
+ * MD5 / AES-128 on the server's cores -- for small calls (one key, put_work's shape, common.php:902) and, because
+ * ffi() turns allow_cpu_fallback on, on a server without a usable GPU or after a failed device call.  So the
+ * reference's own function is not needed for correctness; kept under the name check_key_m22000_php it is only the
+ * last resort below (INTEGRATION.md section 2).
  *
  * Library return code -> behaviour (pinned by tests/test_php_wrapper.py, which parses this file):
  *   DWPA_HIT (1)                                      -> [PSK, NC, endian, PMK]
  *   DWPA_MISS (0), parse codes -1..-4                 -> False, exactly as check_key_m22000's own early returns
  *                                                        (common.php:160-164,276,306)
- *   device / runtime codes <= -10 (NODEV, HIP, ARG,   -> never False: put_work (common.php:902,919) reads False
- *   NOMEM, IO, OVERFLOW, RULE)                           as "this PSK is wrong" and would discard a genuine crack.
- *                                                        The job goes to the original PHP check, kept under the
- *                                                        name check_key_m22000_php (INTEGRATION.md section 2), or,
- *                                                        if that is not defined, a Dwpa22000Error is thrown.
- *   a caller $pmk that is not 32 bytes                 -> the original PHP check as well: PHP HMACs with the PMK's
- *                                                        actual length (common.php:178-188), the ABI takes 32 bytes.
+ *   runtime codes <= -10 (the host backend failed     -> never False: put_work (common.php:902,919) reads False
+ *   too: NOMEM, ...; ARG)                                as "this PSK is wrong" and would discard a genuine crack.
+ *                                                        The job goes to check_key_m22000_php if it is defined,
+ *                                                        else a Dwpa22000Error is thrown.
+ *   a caller $pmk that is not 32 bytes                 -> the same last resort: PHP HMACs with the PMK's actual
+ *                                                        length (common.php:178-188), the ABI takes 32 bytes
+ *                                                        (nets.pmk is binary(32), db/wpa.sql, so no call site has one).
  *
  * Not exercised by a PHP interpreter here: the build image has none (SURVEY.md section 8c); the same C entry
- * points are exercised through ctypes by tests/test_gpu_parity.py.
+ * points are exercised through ctypes by tests/test_gpu_parity.py and tests/test_host_backend.py.
  */
 
 final class Dwpa22000Error extends RuntimeException
@@ -34,14 +40,10 @@ final class Dwpa22000
     const FIRST_DEVICE_ERROR = -10;  /* DWPA_E_NODEV; every code <= this is a device/runtime failure */
 
     private static $ffi = null;
-    /* whether this worker process has made a library call yet: its first one also initialises the HIP runtime, loads
-     * the code objects and creates the call context (bench.py --workload c1cold, INTEGRATION.md section 2) */
-    public static $warm = false;
-    /* a cold worker sends a derive to the GPU only from this many keys on: PHP's ~1.1 ms per key then costs about what
-     * the first call does (~0.2-0.3 s for a worker started alone, up to ~0.7 s in a start-up storm of 16) */
-    const COLD_MIN_KEYS = 256;
-    /* DWPA_NC_MAX: the largest nc the library takes; the ABI's nc is an int32 */
-    const NC_MAX = 65536;
+    /* DWPA_NC_MAX: the largest nc the library takes (every reference call site fits); the ABI's nc is an int32 */
+    const NC_MAX = 65664;
+    /* dwpa_config.allow_cpu_fallback for this worker: 1 = the host backend answers without a usable GPU */
+    const CPU_FALLBACK = 1;
 
     public static function ffi()
     {
@@ -50,24 +52,34 @@ final class Dwpa22000
 typedef struct { const uint8_t *ptr; size_t len; } dwpa_bytes;
 typedef struct { int32_t key_index; int32_t nc; int8_t endian; uint8_t nc_valid; uint8_t reserved[2]; uint8_t pmk[32]; } dwpa_result;
 typedef struct { const char *line; size_t line_len; const dwpa_bytes *keys; size_t nkeys; const uint8_t *pmk; int32_t nc; } dwpa_job;
+typedef struct { uint32_t struct_size; uint32_t device_mask; uint32_t batch; int32_t nc_mode; int32_t rule_mode; int32_t allow_cpu_fallback; int32_t host_max_pmks; int32_t reserved[1]; } dwpa_config;
+int dwpa_init(const dwpa_config *cfg);
 int dwpa_check_m22000(const char *line, size_t line_len, const dwpa_bytes *keys, size_t nkeys, const uint8_t *pmk, int nc, dwpa_result *out);
 int dwpa_check_batch(const dwpa_job *jobs, size_t njobs, dwpa_result *out, int *rcs);
 int dwpa_device_count(void);
 const char *dwpa_strerror(int code);
 CDEF;
             $lib = getenv('DWPA_LIB') ?: (defined('DWPA_LIB') ? DWPA_LIB : '/opt/dwpa/libdwpa22000.so');
-            self::$ffi = FFI::cdef($cdef, $lib);
+            $ffi = FFI::cdef($cdef, $lib);
+            // the host backend answers when this server has no usable GPU (host_max_pmks 0: the library default)
+            $cfg = $ffi->new('dwpa_config');
+            $cfg->struct_size = FFI::sizeof($cfg);
+            $cfg->allow_cpu_fallback = self::CPU_FALLBACK;
+            $ffi->dwpa_init(FFI::addr($cfg));
+            self::$ffi = $ffi;
         }
         return self::$ffi;
     }
 
-    /* rc <= -10: the library could not decide (no device, runtime error, ...) -- the answer is not "wrong key" */
+    /* rc <= -10: the library could not decide (its host backend failed too, or an argument it cannot take) -- the
+     * answer is not "wrong key" */
     public static function is_device_error($rc)
     {
         return $rc <= self::FIRST_DEVICE_ERROR;
     }
 
-    /* the original PHP check_key_m22000 (renamed check_key_m22000_php), or an exception -- never False */
+    /* last resort: the original PHP check_key_m22000 if kept (renamed check_key_m22000_php), or an exception --
+     * never False */
     public static function fallback($rc, $hashline, $keys, $pmk, $nc)
     {
         if (function_exists('check_key_m22000_php')) {
@@ -156,7 +168,6 @@ function check_key_m22000_gpu($hashline, $keys, $pmk = False, $nc = 128)
     $res = $ffi->new('dwpa_result');
     $rc = $ffi->dwpa_check_m22000($hashline, strlen($hashline), $arr, count($vals),
                                   $pm === null ? null : FFI::addr($pm[0]), (int) $nc, FFI::addr($res));
-    Dwpa22000::$warm = true;
     if ($rc == Dwpa22000::HIT) {
         return Dwpa22000::result($vals, $res);
     }
@@ -208,7 +219,6 @@ function check_keys_m22000_gpu_batch($jobs)
         $out = $ffi->new("dwpa_result[$m]");
         $rcs = $ffi->new("int[$m]");
         $rc = $ffi->dwpa_check_batch($cj, $m, $out, $rcs);
-        Dwpa22000::$warm = true;
         foreach ($gpu as $s => $i) {
             // the whole batch failed (rc < 0), or this job did: the PHP check decides, never a silent False
             $jrc = $rc < 0 ? $rc : $rcs[$s];
@@ -228,41 +238,32 @@ function check_keys_m22000_gpu_batch($jobs)
     return $res;
 }
 
-/* Routing by call shape (INTEGRATION.md §2, round-4 latencies in profiles/r04/c1lat.json): a one-key check and a
- * caller-PMK check of a PMKID line stay in PHP (one PBKDF2 on one core, 1.1 ms, against 8.5 ms for the GPU's single
- * PBKDF2 chain; one HMAC, 4 us, against a GPU call's ~0.08 ms); a check of several keys and a caller-PMK check of an
- * EAPOL line (up to 521 PRF + MIC attempts, 2-12x faster on the GPU) go to the library.  Needs
- * check_key_m22000_php, the reference's function renamed; without it everything goes to the library. */
+/* Since ABI 4 the library routes by call shape itself (one key, or a handful: its host backend on this server's
+ * cores, well under PHP's 1.1 ms per key; more keys and caller-PMK checks of EAPOL lines: the GPU), and a worker's
+ * first GPU call is taken only by a call big enough to amortise the runtime start-up (the threshold is 8x higher
+ * until then, INTEGRATION.md section 2).  check_key_m22000_routed stays as the name earlier deployments call. */
 function check_key_m22000_routed($hashline, $keys, $pmk = False, $nc = 128)
 {
-    if (function_exists('check_key_m22000_php')) {
-        $pmkid = strncmp($hashline, 'WPA*01*', 7) === 0;
-        if ($pmk ? $pmkid : count($keys) < 2) {
-            return check_key_m22000_php($hashline, $keys, $pmk, $nc);
-        }
-        // a worker's first library call pays the runtime start-up (round 5, profiles/r05/c1cold/): until then only
-        // a derive big enough to cost PHP as much goes to the GPU; caller-PMK checks (<= 1.8 ms in PHP) stay in PHP
-        if (!Dwpa22000::$warm && ($pmk || count($keys) < Dwpa22000::COLD_MIN_KEYS)) {
-            return check_key_m22000_php($hashline, $keys, $pmk, $nc);
-        }
-    }
     return check_key_m22000_gpu($hashline, $keys, $pmk, $nc);
 }
 
-/* Optional, for pools that keep their workers (pm = static, pm.max_requests = 0): pay the start-up in this worker
- * now -- the runtime, the code objects and the call context, through one one-key check of a fixed PMKID line (a
- * miss) -- e.g. from an auto_prepend_file on the worker's first request, so that its later calls are all warm.
- * Returns the number of usable gfx950 devices (0: none -- every check then goes to check_key_m22000_php). */
+/* Optional, for pools that keep their workers (pm = static, pm.max_requests = 0): pay the GPU start-up in this worker
+ * now -- the runtime, the code objects and the call context, through one 512-key check of a fixed PMKID line (a
+ * miss; big enough to go to the GPU) -- e.g. from an auto_prepend_file on the worker's first request.  Returns the
+ * number of usable gfx950 devices (0: none -- every check then runs on the library's host backend). */
 function dwpa22000_warmup()
 {
     $ffi = Dwpa22000::ffi();
     $n = $ffi->dwpa_device_count();
     if ($n > 0) {
         $line = 'WPA*01*' . str_repeat('0', 32) . '*020000000001*020000000002*7761726d7570***';
-        [$arr, $keep, $vals] = Dwpa22000::keys(['warmup-key']);
+        $keys = [];
+        for ($i = 0; $i < 512; $i++) {
+            $keys[] = sprintf('warmup-key-%04d', $i);
+        }
+        [$arr, $keep, $vals] = Dwpa22000::keys($keys);
         $res = $ffi->new('dwpa_result');
-        $rc = $ffi->dwpa_check_m22000($line, strlen($line), $arr, 1, null, 128, FFI::addr($res));
-        Dwpa22000::$warm = $rc >= 0;
+        $ffi->dwpa_check_m22000($line, strlen($line), $arr, count($vals), null, 128, FFI::addr($res));
     }
     return max(0, $n);
 }

@@ -13,6 +13,7 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built libdwpa22000.so")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "host_routing: a GPU test of the library's small-call host routing")
 
 
 def load_golden(name):
@@ -34,6 +35,17 @@ def job_args(j):
     keys = [None if k is None else bytes.fromhex(k) for k in j["keys"]]
     pmk = bytes.fromhex(j["pmk"]) if j["pmk"] else False
     return line, keys, pmk, j["nc"]
+
+
+@pytest.fixture(autouse=True)
+def _device_path_for_gpu_tests(request, monkeypatch):
+    """GPU tests measure the device path: the library's small-call routing to its host backend (ABI 4,
+    dwpa_config.host_max_pmks) is off for them, so a one-key parity check runs the HIP kernels, not the CPU.  Tests
+    marked host_routing exercise the routing and set it themselves."""
+    if request.node.get_closest_marker("gpu") and not request.node.get_closest_marker("host_routing"):
+        monkeypatch.setenv("DWPA_HOST_MAX_PMKS", "-1")
+        monkeypatch.delenv("DWPA_CPU_FALLBACK", raising=False)
+    yield
 
 
 @pytest.fixture(scope="session")

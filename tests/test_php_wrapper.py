@@ -5,8 +5,9 @@ are checked against include/dwpa22000.h:
 
 * DWPA_HIT -> the [PSK, NC, endian, PMK] array; DWPA_MISS and the parse codes -1..-4 -> False, as
   check_key_m22000's own early returns (web/common.php:160-164,276,306);
-* every device/runtime code (<= -10) -> the original PHP check (check_key_m22000_php) or an exception, never
-  False: put_work (common.php:902,919) reads False as "wrong PSK" and would silently drop a genuine crack;
+* every runtime code (<= -10; since ABI 4 the library's host backend has already answered a call without a GPU) ->
+  the original PHP check if kept (check_key_m22000_php) or an exception, never False: put_work (common.php:902,919)
+  reads False as "wrong PSK" and would silently drop a genuine crack;
 * a caller $pmk of any length other than 32 -> the original PHP check (PHP HMACs with the actual length,
   common.php:178-188); no padding or truncation.
 """
@@ -110,31 +111,25 @@ def test_pmk_is_never_padded_or_truncated():
     assert "return !$pmk || strlen((string) $pmk) == 32;" in ok
 
 
-def test_routed_check_follows_the_latency_table():
-    """check_key_m22000_routed (profiles/r04/c1lat.json): one-key checks and PMKID caller-PMK
-    checks go to the PHP function when it exists; everything else to the library."""
+def test_library_routes_and_falls_back_itself():
+    """ABI 4: ffi() turns the library's host backend on for a server without a usable GPU (allow_cpu_fallback), and
+    check_key_m22000_routed no longer needs the reference's function: it is the library's own routing (small calls on
+    the host backend, the rest on the GPU) under the name earlier deployments call.  dwpa22000_warmup() sends one call
+    big enough for the GPU even before the first device call (8 x the default 24 PMK-equivalents)."""
     src = _src()
-    body = src[src.index("function check_key_m22000_routed"):]
-    assert "function_exists('check_key_m22000_php')" in body
-    assert "strncmp($hashline, 'WPA*01*', 7) === 0" in body
-    assert "$pmk ? $pmkid : count($keys) < 2" in body
-    assert body.index("return check_key_m22000_php(") < body.index("return check_key_m22000_gpu(")
-
-
-def test_routed_check_accounts_for_the_cold_first_call():
-    """Round 5 (profiles/r05/c1cold/): a worker's first library call also starts the HIP runtime (~0.2-0.7 s), so a
-    cold worker routes only derives of >= COLD_MIN_KEYS keys to the GPU; every library call marks the worker warm;
-    dwpa22000_warmup() pays the start-up with one fixed one-key check and marks it warm only on success."""
-    src = _src()
-    body = _function(src, "check_key_m22000_routed")
-    assert "!Dwpa22000::$warm && ($pmk || count($keys) < Dwpa22000::COLD_MIN_KEYS)" in body
-    assert "const COLD_MIN_KEYS = 256;" in src
-    assert _function(src, "check_key_m22000_gpu").count("Dwpa22000::$warm = true;") == 1
-    assert _function(src, "check_keys_m22000_gpu_batch").count("Dwpa22000::$warm = true;") == 1
+    ffi = _function(src, "ffi")
+    assert "$cfg->allow_cpu_fallback = self::CPU_FALLBACK;" in ffi and "$ffi->dwpa_init(FFI::addr($cfg));" in ffi
+    assert "$cfg->struct_size = FFI::sizeof($cfg);" in ffi
+    assert _const(src, "CPU_FALLBACK") == 1
+    routed = _function(src, "check_key_m22000_routed")
+    assert "check_key_m22000_php" not in routed
+    assert routed.strip() == "return check_key_m22000_gpu($hashline, $keys, $pmk, $nc);"
+    assert "$warm" not in src and "COLD_MIN_KEYS" not in src
     warm = _function(src, "dwpa22000_warmup")
-    assert "dwpa_device_count()" in warm and "Dwpa22000::$warm = $rc >= 0;" in warm
+    n = int(re.search(r"\$i < (\d+);", warm).group(1))
+    assert n > 8 * 24
     line = "WPA*01*" + "0" * 32 + "*020000000001*020000000002*7761726d7570***"
-    assert line.split("*")[3:6] == ["020000000001", "020000000002", "7761726d7570"]
+    assert "$line = 'WPA*01*' . str_repeat('0', 32) . '*020000000001*020000000002*7761726d7570***';" in warm
     import dwpa_amd
     assert dwpa_amd.parse_m22000(line)["type"] == 1  # the warm-up line is a valid PMKID line
 
