@@ -221,6 +221,37 @@ def make_dictionary(n, seed=2):
     return off, data
 
 
+def _pmk_cache(S, essid):
+    cache = {}
+
+    def pmk_of(psk):
+        if psk not in cache:
+            cache[psk] = S.pmk(psk, essid)
+        return cache[psk]
+    return pmk_of
+
+
+def verify_timed_hits(w, hits, batches):
+    """The hits of the timed steps (untimed check): every reported hit is genuine (w.genuine
+    re-derives it: the candidate at the reported id is the line's PSK and the PMK is the oracle's), and every expected
+    (line, candidate) -- the plant, and in C3 every line whose PSK is in the keyspace -- is reported exactly once per
+    timed scan of the batch that holds it."""
+    from collections import Counter
+    got = Counter((h["line"], h["cand"]) for h in hits)
+    false_hits = sum(1 for h in hits if not w.genuine(h))
+    scans = Counter(batches)
+    missing = extra = 0
+    for key, b in w.expected.items():
+        want, have = scans.get(b, 0), got.get(key, 0)
+        missing += max(0, want - have)
+        extra += max(0, have - want)
+    plant_scans = scans.get(w.plant_batch, 0)
+    return (false_hits == 0 and missing == 0 and extra == 0), {
+        "timed_hits": len(hits), "timed_hits_false": false_hits, "timed_expected_missing": missing,
+        "timed_expected_extra": extra, "timed_plant_scans": plant_scans,
+        "expected_pairs": len(w.expected), "timed_expected_reports": sum(scans.get(b, 0) for b in w.expected.values())}
+
+
 class Workload:
     """One BASELINE.json config as a sequence of steps over HBM-resident candidates."""
     name = ""
@@ -261,12 +292,18 @@ def build_c2(args, local, S, Scan, Dictionary, shard=0):
         return any(h["cand"] == w.plant and h["nc"] == 3 and h["endian"] == "LE" and h["pmk"] == S.pmk(w.psk, w.essid)
                    for h in hits)
 
+    def genuine(h):  # the reported word is the line's PSK (the plant, or a dictionary duplicate of it)
+        word = w.data[int(w.off[h["cand"]]):int(w.off[h["cand"] + 1])].tobytes()
+        return h["line"] == 0 and word == w.psk and (h["nc"], h["endian"]) == (3, "LE") and h["pmk"] == pmk_of(w.psk)
+
     def cpu_keys(m):  # the m dictionary words ending at the planted PSK
         lo = w.plant - m + 1
         o = w.off[lo:w.plant + 2].astype("int64")
         raw = w.data[o[0]:o[-1]].tobytes()
         return [raw[o[i] - o[0]:o[i + 1] - o[0]] for i in range(m)]
+    pmk_of = _pmk_cache(S, w.essid)
     w.load, w.check, w.plant_batch = load, check, w.plant // w.B
+    w.genuine, w.expected = genuine, {(0, w.plant): w.plant_batch}
     w.cpu_line, w.cpu_keys, w.cpu_what = w.line, cpu_keys, "dictionary words"
     w.algo_bytes_per_pmk = ALGO_BYTES_PER_PMK
     return w
@@ -298,7 +335,12 @@ def build_c4(args, local, S, Scan, Dictionary, shard=0):
 
     def check(hits):
         return any(h["cand"] == w.plant and h["pmk"] == S.pmk(b"%08d" % w.plant, w.essid) for h in hits)
+
+    def genuine(h):
+        return h["line"] == 0 and h["cand"] == w.plant and h["pmk"] == pmk_of(b"%08d" % w.plant)
+    pmk_of = _pmk_cache(S, w.essid)
     w.load, w.check, w.plant_batch = load, check, w.plant // w.B
+    w.genuine, w.expected = genuine, {(0, w.plant): w.plant_batch}
     w.cpu_line, w.cpu_keys = w.line, lambda m: [b"%08d" % v for v in range(w.plant - m + 1, w.plant + 1)]
     w.cpu_what = "8-digit candidates"
     w.algo_bytes_per_pmk = ALGO_BYTES_PER_PMK
@@ -323,6 +365,7 @@ def build_c3(args, local, S, Scan, Dictionary, shard=0):
     w.off, w.data = dictionary_arrays(base)
     w.dict = Dictionary(w.off, w.data, device=local)
     lines, w.plants = [], []
+    line_psk = []  # per line: (PSK or None when it is outside the keyspace, ESSID, candidate id)
     for e in range(args.essids):
         essid, ap, sta, an, sn = S.random_net(net_rng)
         for k in range(rng.randint(1, 4)):
@@ -330,8 +373,11 @@ def build_c3(args, local, S, Scan, Dictionary, shard=0):
             psk = expanded[4 * e + k][ri]
             if not psk or not 8 <= len(psk) <= 63:
                 psk = b"not-in-keyspace-%d" % k
-            elif e == 0 and k == 0:
-                w.plants.append((len(lines), wi * len(rules) + ri, essid, psk))
+                line_psk.append((None, essid, None))
+            else:
+                line_psk.append((psk, essid, wi * len(rules) + ri))
+                if e == 0 and k == 0:
+                    w.plants.append((len(lines), wi * len(rules) + ri, essid, psk))
             if k % 2:
                 lines.append(S.pmkid_line(psk, essid, rng.randbytes(6), sta))
             else:
@@ -360,6 +406,24 @@ def build_c3(args, local, S, Scan, Dictionary, shard=0):
     def check(hits):
         return all(any(h["line"] == li and h["pmk"] == S.pmk(psk, essid) for h in hits)
                    for li, cand, essid, psk in w.plants)
+
+    from oracle import rules as R
+    parsed_rules = [R.parse(r) for r in rules]
+    pmks = {}
+
+    def genuine(h):  # the reported (word, rule) candidate is the line's PSK, and the PMK is the oracle's
+        psk, essid, _ = line_psk[h["line"]]
+        wi, ri = divmod(h["cand"], w.nrules)
+        if psk is None or R.apply(parsed_rules[ri], base[wi]) != psk:
+            return False
+        if h["line"] not in pmks:
+            pmks[h["line"]] = S.pmk(psk, essid)
+        return h["pmk"] == pmks[h["line"]]
+    # every in-keyspace line is reported once per scan of the batch holding its (word, rule) candidate
+    w.genuine = genuine
+    assert w.nrules == len(rules), "every rule of the WPA set parses, so candidate ids are word * len(rules) + rule"
+    w.expected = {(li, c): (c // w.nrules) // w.words_per_step
+                  for li, (psk, _, c) in enumerate(line_psk) if psk is not None}
 
     def cpu_keys(m):  # the m rule candidates (word-major, 8..63 only) ending at the first planted one
         from oracle import rules as R
@@ -575,11 +639,17 @@ def main():
     else:
         total = float(done)
 
-    # correctness: the batch holding the planted PSK(s) must report them (untimed)
+    # correctness (untimed): the hits of the timed steps, each re-derived, and every timed scan of the planted batch
+    # reporting the plant; then one more scan of the planted batch, which must report it too
+    timed_hits = []
     for k in range(P):
-        w.scans[k].hits(streams[k].handle)
+        timed_hits += w.scans[k].hits(streams[k].handle)
+    timed_ok, hits_check = verify_timed_hits(w, timed_hits,
+                                             [b for _, b in weak_units(rank, args.warmup, args.steps, w.nbatches)])
     step(w.plant_batch, 0)
-    verified = bool(w.check(w.scans[0].hits(streams[0].handle)))
+    plant_ok = bool(w.check(w.scans[0].hits(streams[0].handle)))
+    hits_check["plant_rescan_ok"] = plant_ok
+    verified = timed_ok and plant_ok
     if world > 1:  # every rank's own planted PSK must come back (each rank scans its own shard)
         from dwpa_amd.shard import all_ranks
         verified = all_ranks(dist, verified)
@@ -614,6 +684,7 @@ def main():
                                        w.algo_bytes_per_pmk, args.peak_costs),
             "cpu_baseline": cpu,
             "hits_verified": verified,
+            "hits_check": hits_check,
             "pbkdf2_kernel": "k_pbkdf2 (hipcc schedule)" if os.environ.get("DWPA_PBKDF2_PLAIN", "0") not in ("", "0")
                              else "k_pbkdf2_gfx950 (gfx950 VALU issue pass)",
             "rank0_local_s": round(elapsed_local, 4),

@@ -139,3 +139,27 @@ def test_rank_device_index(monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "4,5")
     with pytest.raises(SystemExit):
         bench.check_device(5, 5)
+
+
+def test_timed_hits_verification():
+    """bench.py's check of the timed steps' hits: every timed scan of the planted batch must
+    report the plant exactly once, a hit that is not genuine fails the line, and so does a missing or repeated one."""
+    import bench
+
+    class W:
+        plant_batch = 5
+        expected = {(0, 99): 5}
+
+        @staticmethod
+        def genuine(h):
+            return h["cand"] == 99
+
+    batches = [5, 0, 1, 2, 3, 4, 5]  # two timed scans of batch 5
+    plant = {"line": 0, "cand": 99}
+    ok, d = bench.verify_timed_hits(W, [plant, plant], batches)
+    assert ok and d["timed_plant_scans"] == 2 and d["timed_hits_false"] == 0
+    assert not bench.verify_timed_hits(W, [plant], batches)[0]                      # one scan lost the plant
+    assert not bench.verify_timed_hits(W, [plant, plant, plant], batches)[0]        # reported three times
+    assert not bench.verify_timed_hits(W, [plant, plant, {"line": 0, "cand": 7}], batches)[0]  # a false hit
+    ok, d = bench.verify_timed_hits(W, [], [0, 1, 2])                               # plant batch not timed
+    assert ok and d["timed_plant_scans"] == 0

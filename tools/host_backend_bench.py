@@ -1,0 +1,77 @@
+"""Host backend figures on this machine's CPU (dwpa_amd/csrc/host_check.cpp): which primitives CPUID selected,
+PBKDF2 throughput at 1 thread and at the pool's threads, and the latency of the server's small check calls (one key
+vs a PMKID / EAPOL keyver 2 / keyver 3 line at nc=128, caller-PMK checks), each beside the same call through the C
+oracle (OpenSSL, one PHP request's core).  Every result is checked against the oracle.  Prints one JSON line.
+
+    python tools/host_backend_bench.py [--reps N]
+"""
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("DWPA_HOST_MAX_PMKS", "1000000000")  # every call with a derive on the host backend
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import dwpa_amd
+    from dwpa_amd import m22000 as M
+    from oracle import oracle as O
+    from tests import synth as S
+
+    rng = random.Random(11)
+    essid, apm, sta, an, sn = S.random_net(rng, essid_len=10)
+
+    def med(fn, n):
+        fn()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts) * 1e3
+
+    out = {"cpu_model": next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")),
+                             None),
+           "flags": sorted({f for l in open("/proc/cpuinfo") if l.startswith("flags") for f in l.split()}
+                           & {"sha_ni", "aes", "avx2", "avx512f"}),
+           "host_threads_cap": int(os.environ.get("DWPA_HOST_THREADS", "16"))}
+    rows = []
+    for n in (1, 2, 16, 64, 256):
+        keys = [S.fast_psk(rng) for _ in range(n)]
+        ms = med(lambda: dwpa_amd.pbkdf2_pmk(keys, essid), max(3, args.reps // (1 + n // 16)))
+        ok = b"".join(dwpa_amd.pbkdf2_pmk(keys, essid)) == O.c_pbkdf2_many(keys, essid, threads=8)
+        rows.append({"call": f"dwpa_pbkdf2_pmk, {n} key(s)", "ms": round(ms, 3), "pmk_per_s": round(n / ms * 1e3),
+                     "same_result": ok})
+    psk = S.fast_psk(rng)
+    pmk = S.pmk(psk, essid)
+    lines = {"pmkid": S.pmkid_line(psk, essid, apm, sta),
+             "eapol-kv2": S.eapol_line(psk, essid, apm, sta, an, sn, 2, -5, "BE", rng=rng),
+             "eapol-kv3": S.eapol_line(psk, essid, apm, sta, an, sn, 3, 7, "LE", rng=rng)}
+    for kind, line in lines.items():
+        for label, job in (("1 key, hit", (line, [psk], False, 128)),
+                           ("1 key, miss", (line, [S.fast_psk(rng)], False, 128)),
+                           ("caller PMK, miss, nc=258", (line, [b""], bytes(32), 258))):
+            ms = med(lambda: dwpa_amd.check_key_m22000(*job), args.reps)
+            got = dwpa_amd.check_key_m22000(*job)
+            backend = M.check_stats()["backend"]
+            cpu = med(lambda: O.c_check_key_m22000(*job), max(3, args.reps // 4))
+            rows.append({"call": f"check_key_m22000, {kind}, {label}", "ms": round(ms, 3),
+                         "oracle_openssl_1core_ms": round(cpu, 3), "backend": backend,
+                         "same_result": got == O.c_check_key_m22000(*job)})
+    out["rows"] = rows
+    out["all_same"] = all(r["same_result"] for r in rows)
+    print(json.dumps(out))
+    sys.exit(0 if out["all_same"] else 3)
+
+
+if __name__ == "__main__":
+    main()
