@@ -26,10 +26,18 @@ build/pbkdf2/pbkdf2_gfx950.s: $(SRC)/pbkdf2_gfx950.hip $(SRC)/pbkdf2_dev.hpp $(S
 	@mkdir -p build/pbkdf2
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 --cuda-device-only -S $< -o $@
 
-build/pbkdf2/pbkdf2_issue.s: build/pbkdf2/pbkdf2_gfx950.s $(SRC)/gen/issue_pass.py Makefile
-	python3 $(SRC)/gen/issue_pass.py $< $@ k_pbkdf2_gfx950+k_pbkdf2_gfx950_ms+k_pbkdf2_gfx950_mg+k_pbkdf2_gfx950_p+k_pbkdf2_gfx950_ms_p+k_pbkdf2_gfx950_mg_p+k_pbkdf2_gfx950_q+k_pbkdf2_gfx950_mg_q $(ISSUE_RULE)
+PBKDF2_KERNELS := k_pbkdf2_gfx950+k_pbkdf2_gfx950_ms+k_pbkdf2_gfx950_mg+k_pbkdf2_gfx950_p+k_pbkdf2_gfx950_ms_p+k_pbkdf2_gfx950_mg_p+k_pbkdf2_gfx950_q+k_pbkdf2_gfx950_mg_q
 
-build/pbkdf2/pbkdf2_gfx950.hsaco: build/pbkdf2/pbkdf2_issue.s
+# the pass fails closed (an instruction it cannot model stops the build) ...
+build/pbkdf2/pbkdf2_issue.s: build/pbkdf2/pbkdf2_gfx950.s $(SRC)/gen/issue_pass.py Makefile
+	python3 $(SRC)/gen/issue_pass.py $< $@ $(PBKDF2_KERNELS) $(ISSUE_RULE)
+
+# ... and every scheduled loop must compute the compiler's results (tools/issue_equiv.py) before the code object links
+build/pbkdf2/issue_equiv.ok: build/pbkdf2/pbkdf2_gfx950.s build/pbkdf2/pbkdf2_issue.s tools/issue_equiv.py
+	python3 tools/issue_equiv.py $< $(PBKDF2_KERNELS) $(ISSUE_RULE) 2
+	@touch $@
+
+build/pbkdf2/pbkdf2_gfx950.hsaco: build/pbkdf2/pbkdf2_issue.s build/pbkdf2/issue_equiv.ok
 	$(LLVM)/clang -target amdgcn-amd-amdhsa -mcpu=$(ARCH) -c $< -o build/pbkdf2/pbkdf2_issue.o
 	$(LLVM)/ld.lld -shared build/pbkdf2/pbkdf2_issue.o -o $@
 

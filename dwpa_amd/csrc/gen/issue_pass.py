@@ -26,10 +26,14 @@ Rules (comma-separated, applied in the loop body only):
                   where the dependences allow; `alt` also prefers alternating 2-/4-cycle ops, `group` runs of one
                   rate (fewer 2 <-> 4-cycle transitions, for lone waves); ties go to the longest remaining critical
                   path, or with `orig` to the compiler's order; `asmnop` first drops the s_nop LLVM places after
-                  inline-asm blocks (the loop's v_bitop3 ops); `bank` then renames loop-local values so that fewer
+                  inline-asm blocks where provably dead (drop_asm_nops); `bank` then renames loop-local values so that fewer
                   v_bitop3_b32 read sources from one VGPR bank (bank_rename; A/B only, profiles/r05/vgpr_bank/).
-                  Applied before the nop rules (A/B)
+                  Applied before the nop rules (A/B).  Fails closed: an instruction outside SCHED_VALU (a second
+                  destination, an implicit operand, a transcendental op, DPP/SDWA) stops the build
   none            copy through
+
+The Makefile runs tools/issue_equiv.py on every scheduled kernel after the pass: the scheduled loop body must compute
+the same registers as the compiler's on random inputs, or the build stops.
 """
 import re
 import sys
@@ -87,24 +91,95 @@ def split_add3(line):
 
 _REG = re.compile(r"^(v\d+|s\d+|vcc|exec|scc)$")
 
+# The VALU ops the schedule may move (fail closed): each writes exactly one VGPR -- its first
+# operand -- and reads only its other operands, with no implicit operand (VCC, EXEC, M0), no second destination (the
+# _co_ carry-out ops, v_cmp*, v_readlane / v_readfirstlane, v_div_scale write an SGPR pair or VCC as well), no
+# transcendental unit (its results need wait states) and no DPP / SDWA lane crossing.  The PBKDF2 loop uses the first
+# five; any other op in a loop body stops the build instead of being list-scheduled on an assumption.
+SCHED_VALU = {"v_add3_u32", "v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_bitop3_b32", "v_mov_b32", "v_or_b32",
+              "v_and_b32", "v_xor3_b32", "v_or3_b32", "v_xad_u32", "v_bfi_b32", "v_lshl_add_u32", "v_lshl_or_b32",
+              "v_and_or_b32", "v_lshlrev_b32", "v_lshrrev_b32", "v_alignbyte_b32", "v_perm_b32"}
+_MODIFIER_OK = re.compile(r"^bitop3:0x[0-9a-fA-F]+$")
+
+
+def _valu_base(op):
+    return op.replace("_e32", "").replace("_e64", "")
+
+
+def _safe_valu(line):
+    """(op, dst, [sources]) of a VALU the schedule may move, or a ValueError naming why it may not."""
+    m = re.match(r"\s+(v_\w+)\s+(.*)$", line)
+    if not m:
+        raise ValueError(f"not a VALU: {line!r}")
+    op, rest = m.group(1), m.group(2)
+    if _valu_base(op) not in SCHED_VALU:
+        raise ValueError(f"VALU outside the schedulable set (second destination, implicit operand, transcendental or "
+                         f"unknown): {line!r}")
+    parts = [p.strip() for p in rest.split(",")]
+    last = parts[-1].split()
+    parts[-1] = last[0]
+    for mod in last[1:]:
+        if not (_valu_base(op) == "v_bitop3_b32" and _MODIFIER_OK.match(mod)):
+            raise ValueError(f"VALU modifier the schedule does not model ({mod}): {line!r}")
+    if not re.fullmatch(r"v\d+", parts[0]):
+        raise ValueError(f"VALU destination is not one VGPR: {line!r}")
+    for t in parts[1:]:
+        if not (re.fullmatch(r"[vs]\d+", t) or re.fullmatch(r"-?(0x[0-9a-fA-F]+|\d+)", t)):
+            raise ValueError(f"VALU operand the schedule does not model ({t}): {line!r}")
+    return op, parts[0], parts[1:]
+
 
 def _defs_uses(line):
-    """(op, defs, uses) of one loop-body instruction; None for a line that is not an instruction."""
+    """(op, defs, uses) of one loop-body instruction; None for a line that is not an instruction.  Raises ValueError
+    for anything the list schedule cannot prove safe to move (see SCHED_VALU): the pass then fails the build."""
     m = re.match(r"\s+([vs]_\w+)\s*(.*)", line)
     if not m:
         return None
     op = m.group(1)
+    if op.startswith("v_"):
+        _, dst, srcs = _safe_valu(line)
+        return op, {dst}, {t for t in srcs if re.fullmatch(r"[vs]\d+", t)}
     toks = [t.strip().split()[0] for t in m.group(2).split(",") if t.strip()]
     regs = [t if _REG.match(t) else None for t in toks]
-    if op.startswith("v_"):
-        if not regs or regs[0] is None or not regs[0].startswith("v"):
-            raise ValueError(f"unexpected VALU form: {line!r}")
-        return op, {regs[0]}, {r for r in regs[1:] if r}
     if op.startswith("s_cmp"):
         return op, {"scc"}, {r for r in regs if r}
     if op in ("s_add_i32", "s_sub_i32", "s_add_u32", "s_sub_u32"):
         return op, {regs[0], "scc"}, {r for r in regs[1:] if r}
     raise ValueError(f"unexpected instruction in the loop body: {line!r}")
+
+
+def drop_asm_nops(body):
+    """`asmnop`: LLVM puts an `s_nop 0` after every inline-asm block, whose contents it cannot see.  It is dropped only
+    where that is provably dead: the block holds only schedulable VALUs (one VGPR out, VGPR / SGPR / constant in) and
+    the next instruction is a schedulable VALU reading VGPRs and constants only.  Elsewhere it stays."""
+    out = []
+    for k, l in enumerate(body):
+        if l.strip() == "s_nop 0" and k and body[k - 1].strip() == ";;#ASMEND":
+            j = k - 2
+            block = []
+            while j >= 0 and body[j].strip() != ";;#ASMSTART":
+                if body[j].strip() and not body[j].strip().startswith(";"):
+                    block.append(body[j])
+                j -= 1
+            nxt = next((x for x in body[k + 1:] if x.strip() and not x.strip().startswith(";")), None)
+
+            def vgpr_only_valu(x):
+                try:
+                    _, _, srcs = _safe_valu(x)
+                except ValueError:
+                    return False
+                return not any(re.fullmatch(r"s\d+", t) for t in srcs)
+
+            def safe(x):
+                try:
+                    _safe_valu(x)
+                    return True
+                except ValueError:
+                    return False
+            if j >= 0 and block and all(safe(b) for b in block) and nxt is not None and vgpr_only_valu(nxt):
+                continue
+        out.append(l)
+    return out
 
 
 def reschedule(body, dmin, alt, group=False, orig=False):
@@ -290,15 +365,10 @@ def nopify(lines, kernel, rules):
             arg = r.split("=", 1)[1].split(":")
             body = lines[h + 1:e]
             if "asmnop" in arg[1:]:
-                # LLVM puts an `s_nop 0` after an inline-asm block it cannot see into; after the loop's
-                # v_bitop3_b32 blocks (VGPR in, VGPR out, no hazard between VALU ops) it is dead weight
-                body = [l for k, l in enumerate(body)
-                        if not (l.strip() == "s_nop 0" and k and body[k - 1].strip() == ";;#ASMEND")]
-            try:
-                body = reschedule(body, int(arg[0]), "alt" in arg[1:], "group" in arg[1:], "orig" in arg[1:])
-            except ValueError as err:  # e.g. a hazard s_nop of another compiler: keep its order, spacers still apply
-                sys.stderr.write(f"issue_pass: {kernel}: {r} skipped ({err})\n")
-                continue
+                body = drop_asm_nops(body)
+            # fail closed: an instruction the schedule cannot model raises here and stops the build (ISSUE_RULE=none
+            # builds the compiler's schedule unchanged)
+            body = reschedule(body, int(arg[0]), "alt" in arg[1:], "group" in arg[1:], "orig" in arg[1:])
             if "bank" in arg[1:]:
                 start = next(i for i, l in enumerate(lines) if l.startswith(kernel + ":"))
                 end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
@@ -358,5 +428,10 @@ if __name__ == "__main__":
     lines = open(src).read().split("\n")
     if rules != ["none"]:
         for k in kernel.split("+"):  # several kernels may share one .s
-            lines = nopify(lines, k, rules)
+            try:
+                lines = nopify(lines, k, rules)
+            except ValueError as err:
+                sys.stderr.write(f"issue_pass: {k}: {err}\nissue_pass: refusing to schedule this loop; fix the pass "
+                                 f"or build with ISSUE_RULE=none\n")
+                sys.exit(1)
     open(dst, "w").write("\n".join(lines))

@@ -3,7 +3,10 @@ register file, in a small interpreter of the loop's VALU ops. After one pass thr
 match. That holds for the schedule (same instructions, dependences kept) and for the bank renaming (a renamed value
 lives in a register the body writes again before reading it).
 
-    python3 tools/issue_equiv.py build/pbkdf2/pbkdf2_gfx950.s k_pbkdf2_gfx950_q RULES [trials]
+    python3 tools/issue_equiv.py build/pbkdf2/pbkdf2_gfx950.s KERNEL[+KERNEL...] RULES [trials]
+
+`make` runs it on every kernel the pass schedules (build/pbkdf2/issue_equiv.ok): the library is not linked unless
+the scheduled loops compute what the compiler's do.
 """
 import random
 import re
@@ -77,6 +80,11 @@ def check(path, kernel, rules, trials=3):
 
 
 if __name__ == "__main__":
-    ok, bad = check(sys.argv[1], sys.argv[2], sys.argv[3].split(","), int(sys.argv[4]) if len(sys.argv) > 4 else 3)
-    print("equal" if ok else f"DIFFERENT: {sorted(bad)[:10]}")
-    sys.exit(0 if ok else 1)
+    # kernels "+"-separated (the Makefile checks every kernel the pass scheduled); exit 1 on any difference
+    trials = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+    failed = False
+    for kern in sys.argv[2].split("+"):
+        ok, bad = check(sys.argv[1], kern, sys.argv[3].split(","), trials)
+        print(f"issue_equiv: {kern}: " + ("equal" if ok else f"DIFFERENT: {sorted(bad)[:10]}"))
+        failed |= not ok
+    sys.exit(1 if failed else 0)
