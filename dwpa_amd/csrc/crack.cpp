@@ -324,7 +324,9 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
         stop_all();
     };
     std::vector<std::thread> th;
-    if (rc >= 0)
+    // A worker thread that cannot start (std::system_error, e.g. under RLIMIT_NPROC) stops the ones that did and
+    // fails the call; the vector never unwinds with joinable threads in it.
+    if (rc >= 0) try {
         for (size_t k = 0; k < G; k++) {
             th.emplace_back([&, k] {  // stager
                 DevWork& w = *work[k];
@@ -385,6 +387,9 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
                 }
             });
         }
+    } catch (...) {
+        fail(DWPA_E_NOMEM);
+    }
     for (auto& t : th) t.join();
     source.finish();
     const bool ioerr = items.io_error();
@@ -464,6 +469,13 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
     } else if (!(fo = fopen(out_path, "wb"))) {
         return DWPA_E_IO;
     }
+    // The text packer's offsets and totals are 32-bit: one word's candidates (nr of them, at most TEXT_MAX bytes each
+    // as $HEX[..]) must fit 4 GiB, which bounds a rules file here to ~8.27M rules (bestWPA.rule has 145).
+    constexpr size_t TEXT_MAX = 5 + 2 * (size_t)RP_PASSWORD_SIZE + 2;
+    if (rs.size() > (size_t)UINT32_MAX / TEXT_MAX) {
+        fprintf(stderr, "[dwpa] %zu rules: more than the %zu one expansion packs\n", rs.size(), (size_t)UINT32_MAX / TEXT_MAX);
+        return DWPA_E_RULE;
+    }
     DevRules dr;
     rc = rules_upload(device, rs, &dr);
     const size_t nr = rs.size();
@@ -481,10 +493,10 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
         size_t words = 0;  // words of the sub-batch
         bool busy = false;
         int grow(size_t want) {  // device text buffer and its pinned host mirror, both `want` bytes
-            if (h_text) (void)hipHostFree(h_text);
+            pinned_free(h_text, h_cap);
             h_text = nullptr;
             h_cap = 0;
-            if (text.ensure(want) || hipHostMalloc((void**)&h_text, want) != hipSuccess) return DWPA_E_NOMEM;
+            if (text.ensure(want) || pinned_alloc((void**)&h_text, want) < 0) return DWPA_E_NOMEM;
             h_cap = want;
             return 0;
         }
@@ -493,7 +505,7 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
         if (rc < 0) break;
         if (S.out.ensure(ncap * 256) || S.len.ensure(ncap * 4) || S.tlen.ensure(ncap * 4) ||
             S.off.ensure((wpb + 1) * 8) || S.bsum.ensure(nblk * 4) || S.bcnt.ensure(nblk * 4) || S.tot.ensure(8) ||
-            S.grow(ncap * 24) || hipHostMalloc((void**)&S.h_tot, 8) != hipSuccess)
+            S.grow(ncap * 24) || pinned_alloc((void**)&S.h_tot, 8) < 0)
             rc = DWPA_E_NOMEM;
         else if (hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking) != hipSuccess ||
                  hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess ||
@@ -575,8 +587,8 @@ static int rules_expand_file_impl(int device, const char* rules_file, const char
     for (Set& S : set) {
         if (S.s) (void)hipStreamSynchronize(S.s);
         for (DevBuf* b : {&S.off, &S.bytes, &S.out, &S.len, &S.tlen, &S.bsum, &S.bcnt, &S.tot, &S.text}) b->release();
-        if (S.h_text) (void)hipHostFree(S.h_text);
-        if (S.h_tot) (void)hipHostFree(S.h_tot);
+        pinned_free(S.h_text, S.h_cap);
+        pinned_free(S.h_tot, 8);
         if (S.done) (void)hipEventDestroy(S.done);
         if (S.up) (void)hipEventDestroy(S.up);
         if (S.s) (void)hipStreamDestroy(S.s);

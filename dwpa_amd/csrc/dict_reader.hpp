@@ -262,15 +262,24 @@ class BlockInflater {
         gzclose(gz);
         return ok;
     }
+    // The inflater thread.  No exception leaves it (that would terminate the caller's process): one that a file
+    // raises (std::bad_alloc, a thread that cannot start) ends the stream as failed, and the reader reports an I/O
+    // error for the call.
     void run() {
-        bool all = true;
-        for (const std::string& path : paths_)
-            if (!file(path) || cancelled()) {
-                all = false;
-                break;
-            }
+        bool all = true, failed = false;
+        try {
+            for (const std::string& path : paths_)
+                if (!file(path) || cancelled()) {
+                    all = false;
+                    break;
+                }
+        } catch (...) {
+            all = false;
+            failed = true;
+        }
         std::lock_guard<std::mutex> lk(mu_);
         complete_ = all && !cancelled();
+        failed_ = failed;
         done_ = true;
         cv_.notify_all();
     }
@@ -282,7 +291,14 @@ class BlockInflater {
     std::condition_variable cv_;
     std::deque<Block> q_;
     std::vector<std::vector<uint8_t>> free_;
-    bool stop_ = false, done_ = false, complete_ = false;
+    bool stop_ = false, done_ = false, complete_ = false, failed_ = false;
+
+  public:
+    // The inflater thread failed (an exception inside it); valid once next() has returned false.
+    bool failed() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return failed_;
+    }
 };
 
 // Dictionary reader: plain or gzip (zlib reads both), one word per line, "\n" or "\r\n", $HEX[] decoded.  Lines
@@ -309,6 +325,10 @@ class DictReader {
                 }
                 if (!src_.next(blk_)) {
                     finished_ = true;
+                    if (src_.failed()) {
+                        err = true;
+                        return false;
+                    }
                     break;
                 }
                 if (blk_.err) { err = true; return false; }
@@ -485,12 +505,17 @@ class ChunkSource {
         const size_t T = std::max<size_t>(1, std::min<size_t>(paths.size(), 4));
         cap_ = T + 1;
         live_ = T;
-        for (size_t t = 0; t < T; t++) {
-            std::vector<size_t> mine;
-            for (size_t i = t; i < paths.size(); i += T) mine.push_back(i);
-            workers_.emplace_back([this, paths, mine, first_words, max_words, T] {
-                work(paths, mine, first_words, std::max<size_t>(first_words, max_words / T));
-            });
+        try {
+            for (size_t t = 0; t < T; t++) {
+                std::vector<size_t> mine;
+                for (size_t i = t; i < paths.size(); i += T) mine.push_back(i);
+                workers_.emplace_back([this, paths, mine, first_words, max_words, T] {
+                    work(paths, mine, first_words, std::max<size_t>(first_words, max_words / T));
+                });
+            }
+        } catch (...) {  // a reader thread that cannot start: stop and join the started ones, then report it
+            finish();
+            throw;
         }
     }
     ~ChunkSource() { finish(); }
@@ -551,8 +576,27 @@ class ChunkSource {
         cv_.notify_all();
         return true;
     }
+    // A reader thread.  No exception leaves it (std::terminate would end the caller's process): one raised while
+    // reading (std::bad_alloc) fails the call like an I/O error.
     void work(const std::vector<std::string>& paths, const std::vector<size_t>& mine, size_t words,
               size_t max_words) {
+        bool err = false;
+        try {
+            err = read_files(paths, mine, words, max_words);
+        } catch (...) {
+            err = true;
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        err_ = err_ || err;
+        live_--;
+        cv_.notify_all();
+    }
+    // A chunk's byte capacity is reserved from the previous chunk's bytes per word (growing fresh 10-100 MB vectors
+    // cost the crack path half its line-cutting rate), at most this much: a file of 1 MiB lines would otherwise ask
+    // for words x 1 MiB.
+    static constexpr size_t RESERVE_MAX = (size_t)256 << 20;
+    bool read_files(const std::vector<std::string>& paths, const std::vector<size_t>& mine, size_t words,
+                    size_t max_words) {
         DictCache& cache = DictCache::get();
         bool err = false;
         for (const size_t fi : mine) {
@@ -573,7 +617,7 @@ class ChunkSource {
             for (;;) {
                 auto c = std::make_shared<Chunk>();
                 c->off.reserve(words + 1);
-                c->bytes.reserve(words * (per_word + per_word / 8) + 64);
+                c->bytes.reserve(std::min(words * (per_word + per_word / 8) + 64, RESERVE_MAX));
                 const bool have = reader.next(*c, words, (size_t)1 << 31, err, &cancel_);
                 if (c->words()) per_word = c->bytes.size() / c->words() + 1;
                 words = std::min(max_words, 2 * words);
@@ -595,10 +639,7 @@ class ChunkSource {
             if (whole && !err && !reader.damaged() && reader.complete() && !cancel_.load())
                 cache.put(key, std::move(keep));
         }
-        std::lock_guard<std::mutex> lk(mu_);
-        err_ = err_ || err;
-        live_--;
-        cv_.notify_all();
+        return err;
     }
     std::mutex mu_;
     std::condition_variable cv_;

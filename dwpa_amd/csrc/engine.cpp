@@ -85,6 +85,20 @@ void DevBuf::release() {
     n = 0;
 }
 
+int pinned_alloc(void** p, size_t bytes) {
+    if (hipHostMalloc(p, bytes, hipHostMallocDefault) != hipSuccess) {
+        *p = nullptr;
+        return DWPA_E_NOMEM;
+    }
+    g_pinned_bytes += bytes;
+    return 0;
+}
+void pinned_free(void* p, size_t bytes) {
+    if (!p) return;
+    (void)hipHostFree(p);
+    g_pinned_bytes -= bytes;
+}
+
 // Pinned host staging (hipHostMalloc): uploads from it are plain DMA, unlike pageable copies, which HIP stages
 // through its own buffers on the calling thread.  One arena per device, carved per call; the caller synchronises
 // the stream before the arena is reused.

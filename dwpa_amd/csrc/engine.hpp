@@ -68,6 +68,10 @@ HostCost host_cost(const dwpa_job* jobs, size_t njobs);
 int host_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs, dwpa_check_stats& stats);
 int host_pbkdf2(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out);
 
+// Pinned host memory (hipHostMalloc) counted in dwpa_resource_stats.pinned_host_bytes; free with the same size.
+int pinned_alloc(void** p, size_t bytes);
+void pinned_free(void* p, size_t bytes);
+
 int engine_init();
 // Rule-file loader mode of the process: dwpa_init's cfg->rule_mode when given, else DWPA_RULE_MODE=full|hashcat
 // from the environment, else DWPA_RULES_HASHCAT.  Host only (no device needed).

@@ -95,19 +95,27 @@ class ParallelGunzip {
         data_ = (const uint8_t*)area;
         nchunks_ = (n + chunk_ - 1) / chunk_;
         jobs_.resize(nchunks_);
-        loader_ = std::thread([this, fd, area] { load(fd, (uint8_t*)area); });
-        for (unsigned t = 0; t < nthreads_; t++) pool_.emplace_back([this] { worker(); });
+        try {
+            loader_ = std::thread([this, fd, area] { load(fd, (uint8_t*)area); });
+            for (unsigned t = 0; t < nthreads_; t++) pool_.emplace_back([this] { worker(); });
+        } catch (...) {  // a thread that cannot start: stop and join the ones that did, then report it
+            shutdown();
+            throw;
+        }
     }
-    ~ParallelGunzip() {
+    ~ParallelGunzip() { shutdown(); }
+    void shutdown() {
         quit_flag_.store(true, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> lk(mu_);
             quit_ = true;
         }
         cv_.notify_all();
-        for (auto& t : pool_) t.join();
+        for (auto& t : pool_)
+            if (t.joinable()) t.join();
         if (loader_.joinable()) loader_.join();
         if (data_) munmap((void*)data_, maplen_);
+        data_ = nullptr;
     }
 
     // The loader: the file in order, LOAD_STEP bytes per pread, publishing how far it got (the ThreadSanitizer build
@@ -197,8 +205,22 @@ class ParallelGunzip {
         return NONE;
     }
 
-    // chunk j from bit `start` (0 = the file's gzip header) to bit `stop` (NONE = the end of the stream)
+    // chunk j from bit `start` (0 = the file's gzip header) to bit `stop` (NONE = the end of the stream).  An
+    // allocation that fails ends the chunk with an error: go() then hands the rest of the file to gzread.
     void decode(size_t j, uint64_t start, uint64_t stop) {
+        try {
+            decode_chunk(j, start, stop);
+        } catch (...) {
+            Job& J = jobs_[j];
+            J.err = "out of memory in the parallel inflate";
+            J.pieces.clear();
+            J.trailers.clear();
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        jobs_[j].decoded = true;
+        done_cv_.notify_all();
+    }
+    void decode_chunk(size_t j, uint64_t start, uint64_t stop) {
         need(stop == NONE ? n_ : stop / 8 + 2 * chunk_);
         Job& J = jobs_[j];
         GzipDecoder dec(data_, n_, true);
@@ -236,9 +258,6 @@ class ParallelGunzip {
             }
         }
         J.trailers = dec.trailers();
-        std::lock_guard<std::mutex> lk(mu_);
-        J.decoded = true;
-        done_cv_.notify_all();
     }
 
     uint64_t wait_start(size_t j) {
@@ -262,7 +281,12 @@ class ParallelGunzip {
             for (; next_find < nchunks_ && next_find <= upto; next_find++) {
                 const size_t j = next_find;
                 submit([this, j] {
-                    const uint64_t s = find(j);
+                    uint64_t s;
+                    try {
+                        s = find(j);
+                    } catch (...) {  // no memory for the probe: no boundary, the previous chunk decodes through
+                        s = NONE;
+                    }
                     std::lock_guard<std::mutex> lk(mu_);
                     jobs_[j].start = s;
                     jobs_[j].found_done = true;

@@ -186,10 +186,12 @@ __global__ __launch_bounds__(256) void k_text_pack(const uint8_t* __restrict__ o
 #pragma unroll 1
     for (int j = 0; j < 4; j++) {
         const uint32_t c = base + 4 * threadIdx.x + j;
-        if (!v[j] || (uint64_t)pos + v[j] > cap) continue;
+        const uint32_t at = pos;
+        pos += v[j];  // advanced whether or not this candidate is written: the next one's offset depends on it
+        if (!v[j] || (uint64_t)at + v[j] > cap) continue;
         const uint32_t len = out_len[c];
         const uint8_t* p = out + (size_t)c * RP_PASSWORD_SIZE;
-        uint8_t* d = text + pos;
+        uint8_t* d = text + at;
         if (v[j] == len + 1) {
             for (uint32_t k = 0; k < len; k++) d[k] = p[k];
             d[len] = '\n';
@@ -202,7 +204,6 @@ __global__ __launch_bounds__(256) void k_text_pack(const uint8_t* __restrict__ o
             d[5 + 2 * len] = ']';
             d[6 + 2 * len] = '\n';
         }
-        pos += v[j];
     }
 }
 

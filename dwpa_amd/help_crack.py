@@ -324,6 +324,12 @@ def install(helpcrack_cls, device: int = 0):
     * the module's ``subprocess`` becomes a SubprocessShim, so the ``hashcat --stdout`` expansions of
       ``expandcracked`` (:508) and ``prepare_dicts`` (:575) run on the GPU (``device``) unchanged.
 
+    Rule files (the server's ``rules``, :445-447, and the ``-r`` of both expansions) load as hashcat's ``-r`` does by
+    default: a line using a reject function (``< > _ ! / ( ) = % Q``) or a memory function (``M 4 6 X``) is skipped
+    and counted.  Which lines hashcat -r skips is third-party behaviour no reference file pins (parity unpinned);
+    set ``DWPA_RULE_MODE=full`` in the environment (or ``rule_mode=DWPA_RULES_FULL``) if your rules rely on those
+    functions and should run them.
+
     Idempotent.  Returns the class."""
     module = sys.modules.get(helpcrack_cls.__module__)
 

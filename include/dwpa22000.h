@@ -69,7 +69,10 @@ extern "C" {
                                   environment, else DWPA_RULES_HASHCAT                                            */
 #define DWPA_RULES_HASHCAT 1   /* hashcat's -r loader: a line using a reject function (< > _ ! / ( ) = % Q) or a memory
                                   function (M 4 6 X) is skipped and counted like an invalid one -- those work only
-                                  with -j/-k -- so the candidates are exactly the ones hashcat -r tries (default)  */
+                                  with -j/-k -- so the candidates are the ones hashcat -r tries (default).  Parity
+                                  unpinned: hashcat is not in the reference, no reference file shows which lines -r
+                                  skips; this follows hashcat's documentation (oracle/rules.py).  Rules relying on
+                                  those functions: DWPA_RULES_FULL / DWPA_RULE_MODE=full                          */
 #define DWPA_RULES_FULL 2      /* every line of the whole rule language runs, reject and memory functions included (a
                                   superset of hashcat -r's candidates)                                             */
 

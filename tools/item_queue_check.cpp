@@ -9,6 +9,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <string>
@@ -34,8 +35,10 @@ int main(int argc, char** argv) {
     std::vector<double> done_ms(W, 0);
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
+    std::atomic<bool> tool_oom{false};
     for (size_t w = 0; w < W; w++)
         th.emplace_back([&, w] {
+          try {
             dwpa::WorkItem it;
             while (items.next(it)) {
                 const size_t n = it.e - it.b;
@@ -51,13 +54,16 @@ int main(int argc, char** argv) {
             }
             std::lock_guard<std::mutex> lk(mu);
             done_ms[w] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+          } catch (const std::bad_alloc&) {  // this tool's own copies of the words; the library's threads catch theirs
+            tool_oom = true;
+          }
         });
     for (auto& t : th) t.join();
     size_t total = seen.size();
     std::sort(seen.begin(), seen.end());
     const bool unique = std::adjacent_find(seen.begin(), seen.end()) == seen.end();
-    printf("{\"words_total\": %zu, \"unique\": %s, \"io_error\": %s, \"workers\": [", total, unique ? "true" : "false",
-           items.io_error() ? "true" : "false");
+    printf("{\"words_total\": %zu, \"unique\": %s, \"io_error\": %s, \"tool_oom\": %s, \"workers\": [", total,
+           unique ? "true" : "false", items.io_error() ? "true" : "false", tool_oom.load() ? "true" : "false");
     for (size_t w = 0; w < W; w++)
         printf("%s{\"words\": %zu, \"items\": %zu, \"largest\": %zu, \"done_ms\": %.2f}", w ? ", " : "", words[w],
                nitems[w], largest[w], done_ms[w]);
