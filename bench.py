@@ -533,13 +533,15 @@ def check_device(local: int, rank: int) -> int:
 
 def main():
     args = parse()
-    if os.environ.get("WORLD_SIZE") is None and (args.gpus or 1) > 1:
+    if args.workload == "c2files":  # the client's node mode: one process over N devices, never rank processes
+        os.environ.setdefault("DWPA_DICT_CACHE_MB", "0")
+    elif os.environ.get("WORLD_SIZE") is None and (args.gpus or 1) > 1:
         sys.exit(spawn_ranks(args))
     quiet_stdout()
     if args.workload == "c1cold":  # before anything touches the GPU: the parent never does
         return {"parent": main_cold, "worker": cold_worker, "context": cold_context}[args.cold_role](args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus is not None and args.gpus != world:
+    if args.gpus is not None and args.gpus != world and not (args.workload == "c2files" and world == 1):
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.scaling == "strong" and args.workload != "c4":
         sys.exit("bench.py: --scaling strong is defined for --workload c4 (the numeric keyspace)")
@@ -705,6 +707,8 @@ def main_dry(args, world, rank):
     scan (weak: (its own shard r, batch) of every timed step; strong c4: its contiguous keyspace
     range), then the gloo barrier and the max/sum reductions run as in a measured run; rank 0 prints the coverage
     of every rank.  tests/test_bench_spawn.py checks N ranks and disjoint coverage through `--gpus N`."""
+    if args.workload == "c2files":
+        return dry_node(args)
     import torch.distributed as dist
     from dwpa_amd.shard import reduce_timing, strong_batches, weak_units
     if os.environ.get("DWPA_TEST_RANK_SLEEP"):  # tests/test_bench_spawn.py: keep the ranks alive while it kills the parent
@@ -736,6 +740,42 @@ def main_dry(args, world, rank):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def dry_node(args):
+    """--workload c2files --dry-run: the node mode's work distribution with no GPU.  One process (no ranks); a scaled
+    C2 gzip dictionary (at most 2M words) goes through the library's own reader and item queue (dict_reader.hpp:
+    ChunkSource + ItemQueue, in tools/bin/item_queue_check) to N x DWPA_CRACK_SHARDS_PER_DEVICE workers that hold
+    each item for a time proportional to its size, with crack.cpp's item sizes for a batch scaled to the dictionary.
+    Reports every worker's words and items and whether every word went out exactly once."""
+    import copy
+    import subprocess
+    import tempfile
+    ngpu = args.gpus or 1
+    spd = int(os.environ.get("DWPA_CRACK_SHARDS_PER_DEVICE", "1") or 1)
+    W = ngpu * spd
+    a = copy.copy(args)
+    a.dict_words = min(args.dict_words, 2_000_000)
+    tmp = tempfile.mkdtemp(prefix="dwpa_node_dry_")
+    path, _, _, _, _ = _c2_gz_dictionary(a, tmp)
+    B = max(64, a.dict_words // (16 * W))  # batch scaled so every worker takes several items
+    first = max(1, B // 16)
+    most = min(16 * B, max(first, 2 * B)) if W > 1 else 16 * B  # crack.cpp: items of at most 2 batches when W > 1
+    tool = os.path.join(ROOT, "tools", "bin", "item_queue_check")
+    r = subprocess.run([tool, str(W), str(first), str(most), "200000", path], capture_output=True, text=True,
+                       timeout=300)
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    if r.returncode != 0:
+        raise SystemExit(f"item_queue_check failed: {r.stderr[-1000:]}")
+    q = json.loads(r.stdout)
+    emit({"metric": METRIC, "value": None, "unit": "PMK/s", "n_gpus": ngpu, "steps": args.steps,
+          "warmup": args.warmup, "dry_run": True, "scaling": "weak",
+          "config": {"workload": "c2files", "device_mask": (1 << ngpu) - 1, "workers": W,
+                     "shard_workers_per_device": spd, "dict_words": a.dict_words, "batch_scaled": B,
+                     "items_first_most": [first, most], "parallelism": f"one process, {ngpu} device(s) x {spd} worker(s)"},
+          "words_total": q["words_total"], "every_word_once": q["unique"] and q["words_total"] == a.dict_words,
+          "workers": q["workers"], "pid": os.getpid()})
 
 
 def main_strong(args, world, rank, local):
@@ -1260,22 +1300,12 @@ def main_cold(args):
         sys.exit(3)
 
 
-def main_files(args, world, rank, local):
-    """C2 end to end through the client path (dwpa_crack_files, help_crack.py:765-802): the 100M-word dictionary
-    as a gzip file on local disk, streamed, inflated and $HEX[]-decoded on the host, uploaded chunk by chunk and
-    scanned against the C2 line (hashcat nonce mode, --nonce-error-corrections=8).  The planted PSK is the
-    99,999,000th word, so the run covers the dictionary up to there.  One pass = one step; N>1 runs replicas."""
+def _c2_gz_dictionary(args, tmp):
+    """The C2 dictionary as a gzip file on local disk: args.dict_words words (seed 2; lengths geometric around 10,
+    ~30 % under 8 with --short-words), the planted PSK the 99,999,000th word.  Returns (path, psk, PMKs a pass
+    derives up to the plant = words inside 8..63, gz bytes, seconds to write it)."""
     import gzip
-    import random
-    import tempfile
     import numpy as np
-    import torch.distributed as dist
-    import dwpa_amd
-    from tests import synth as S
-    from dwpa_amd.shard import reduce_timing
-
-    if world > 1:
-        dist.init_process_group("gloo")
     n = args.dict_words
     plant = min(PLANT_INDEX, n - 1)
     rng = np.random.default_rng(2)
@@ -1285,104 +1315,26 @@ def main_files(args, world, rank, local):
     text = rng.integers(0x21, 0x7F, int(ends[-1]), dtype=np.uint8)
     text[ends - 1] = 0x0A
     psk = text[int(ends[plant - 1]) if plant else 0:int(ends[plant]) - 1].tobytes()
-    rr = random.Random(1)
-    essid, ap, sta, an, sn = S.random_net(rr, essid_len=10)
-    line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rr)
-    tmp = tempfile.mkdtemp(prefix="dwpa_c2files_")
-    dpath, hpath, opath = (os.path.join(tmp, x) for x in ("dict.txt.gz", "h.hash", "o.key"))
+    path = os.path.join(tmp, "dict.txt.gz")
     t0 = time.perf_counter()
-    with gzip.open(dpath, "wb", compresslevel=1) as f:
+    with gzip.open(path, "wb", compresslevel=1) as f:
         step = 64 << 20
         for o in range(0, len(text), step):
             f.write(text[o:o + step].tobytes())
-    gz_s = time.perf_counter() - t0
-    gz_bytes = os.path.getsize(dpath)
-    reader = None
-    tool = os.path.join(ROOT, "tools", "bin", "inflate_bench")
-    if rank == 0 and os.path.exists(tool):
-        # crack_files' own dictionary reader on this host (dict_reader.hpp): how many GPUs one gz stream feeds
-        import subprocess
-        r = subprocess.run([tool, dpath], capture_output=True, text=True, timeout=300)
-        if r.returncode == 0:
-            reader = json.loads(r.stdout)
-    del text
-    with open(hpath, "wb") as f:
-        f.write(line + b"\n")
-    cracked = True
-    times, all_passes = [], []
-    for rep in range(args.warmup + args.steps):
-        if os.path.exists(opath):
-            os.remove(opath)
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        rc = dwpa_amd.crack_files(hpath, [dpath], None, 8, opath, device_mask=1 << local, batch=args.batch)
-        el = time.perf_counter() - t0
-        st = dwpa_amd.m22000.crack_stats()
-        reported = st["candidates"]
-        rules_loaded = (st["rules"], st["rules_skipped"])
-        all_passes.append(round(el, 3))
-        if rep >= args.warmup:
-            times.append(el)
-        recs = open(opath, "rb").read().strip().split(b"\n") if os.path.exists(opath) else []
-        cracked &= rc == 0 and len(recs) == 1 and recs[0].endswith(b":" + psk)
-    elapsed = sum(times) / len(times)
-    words = int(np.count_nonzero(lens[:plant + 1] >= 8))  # PMKs derived: words inside the 8..63 filter
-    if world > 1:
-        from dwpa_amd.shard import all_ranks
-        cracked = all_ranks(dist, cracked)
-        elapsed, total = reduce_timing(dist, elapsed, float(words))
-    else:
-        total = float(words)
-    if rank == 0:
-        emit({
-            "metric": METRIC, "value": round(total / elapsed, 1), "unit": "PMK/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-            "config": {"workload": "C2 via dwpa_crack_files: 100M-word gzip dictionary on local disk (streamed, "
-                                   "inflated and uploaded per chunk), one EAPOL keyver-2 line, hashcat NC mode 8"
-                                   + (", ~30 % of the words shorter than 8" if args.short_words else ""),
-                       "dict_words": n, "gz_bytes": gz_bytes, "gz_write_s": round(gz_s, 2),
-                       "words_scanned_per_pass": words, "candidates_reported_by_library": reported,
-                       "batch": args.batch,
-                       "parallelism": f"replicas x{world}",
-                       "dict_cache": "passes after the first replay the decoded dictionary from the library's "
-                                     "DictCache (no inflate)" if os.environ.get("DWPA_DICT_CACHE_MB", "") != "0"
-                                     else "off"},
-            "pass_s": all_passes,
-            "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked), "reader": reader})
-    for x in (dpath, hpath, opath):
-        if os.path.exists(x):
-            os.remove(x)
-    os.rmdir(tmp)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    if rank == 0 and not cracked:
-        sys.exit(3)
+    return path, psk, int(np.count_nonzero(lens[:plant + 1] >= 8)), os.path.getsize(path), time.perf_counter() - t0
 
 
-def main_files_rules(args, world, rank, local):
-    """The client's rule pass through dwpa_crack_files (help_crack.py:929-933: `-S -r <rules>` over the work
-    unit's dictionaries; SURVEY.md 8(a) A12, 8(f) row 3): a gzip dictionary of --rule-words base words (6..16
-    printable bytes) on local disk x the WPA rule set (dwpa_amd/rulesets.py, 148 rules of bestWPA.rule's ops) in a
-    rules file, amplified on the GPU, one EAPOL keyver-2 line in hashcat NC mode 8.  The planted PSK is one rule's
-    output of the 1000th-last word, so a pass covers the dictionary up to there.  PMKs counted = candidates inside
-    the 8..63 filter: every rule of the set changes a word's length as a function of that length only, so the
-    count is sum over word lengths of (words of that length) x (rules whose output length is in 8..63), taken from
-    the library's own rule expansion of one word per length.  One pass = one step; N>1 runs replicas."""
+def _rule_pass_inputs(args, tmp, local):
+    """The client's rule pass (help_crack.py:929-933, `-S -r <rules>`): a gzip dictionary of args.rule_words base
+    words (6..16 printable bytes, seed 6) and a rules file (dwpa_amd/rulesets.py: the WPA set, 148 rules of
+    bestWPA.rule's ops, or the server set), the planted PSK one rule's output of the 1000th-last word.  Candidates
+    counted = those inside the 8..63 filter up to the plant: every rule of the WPA set changes a word's length as a
+    function of that length only, so the count is sum over lengths of (words of that length) x (rules whose output
+    length is in 8..63), from the library's own expansion of one word per length.  Returns a dict."""
     import gzip
-    import random
-    import tempfile
     import numpy as np
-    import torch.distributed as dist
     import dwpa_amd
-    from tests import synth as S
     from dwpa_amd.rulesets import server_rules, wpa_rules
-    from dwpa_amd.shard import reduce_timing
-
-    if world > 1:
-        dist.init_process_group("gloo")
     n = max(2000, args.rule_words)
     rules = wpa_rules() if args.rules_set == "wpa" else server_rules()
     rules_text = "\n".join(rules)
@@ -1402,23 +1354,150 @@ def main_files_rules(args, world, rank, local):
     # wpa: a rule in the middle of the set; server: the last kept one (of the added part: a memory / reject line
     # with --rule-mode full, a byte-arithmetic line under hashcat's loader)
     plant_rule = good[len(good) // 2] if args.rules_set == "wpa" else good[-1]
-    psk = row[plant_rule]
-    # candidates inside the filter per base-word length (rule output lengths depend on the input length only)
     reps = [bytes(b"abcdefghijklmnop"[:L]) for L in range(6, 17)]
     per_len = {L: sum(1 for c in r if c is not None and 8 <= len(c) <= 63)
                for L, r in zip(range(6, 17), dwpa_amd.rules_expand(rules_text, reps, device=local))}
     counts = np.bincount(lens[:plant_word + 1], minlength=17)
-    cands = int(sum(int(counts[L]) * per_len[L] for L in range(6, 17)))
+    dpath, rpath = os.path.join(tmp, "rules_dict.txt.gz"), os.path.join(tmp, "wpa.rule")
+    with gzip.open(dpath, "wb", compresslevel=6) as f:
+        f.write(text.tobytes())
+    with open(rpath, "w") as f:
+        f.write(rules_text + "\n")
+    return {"dict": dpath, "rules_file": rpath, "rules": rules, "words": n, "psk": row[plant_rule],
+            "plant": [plant_word, plant_rule], "cands": int(sum(int(counts[L]) * per_len[L] for L in range(6, 17)))}
+
+
+def main_files(args, world, rank, local):
+    """The client's own multi-GPU mode: ONE process runs dwpa_crack_files over a device mask of
+    N GPUs, as help_crack's single hashcat process uses every device (help_crack.py:773) -- one host thread pair per
+    device worker, one shared dictionary stream cut into work items by guided self-scheduling, no rank
+    processes.  One step = the work unit's two passes (help_crack.py:923-933):
+      1. the 100M-word C2 dictionary as a gzip file on local disk (streamed, inflated and $HEX[]-decoded on the
+         host, uploaded item by item), one EAPOL keyver-2 line, --nonce-error-corrections=8, up to the planted word;
+      2. the rule pass: a --rule-words gzip dictionary x the WPA rule set (rules file, amplified on the GPU).
+    value = the PMKs of both passes / their wall time (the node figure); each pass is reported with its words,
+    candidates and feed rate, and every device worker with its items, words, candidates, scan time and the time it
+    waited for the shared feed.  hits_verified: each pass's outfile holds exactly the planted record.
+    --gpus N: the mask covers devices 0..N-1 (n_gpus = N).  Under a launcher (WORLD_SIZE = N) rank 0 runs it and the
+    other ranks exit without touching a GPU.  DWPA_CRACK_SHARDS_PER_DEVICE=k runs k workers per device: on a one-GPU
+    box, k = 8 rehearses an 8-GPU node's worker count and feed (not its throughput).  The library's in-process
+    dictionary cache is off for this leg (DWPA_DICT_CACHE_MB=0 unless set): every pass inflates its gzip file, as a
+    client's first pass over a downloaded dictionary does."""
+    import random
+    import tempfile
+    import dwpa_amd
+    from dwpa_amd import _lib as L
+    from dwpa_amd import m22000 as M
+    from tests import synth as S
+
+    ngpu = max(world, args.gpus or 1)
+    if rank != 0:
+        return
+    ndev = dwpa_amd.device_count()
+    if ngpu > ndev:
+        raise SystemExit(f"bench.py --workload c2files: --gpus {ngpu} but {ndev} gfx950 device(s) visible")
+    mask = (1 << ngpu) - 1
+    spd = int(os.environ.get("DWPA_CRACK_SHARDS_PER_DEVICE", "1") or 1)
+    tmp = tempfile.mkdtemp(prefix="dwpa_node_")
+    d1, psk1, pmk1, gz_bytes, gz_s = _c2_gz_dictionary(args, tmp)
+    rp = _rule_pass_inputs(args, tmp, local)
+    rr = random.Random(1)
+    essid, ap, sta, an, sn = S.random_net(rr, essid_len=10)
+    h1, h2 = os.path.join(tmp, "c2.hash"), os.path.join(tmp, "rules.hash")
+    with open(h1, "wb") as f:
+        f.write(S.eapol_line(psk1, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rr) + b"\n")
+    rr2 = random.Random(2)
+    e2, a2, s2, an2, sn2 = S.random_net(rr2, essid_len=10)
+    with open(h2, "wb") as f:
+        f.write(S.eapol_line(rp["psk"], e2, a2, s2, an2, sn2, 2, 3, "LE", mp=0x80, rng=rr2) + b"\n")
+    reader = None
+    tool = os.path.join(ROOT, "tools", "bin", "inflate_bench")
+    if os.path.exists(tool):
+        # the library's dictionary reader alone on this host (dict_reader.hpp): how many devices one gz stream feeds
+        import subprocess
+        r = subprocess.run([tool, d1], capture_output=True, text=True, timeout=300)
+        if r.returncode == 0:
+            reader = json.loads(r.stdout)
+    passes = []
+    ok = True
+    for rep in range(args.warmup + args.steps):
+        step = []
+        for name, hpath, dpath, rules_file, psk, pmks in (("dictionary", h1, d1, None, psk1, pmk1),
+                                                         ("rules", h2, rp["dict"], rp["rules_file"], rp["psk"],
+                                                          rp["cands"])):
+            opath = os.path.join(tmp, name + ".key")
+            if os.path.exists(opath):
+                os.remove(opath)
+            t0 = time.perf_counter()
+            rc = dwpa_amd.crack_files(hpath, [dpath], rules_file, 8, opath, device_mask=mask, batch=args.batch,
+                                      rule_mode=L.DWPA_RULES_FULL if args.rule_mode == "full" else L.DWPA_RULES_HASHCAT)
+            el = time.perf_counter() - t0
+            st, workers = M.crack_stats(), M.crack_worker_stats()
+            recs = open(opath, "rb").read().strip().split(b"\n") if os.path.exists(opath) else []
+            good = rc == 0 and len(recs) == 1 and recs[0].endswith(b":" + psk)
+            ok &= good
+            step.append({"pass": name, "s": el, "pmks": pmks, "words": st["words"], "candidates": st["candidates"],
+                         "cracked_record_ok": good, "workers": workers})
+        passes.append(step)
+    timed = passes[args.warmup:]
+    t = sum(p["s"] for step in timed for p in step) / len(timed)
+    pmks = pmk1 + rp["cands"]
+    last = timed[-1]
+    emit({
+        "metric": METRIC, "value": round(pmks / t, 1), "unit": "PMK/s", "n_gpus": ngpu, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "client node mode: one process, dwpa_crack_files over a mask of the node's devices; "
+                               "per step the C2 pass (100M-word gzip dictionary, one EAPOL keyver-2 line, hashcat NC 8) "
+                               "then the rule pass (gzip dictionary x WPA rules file)",
+                   "device_mask": mask, "shard_workers_per_device": spd, "workers": ngpu * spd,
+                   "rehearsal": (f"{spd} shard workers on one device: an {spd}-GPU node's worker count and shared "
+                                 "feed, not its throughput") if ngpu == 1 and spd > 1 else None,
+                   "dict_words": args.dict_words, "gz_bytes": gz_bytes, "gz_write_s": round(gz_s, 2),
+                   "rule_words": rp["words"], "rules": len(rp["rules"]), "rules_set": args.rules_set,
+                   "rule_mode": args.rule_mode, "batch": args.batch,
+                   "dict_cache": "off (every pass inflates)" if os.environ.get("DWPA_DICT_CACHE_MB") == "0" else "on",
+                   "parallelism": f"one process, {ngpu} device(s) x {spd} worker(s), shared dictionary feed"},
+        "passes": [{"pass": p["pass"], "s": round(p["s"], 3), "pmks": p["pmks"], "pmk_per_s": round(p["pmks"] / p["s"], 1),
+                    "words": p["words"], "words_per_s_feed": round(p["words"] / p["s"], 1),
+                    "candidates_reported_by_library": p["candidates"], "cracked_record_ok": p["cracked_record_ok"],
+                    "workers": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in w.items()}
+                                for w in p["workers"]]} for p in last],
+        "pass_s": [[round(p["s"], 3) for p in step] for step in passes],
+        "roofline": None, "cpu_baseline": None, "hits_verified": bool(ok), "reader": reader})
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    if not ok:
+        sys.exit(3)
+
+
+def main_files_rules(args, world, rank, local):
+    """The client's rule pass through dwpa_crack_files (help_crack.py:929-933: `-S -r <rules>` over the work
+    unit's dictionaries; SURVEY.md 8(a) A12, 8(f) row 3): a gzip dictionary of --rule-words base words (6..16
+    printable bytes) on local disk x the WPA rule set (dwpa_amd/rulesets.py, 148 rules of bestWPA.rule's ops) in a
+    rules file, amplified on the GPU, one EAPOL keyver-2 line in hashcat NC mode 8.  The planted PSK is one rule's
+    output of the 1000th-last word, so a pass covers the dictionary up to there.  PMKs counted = candidates inside
+    the 8..63 filter: every rule of the set changes a word's length as a function of that length only, so the
+    count is sum over word lengths of (words of that length) x (rules whose output length is in 8..63), taken from
+    the library's own rule expansion of one word per length.  One pass = one step; N>1 runs replicas."""
+    import random
+    import tempfile
+    import torch.distributed as dist
+    import dwpa_amd
+    from tests import synth as S
+    from dwpa_amd.shard import reduce_timing
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    tmp = tempfile.mkdtemp(prefix="dwpa_c3files_")
+    rp = _rule_pass_inputs(args, tmp, local)
+    n, rules, psk, cands = rp["words"], rp["rules"], rp["psk"], rp["cands"]
+    dpath, rpath = rp["dict"], rp["rules_file"]
+    plant_word, plant_rule = rp["plant"]
     rr = random.Random(1)
     essid, ap, sta, an, sn = S.random_net(rr, essid_len=10)
     line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", mp=0x80, rng=rr)
-    tmp = tempfile.mkdtemp(prefix="dwpa_c3files_")
-    dpath, rpath, hpath, opath = (os.path.join(tmp, x) for x in ("dict.txt.gz", "wpa.rule", "h.hash", "o.key"))
-    with gzip.open(dpath, "wb", compresslevel=6) as f:
-        f.write(text.tobytes())
-    del text
-    with open(rpath, "w") as f:
-        f.write(rules_text + "\n")
+    hpath, opath = (os.path.join(tmp, x) for x in ("h.hash", "o.key"))
     with open(hpath, "wb") as f:
         f.write(line + b"\n")
     cracked = True
@@ -1468,10 +1547,8 @@ def main_files_rules(args, world, rank, local):
                        "plant": [plant_word, plant_rule]},
             "pass_s": all_passes,
             "roofline": None, "cpu_baseline": None, "hits_verified": bool(cracked)})
-    for x in (dpath, rpath, hpath, opath):
-        if os.path.exists(x):
-            os.remove(x)
-    os.rmdir(tmp)
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -57,6 +57,11 @@ class CrackStats(ctypes.Structure):
                 ("rules_skipped", ctypes.c_uint32), ("rules_rejmem", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
+class CrackWorker(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("items", ctypes.c_uint32), ("words", ctypes.c_uint64),
+                ("candidates", ctypes.c_uint64), ("wait_s", ctypes.c_double), ("scan_s", ctypes.c_double)]
+
+
 class CheckStats(ctypes.Structure):
     _fields_ = [("jobs", ctypes.c_uint32), ("slots", ctypes.c_uint32), ("pmks", ctypes.c_uint32),
                 ("tail_pmks", ctypes.c_uint32), ("tail_waves", ctypes.c_uint32), ("tail_waves_raised", ctypes.c_uint32),
@@ -107,6 +112,8 @@ SIGNATURES = {
     "dwpa_crack_files": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_int,
                           ctypes.c_char_p, ctypes.POINTER(Config)], ctypes.c_int),
     "dwpa_crack_last_stats": ([ctypes.POINTER(CrackStats)], ctypes.c_int),
+    "dwpa_crack_worker_stats": ([ctypes.POINTER(CrackWorker), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)],
+                                ctypes.c_int),
     "dwpa_crack_files_ex": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t, ctypes.c_char_p,
                              ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(Config), ctypes.POINTER(ctypes.c_int32)],
                             ctypes.c_int),

@@ -64,6 +64,7 @@ struct DevWork {
     size_t items = 0, words = 0;    // statistics (DWPA_TRACE, dwpa_crack_last_stats)
     uint64_t cands = 0;             // candidates loaded inside the 8..63 filter (after rules)
     double wait_s = 0;              // scanner time spent waiting for a staged item
+    double scan_s = 0;              // scanner time spent scanning items
     // stager -> scanner hand-over
     std::mutex mu;
     std::condition_variable cv;
@@ -179,8 +180,9 @@ static size_t shards_per_device() {
     return (size_t)std::min<long>(8, std::max<long>(1, k));
 }
 
-// dwpa_crack_last_stats: the calling thread's last crack call
+// dwpa_crack_last_stats / dwpa_crack_worker_stats: the calling thread's last crack call
 static thread_local dwpa_crack_stats g_last_stats;
+static thread_local std::vector<dwpa_crack_worker> g_last_workers;
 static thread_local bool g_have_stats = false;
 
 static bool trace_on() {
@@ -192,6 +194,7 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
                       const char* out_file, const dwpa_config* cfg, int32_t* dict_status) {
     const auto t_call = std::chrono::steady_clock::now();
     g_last_stats = dwpa_crack_stats{};  // an early return reports zeros, never the previous call
+    g_last_workers.clear();
     g_have_stats = true;
     if (dict_status)
         for (size_t i = 0; i < ndicts; i++) dict_status[i] = DWPA_DICT_OK;
@@ -367,7 +370,9 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
                         w.ready.pop_front();
                         it = w.slot_item[slot];
                     }
+                    const auto ts = std::chrono::steady_clock::now();
                     const int r = guarded([&] { return scan_shard(w, sh, *it.chunk, it.b, it.e, rp, slot); });
+                    w.scan_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count();
                     w.items++;
                     w.words += it.e - it.b;
                     {
@@ -428,6 +433,8 @@ static int crack_impl(const char* hash_file, const char* const* dicts, size_t nd
     for (auto& wp : work) {
         g_last_stats.words += wp->words;
         g_last_stats.candidates += wp->cands;
+        g_last_workers.push_back(dwpa_crack_worker{wp->device, (uint32_t)wp->items, (uint64_t)wp->words, wp->cands,
+                                                   wp->wait_s, wp->scan_s});
     }
     g_last_stats.hashes = (uint32_t)sh.valid;
     g_last_stats.cracked = (uint32_t)sh.ncracked;
@@ -623,6 +630,13 @@ int dwpa_crack_files(const char* hash_file, const char* const* dicts, size_t ndi
 int dwpa_crack_last_stats(dwpa_crack_stats* out) {
     if (!out || !dwpa::g_have_stats) return DWPA_E_ARG;
     *out = dwpa::g_last_stats;
+    return 0;
+}
+
+int dwpa_crack_worker_stats(dwpa_crack_worker* out, size_t cap, size_t* n) {
+    if (!n || (!out && cap) || !dwpa::g_have_stats) return DWPA_E_ARG;
+    *n = dwpa::g_last_workers.size();
+    for (size_t i = 0; i < std::min(cap, *n); i++) out[i] = dwpa::g_last_workers[i];
     return 0;
 }
 

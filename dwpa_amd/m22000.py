@@ -285,6 +285,17 @@ def crack_stats():
             "rules_rejmem": st.rules_rejmem}
 
 
+def crack_worker_stats():
+    """dwpa_crack_worker_stats: per shard worker of this thread's last crack call, [{device, items, words,
+    candidates, wait_s, scan_s}] (wait_s: time its scanner waited for the shared dictionary feed)."""
+    lib = L.load()
+    n = ctypes.c_size_t(0)
+    L.check(lib.dwpa_crack_worker_stats(None, 0, ctypes.byref(n)), "crack_worker_stats")
+    arr = (L.CrackWorker * max(1, n.value))()
+    L.check(lib.dwpa_crack_worker_stats(arr, n.value, ctypes.byref(n)), "crack_worker_stats")
+    return [{k: getattr(arr[i], k) for k, _ in L.CrackWorker._fields_} for i in range(n.value)]
+
+
 class Scan:
     """Device-resident scan of one work unit (hashlines grouped by ESSID) -- the client hot loop.
 

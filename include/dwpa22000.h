@@ -266,6 +266,19 @@ typedef struct {
     uint32_t reserved;
 } dwpa_crack_stats;
 int dwpa_crack_last_stats(dwpa_crack_stats *out);
+/* Per shard worker of the calling thread's last dwpa_crack_files(_ex) call (ABI 4): one worker per selected device
+ * (DWPA_CRACK_SHARDS_PER_DEVICE per device), each a stager thread uploading work items and a scanner thread running
+ * them.  wait_s is the scanner's time waiting for a staged item (the shared dictionary feed not keeping up), scan_s its
+ * time scanning.  Copies min(cap, workers) entries, sets *n = workers; returns 0, or DWPA_E_ARG before any call. */
+typedef struct {
+    int32_t device;
+    uint32_t items;            /* work items (contiguous word ranges of the shared feed) scanned */
+    uint64_t words;            /* dictionary words of those items */
+    uint64_t candidates;       /* candidates derived (after the rules, inside the 8..63 filter) */
+    double wait_s;
+    double scan_s;
+} dwpa_crack_worker;
+int dwpa_crack_worker_stats(dwpa_crack_worker *out, size_t cap, size_t *n);
 
 /* hashcat rules (the whole rule language of hashcat >= 6.2.6: every mangling, reject and memory function; one
  * rule per line, '#' comments; semantics in dwpa_amd/csrc/rules.hpp and oracle/rules.py).  The text entry points

@@ -163,3 +163,15 @@ def test_timed_hits_verification():
     assert not bench.verify_timed_hits(W, [plant, plant, {"line": 0, "cand": 7}], batches)[0]  # a false hit
     ok, d = bench.verify_timed_hits(W, [], [0, 1, 2])                               # plant batch not timed
     assert ok and d["timed_plant_scans"] == 0
+
+
+def test_node_mode_dry_run_one_process():
+    """`bench.py --workload c2files --gpus 8` is the client's node mode: one process over a mask
+    of 8 devices, no rank processes.  Its --dry-run drives the library's reader and item queue (ChunkSource +
+    ItemQueue) with 8 workers: every word goes out exactly once and every worker takes a share."""
+    subprocess.run(["make", "-s", "-C", ROOT, "tools/bin/item_queue_check"], check=True)
+    out = _line(_bench("--workload", "c2files", "--gpus", "8", "--dry-run", "--dict-words", "400000"))
+    assert out["n_gpus"] == 8 and out["config"]["device_mask"] == 255 and out["config"]["workers"] == 8
+    assert out["pid"] and out["every_word_once"] and out["words_total"] == 400000
+    words = [w["words"] for w in out["workers"]]
+    assert len(words) == 8 and min(words) > 0 and max(words) < 3 * sum(words) / 8
