@@ -979,7 +979,6 @@ def main_ffi(args, world, rank, local):
             "mismatches": mismatches if args.workload == "c5" else None,
             "window_unix": window,
             "last_call": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in call_stats.items()},
-            "tail_prio": int(os.environ.get("DWPA_TAIL_PRIO", "2")),
             "hits_checked": "every job's result against its planted key's [PSK, NC, endian, PMK] (re-derived by the "
                             "CPU oracle) or False" if args.workload == "c5" else "the planted PSK and its PMK"})
     if world > 1:

@@ -511,34 +511,15 @@ constexpr AesTables make_aes_tables() {
 }
 __constant__ static const AesTables AES_TABLES = make_aes_tables();
 
-// AES-128 encryption over four T-tables in LDS (te4 = Te0..Te3, Te_k = Te0 rotated right by 8k: no rotate per
-// lookup), with the key schedule computed round by round (FIPS-197 5.2) instead of held as rk[44] (40 fewer live
-// registers; 40 more lookups per block).  S-box bytes come out of the T-tables already in place: S[x] is byte 3
-// of Te2/Te3, byte 2 of Te0/Te3, byte 1 of Te0/Te1 and byte 0 of Te1/Te2, so a SubWord is 4 lookups + 3 v_perm.
+// AES-128 encryption for the keyver-3 CMAC, one lane-sliced T-table in LDS, with the key schedule computed round by
+// round (FIPS-197 5.2) instead of held as rk[44] (40 fewer live registers; 40 more lookups per block).
 //
-// Sliced tables (build switch DWPA_KV3_SLICES = S, default 1 = plain): every table holds S interleaved copies,
-// entry x of copy c at word S x + c, and lane l reads copy l % S.  ds_read_b32 banks are (address / 4) mod 32 per
-// 32-lane group, so with S = 16 two lanes can only collide when they share a copy (l and l + 16) and their entries
-// have the same parity: 2-way conflicts at most.  The plain tables put 68 % of the keyver-3 verify's LDS cycles into
-// random-index bank conflicts; S = 16 halves the conflict cycles and takes the kernel alone from 2.02 to 1.56 ms per
-// launch, one C5 call from 51.8 to 51.2 ms -- but its 64 KiB, 512-thread workgroups (2 waves per SIMD at once) no
-// longer fit beside another call's PBKDF2 head, and two concurrent callers fell from 4.06 to 3.26 M PMK/s
-// (profiles/r02/kv3_slices_ab), so the default stays plain.
-//
-// Lane-sliced Te0 (build switch DWPA_KV3_AES = 1, the default since round 3): ONE table, Te0, in 32 interleaved
-// copies -- entry x of copy c at word 32 x + c, lane l reads copy l % 32 -- so every ds_read_b32 of a 32-lane group
-// hits 32 distinct banks whatever the indices are: no bank conflicts at all, in 32 KiB per workgroup.  Te1..Te3 are
-// Te0 rotated right by 8/16/24 (one v_alignbit each, 12 per round) and the S-box byte is byte 2 of Te0.  A 256-thread
-// workgroup (one wave per SIMD) still fits beside another call's PBKDF2 head: it needs one 106-VGPR wave slot per
-// SIMD, where the 16-copy four-table layout needed 64 KiB and two per SIMD.  DWPA_KV3_AES = 0 keeps the four plain
-// (or DWPA_KV3_SLICES-sliced) tables for A/B.
-#ifndef DWPA_KV3_AES
-#define DWPA_KV3_AES 1
-#endif
-#ifndef DWPA_KV3_SLICES
-#define DWPA_KV3_SLICES 1
-#endif
-#if DWPA_KV3_AES == 1
+// ONE table, Te0, in 32 interleaved copies -- entry x of copy c at word 32 x + c, lane l reads copy l % 32 -- so every
+// ds_read_b32 of a 32-lane group hits 32 distinct banks whatever the indices are: no bank conflicts at all, in 32 KiB
+// per workgroup.  Te1..Te3 are Te0 rotated right by 8/16/24 (one v_alignbit each, 12 per round) and the S-box byte is
+// byte 2 of Te0.  A 256-thread workgroup (one wave per SIMD) fits beside another call's PBKDF2 head: it needs one
+// 106-VGPR wave slot per SIMD.  (The four-table layouts, sliced or not, a two-table layout and round keys in LDS were
+// measured and dropped: CHANGELOG.md, rounds 2-4.)
 constexpr uint32_t AES_SLICES = 32;                     // copies of Te0
 constexpr uint32_t AES_LDS_WORDS = 256 * AES_SLICES;    // 32 KiB
 // Byte offset of Te0[byte K of s] in the lane's copy: (x << 7) | cw, cw = 4 (lane % 32).  Two full-rate ops for
@@ -562,72 +543,8 @@ __device__ __forceinline__ uint32_t aes4_subword_v1(const uint32_t* te, uint32_t
     const uint32_t lo = __builtin_amdgcn_perm(aes_v1_ld<KC>(te, wc, cw), aes_v1_ld<KD>(te, wd, cw), 0x00000501u);
     return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
 }
-#elif DWPA_KV3_AES == 3
-// A/B variant (round 4): Te0 AND Te1 = rotr(Te0, 8), 16 copies each, in the same 32 KiB and the same 128-byte entry
-// stride as layout 1: entry x of Te0 copy c at word 32 x + c, of Te1 copy c at word 32 x + 16 + c; lane l reads copy
-// l % 16.  Te2 / Te3 are Te0 / Te1 rotated by 16, so a column is Te0[a] ^ Te1[b] ^ rotr(Te0[c] ^ Te1[d], 16): one
-// rotate instead of three.  Lanes l and l + 16 share a copy, so reads are 2-way bank conflicts.
-constexpr uint32_t AES_SLICES = 32;                     // words per entry
-constexpr uint32_t AES_LDS_WORDS = 256 * AES_SLICES;    // 32 KiB
-template <int K>
-__device__ __forceinline__ uint32_t aes_v1_off(uint32_t s, uint32_t cw) {
-    const uint32_t t = K == 3 ? s >> 17 : K == 2 ? s >> 9 : K == 1 ? s >> 1 : s << 7;
-    return __builtin_amdgcn_bitop3_b32(t, 0x7f80u, cw, 0xea);
-}
-template <int K>
-__device__ __forceinline__ uint32_t aes_v1_ld(const uint32_t* te, uint32_t s, uint32_t cw) {
-    return *(const uint32_t*)((const char*)te + aes_v1_off<K>(s, cw));
-}
-template <int KA, int KB, int KC, int KD>
-__device__ __forceinline__ uint32_t aes4_subword_v1(const uint32_t* te, uint32_t cw, uint32_t wa, uint32_t wb,
-                                                    uint32_t wc, uint32_t wd) {
-    const uint32_t hi = __builtin_amdgcn_perm(aes_v1_ld<KA>(te, wa, cw), aes_v1_ld<KB>(te, wb, cw), 0x06020000u);
-    const uint32_t lo = __builtin_amdgcn_perm(aes_v1_ld<KC>(te, wc, cw), aes_v1_ld<KD>(te, wd, cw), 0x00000501u);
-    return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
-}
-#elif DWPA_KV3_AES == 2
-// A/B variant: Te0 AND Te2 = rotr(Te0, 16), 32 copies each, entry x of copy c at byte (x << 8) | (c << 2) (Te2 at
-// +128): one v_perm builds a lookup's whole address from the state byte and the lane's copy offset, and
-// Te1 ^ Te3 = rotr(Te0 ^ Te2, 8) leaves one rotate per column instead of three.  64 KiB per workgroup.
-constexpr uint32_t AES_SLICES = 1;               // the lane's copy is chosen inside the lookups (cw)
-constexpr uint32_t AES_LDS_WORDS = 256 * 64;     // 64 KiB
-__device__ __forceinline__ uint32_t aes_v2_ld(const uint32_t* te, uint32_t s, uint32_t k, uint32_t cw, uint32_t tbl) {
-    const uint32_t off = __builtin_amdgcn_perm(cw, s, 0x0c0c0004u | (k << 8));  // (byte k of s) << 8 | cw
-    return *(const uint32_t*)((const char*)te + off + 128u * tbl);
-}
-__device__ __forceinline__ uint32_t aes4_subword_v2(const uint32_t* te, uint32_t cw, uint32_t wa, uint32_t ka,
-                                                    uint32_t wb, uint32_t kb, uint32_t wc, uint32_t kc, uint32_t wd,
-                                                    uint32_t kd) {
-    // (S[a], S[b], S[c], S[d]) with a = byte ka of wa ...; S[x] = byte 2 (and 1) of Te0[x]
-    const uint32_t hi = __builtin_amdgcn_perm(aes_v2_ld(te, wa, ka, cw, 0), aes_v2_ld(te, wb, kb, cw, 0), 0x06020000u);
-    const uint32_t lo = __builtin_amdgcn_perm(aes_v2_ld(te, wc, kc, cw, 0), aes_v2_ld(te, wd, kd, cw, 0), 0x00000501u);
-    return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
-}
-#else
-constexpr uint32_t AES_SLICES = DWPA_KV3_SLICES;
-constexpr uint32_t AES_LDS_WORDS = 1024 * AES_SLICES;
-#define AES_T(t, x) te4[(t) * 256u * AES_SLICES + (x) * AES_SLICES]
-__device__ __forceinline__ uint32_t aes4_subword(const uint32_t* te4, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    // bytes (S[a], S[b], S[c], S[d]) from most to least significant; a..d are byte values (0..255)
-    const uint32_t hi = __builtin_amdgcn_perm(AES_T(2, a), AES_T(3, b), 0x07020100u);  // S[a]:b3, S[b]:b2
-    const uint32_t lo = __builtin_amdgcn_perm(AES_T(0, c), AES_T(1, d), 0x07060500u);  // S[c]:b1, S[d]:b0
-    return __builtin_amdgcn_perm(hi, lo, 0x07060100u);
-}
-#endif
 // The table image for the workgroup's LDS: word k of AES_LDS_WORDS.
-__device__ __forceinline__ uint32_t aes_lds_word(uint32_t k) {
-#if DWPA_KV3_AES == 1
-    return AES_TABLES.te0[k >> 5];
-#elif DWPA_KV3_AES == 3
-    return rotr(AES_TABLES.te0[k >> 5], (k & 16) >> 1);  // words 32x + c: Te0[x]; 32x + 16 + c: Te1[x]
-#elif DWPA_KV3_AES == 2
-    return rotr(AES_TABLES.te0[k >> 6], (k & 32) >> 1);  // words 64x + c: Te0[x]; 64x + 32 + c: Te2[x]
-#else
-    const uint32_t t = k / (256 * AES_SLICES), x = k / AES_SLICES & 255;  // table t, entry x, copy k % S
-    return rotr(AES_TABLES.te0[x], 8 * t);
-#endif
-}
-#if DWPA_KV3_AES == 1
+__device__ __forceinline__ uint32_t aes_lds_word(uint32_t k) { return AES_TABLES.te0[k >> 5]; }
 // te = the table base (every lane's copy is picked by cw inside the lookups)
 __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uint32_t key[4], uint32_t s[4]) {
     constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
@@ -657,139 +574,6 @@ __device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uin
     s[2] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s2, s3, s0, s1) ^ k2;
     s[3] = aes4_subword_v1<3, 2, 1, 0>(te, cw, s3, s0, s1, s2) ^ k3;
 }
-#elif DWPA_KV3_AES == 3
-__device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uint32_t key[4], uint32_t s[4]) {
-    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
-    const uint32_t c0 = (threadIdx.x & 15u) << 2, c1 = c0 + 64u;  // the lane's Te0 / Te1 copy
-    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
-    uint32_t s0 = s[0] ^ k0, s1 = s[1] ^ k1, s2 = s[2] ^ k2, s3 = s[3] ^ k3;
-#define T0(w, k) aes_v1_ld<k>(te, w, c0)
-#define T1(w, k) aes_v1_ld<k>(te, w, c1)
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-        k0 ^= aes4_subword_v1<2, 1, 0, 3>(te, c0, k3, k3, k3, k3) ^ (RCON[r - 1] << 24);
-        k1 ^= k0;
-        k2 ^= k1;
-        k3 ^= k2;
-        const uint32_t t0 = xor3(T0(s0, 3), T1(s1, 2), k0) ^ rotr(T0(s2, 1) ^ T1(s3, 0), 16);
-        const uint32_t t1 = xor3(T0(s1, 3), T1(s2, 2), k1) ^ rotr(T0(s3, 1) ^ T1(s0, 0), 16);
-        const uint32_t t2 = xor3(T0(s2, 3), T1(s3, 2), k2) ^ rotr(T0(s0, 1) ^ T1(s1, 0), 16);
-        const uint32_t t3 = xor3(T0(s3, 3), T1(s0, 2), k3) ^ rotr(T0(s1, 1) ^ T1(s2, 0), 16);
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-#undef T0
-#undef T1
-    k0 ^= aes4_subword_v1<2, 1, 0, 3>(te, c0, k3, k3, k3, k3) ^ (RCON[9] << 24);
-    k1 ^= k0;
-    k2 ^= k1;
-    k3 ^= k2;
-    s[0] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s0, s1, s2, s3) ^ k0;
-    s[1] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s1, s2, s3, s0) ^ k1;
-    s[2] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s2, s3, s0, s1) ^ k2;
-    s[3] = aes4_subword_v1<3, 2, 1, 0>(te, c0, s3, s0, s1, s2) ^ k3;
-}
-#elif DWPA_KV3_AES == 2
-__device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te, const uint32_t key[4], uint32_t s[4]) {
-    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
-    const uint32_t cw = (threadIdx.x & 31u) << 2;
-    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
-    uint32_t s0 = s[0] ^ k0, s1 = s[1] ^ k1, s2 = s[2] ^ k2, s3 = s[3] ^ k3;
-#define T0(w, k) aes_v2_ld(te, w, k, cw, 0)
-#define T2(w, k) aes_v2_ld(te, w, k, cw, 1)
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-        k0 ^= aes4_subword_v2(te, cw, k3, 2, k3, 1, k3, 0, k3, 3) ^ (RCON[r - 1] << 24);
-        k1 ^= k0;
-        k2 ^= k1;
-        k3 ^= k2;
-        const uint32_t t0 = xor3(T0(s0, 3), T2(s2, 1), k0) ^ rotr(T0(s1, 2) ^ T2(s3, 0), 8);
-        const uint32_t t1 = xor3(T0(s1, 3), T2(s3, 1), k1) ^ rotr(T0(s2, 2) ^ T2(s0, 0), 8);
-        const uint32_t t2 = xor3(T0(s2, 3), T2(s0, 1), k2) ^ rotr(T0(s3, 2) ^ T2(s1, 0), 8);
-        const uint32_t t3 = xor3(T0(s3, 3), T2(s1, 1), k3) ^ rotr(T0(s0, 2) ^ T2(s2, 0), 8);
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-#undef T0
-#undef T2
-    k0 ^= aes4_subword_v2(te, cw, k3, 2, k3, 1, k3, 0, k3, 3) ^ (RCON[9] << 24);
-    k1 ^= k0;
-    k2 ^= k1;
-    k3 ^= k2;
-    s[0] = aes4_subword_v2(te, cw, s0, 3, s1, 2, s2, 1, s3, 0) ^ k0;
-    s[1] = aes4_subword_v2(te, cw, s1, 3, s2, 2, s3, 1, s0, 0) ^ k1;
-    s[2] = aes4_subword_v2(te, cw, s2, 3, s3, 2, s0, 1, s1, 0) ^ k2;
-    s[3] = aes4_subword_v2(te, cw, s3, 3, s0, 2, s1, 1, s2, 0) ^ k3;
-}
-#else
-__device__ __forceinline__ void aes128_encrypt_te4(const uint32_t* te4, const uint32_t key[4], uint32_t s[4]) {
-    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
-    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
-    uint32_t s0 = s[0] ^ k0, s1 = s[1] ^ k1, s2 = s[2] ^ k2, s3 = s[3] ^ k3;
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-        k0 ^= aes4_subword(te4, (k3 >> 16) & 0xff, (k3 >> 8) & 0xff, k3 & 0xff, k3 >> 24) ^ (RCON[r - 1] << 24);
-        k1 ^= k0;
-        k2 ^= k1;
-        k3 ^= k2;
-        const uint32_t t0 = xor3(xor3(AES_T(0, s0 >> 24), AES_T(1, (s1 >> 16) & 0xff), AES_T(2, (s2 >> 8) & 0xff)),
-                                 AES_T(3, s3 & 0xff), k0);
-        const uint32_t t1 = xor3(xor3(AES_T(0, s1 >> 24), AES_T(1, (s2 >> 16) & 0xff), AES_T(2, (s3 >> 8) & 0xff)),
-                                 AES_T(3, s0 & 0xff), k1);
-        const uint32_t t2 = xor3(xor3(AES_T(0, s2 >> 24), AES_T(1, (s3 >> 16) & 0xff), AES_T(2, (s0 >> 8) & 0xff)),
-                                 AES_T(3, s1 & 0xff), k2);
-        const uint32_t t3 = xor3(xor3(AES_T(0, s3 >> 24), AES_T(1, (s0 >> 16) & 0xff), AES_T(2, (s1 >> 8) & 0xff)),
-                                 AES_T(3, s2 & 0xff), k3);
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-    k0 ^= aes4_subword(te4, (k3 >> 16) & 0xff, (k3 >> 8) & 0xff, k3 & 0xff, k3 >> 24) ^ (RCON[9] << 24);
-    k1 ^= k0;
-    k2 ^= k1;
-    k3 ^= k2;
-    s[0] = aes4_subword(te4, s0 >> 24, (s1 >> 16) & 0xff, (s2 >> 8) & 0xff, s3 & 0xff) ^ k0;
-    s[1] = aes4_subword(te4, s1 >> 24, (s2 >> 16) & 0xff, (s3 >> 8) & 0xff, s0 & 0xff) ^ k1;
-    s[2] = aes4_subword(te4, s2 >> 24, (s3 >> 16) & 0xff, (s0 >> 8) & 0xff, s1 & 0xff) ^ k2;
-    s[3] = aes4_subword(te4, s3 >> 24, (s0 >> 16) & 0xff, (s1 >> 8) & 0xff, s2 & 0xff) ^ k3;
-}
-
-// The same with the round keys expanded once per key into LDS (rk[(r - 1) * stride] = round key r, one 16-byte slot
-// per lane: ds_read_b128 of lane-contiguous slots is bank-conflict free), so a CMAC over n blocks pays the 40
-// key-schedule lookups once instead of n times (build with -DDWPA_KV3_RK_LDS=1; A/B of the keyver-3 verify).
-__device__ __forceinline__ void aes128_expand_lds(const uint32_t* te4, const uint32_t key[4], uint4* rk,
-                                                  uint32_t stride) {
-    constexpr uint32_t RCON[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1b, 0x36};
-    uint32_t k0 = key[0], k1 = key[1], k2 = key[2], k3 = key[3];
-#pragma unroll
-    for (int r = 1; r <= 10; r++) {
-        k0 ^= aes4_subword(te4, (k3 >> 16) & 0xff, (k3 >> 8) & 0xff, k3 & 0xff, k3 >> 24) ^ (RCON[r - 1] << 24);
-        k1 ^= k0;
-        k2 ^= k1;
-        k3 ^= k2;
-        rk[(r - 1) * stride] = make_uint4(k0, k1, k2, k3);
-    }
-}
-__device__ __forceinline__ void aes128_encrypt_rk(const uint32_t* te4, const uint32_t key[4], const uint4* rk,
-                                                  uint32_t stride, uint32_t s[4]) {
-    uint32_t s0 = s[0] ^ key[0], s1 = s[1] ^ key[1], s2 = s[2] ^ key[2], s3 = s[3] ^ key[3];
-#pragma unroll
-    for (int r = 1; r < 10; r++) {
-        const uint4 k = rk[(r - 1) * stride];
-        const uint32_t t0 = xor3(xor3(AES_T(0, s0 >> 24), AES_T(1, (s1 >> 16) & 0xff), AES_T(2, (s2 >> 8) & 0xff)),
-                                 AES_T(3, s3 & 0xff), k.x);
-        const uint32_t t1 = xor3(xor3(AES_T(0, s1 >> 24), AES_T(1, (s2 >> 16) & 0xff), AES_T(2, (s3 >> 8) & 0xff)),
-                                 AES_T(3, s0 & 0xff), k.y);
-        const uint32_t t2 = xor3(xor3(AES_T(0, s2 >> 24), AES_T(1, (s3 >> 16) & 0xff), AES_T(2, (s0 >> 8) & 0xff)),
-                                 AES_T(3, s1 & 0xff), k.z);
-        const uint32_t t3 = xor3(xor3(AES_T(0, s3 >> 24), AES_T(1, (s0 >> 16) & 0xff), AES_T(2, (s1 >> 8) & 0xff)),
-                                 AES_T(3, s2 & 0xff), k.w);
-        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
-    }
-    const uint4 k = rk[9 * stride];
-    s[0] = aes4_subword(te4, s0 >> 24, (s1 >> 16) & 0xff, (s2 >> 8) & 0xff, s3 & 0xff) ^ k.x;
-    s[1] = aes4_subword(te4, s1 >> 24, (s2 >> 16) & 0xff, (s3 >> 8) & 0xff, s0 & 0xff) ^ k.y;
-    s[2] = aes4_subword(te4, s2 >> 24, (s3 >> 16) & 0xff, (s0 >> 8) & 0xff, s1 & 0xff) ^ k.z;
-    s[3] = aes4_subword(te4, s3 >> 24, (s0 >> 16) & 0xff, (s1 >> 8) & 0xff, s2 & 0xff) ^ k.w;
-}
-
-#endif  // DWPA_KV3_AES
 
 // CMAC subkey doubling on a 128-bit big-endian value held in 4 words
 __device__ __forceinline__ void cmac_dbl(const uint32_t in[4], uint32_t out[4]) {

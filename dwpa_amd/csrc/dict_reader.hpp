@@ -164,7 +164,8 @@ class BlockInflater {
     }
     // Worker threads for one large gzip file (ParallelGunzip, pinflate.hpp): DWPA_INFLATE_THREADS, default
     // min(8, half the CPUs this process may use); files under 4 chunks (DWPA_INFLATE_CHUNK_MB, default 4) and
-    // DWPA_INFLATE_THREADS=1 take the single-stream decoder.
+    // DWPA_INFLATE_THREADS=1 take the single-stream decoder.  DWPA_INFLATE_CHUNK_MB is the test suite's switch to run
+    // the parallel decoder on small files (tests/test_dict_reader.py).
     static size_t chunk_bytes() {
         const char* e = getenv("DWPA_INFLATE_CHUNK_MB");
         const long mb = e && *e ? atol(e) : 4;

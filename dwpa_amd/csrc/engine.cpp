@@ -1,9 +1,11 @@
-// engine.cpp -- libdwpa22000.so: device contexts, the server-side check path, the device-resident scan API and
-// the C-ABI exports declared in include/dwpa22000.h.
+// engine.cpp -- libdwpa22000.so: device contexts, the server-side check path (routed to the host backend in
+// host_check.cpp for small calls, and without a device when allowed), the device-resident scan API and the C-ABI
+// exports declared in include/dwpa22000.h.
 //
-// Process model: one process may drive every visible MI355X (crack_files: one host thread per device, static
-// contiguous keyspace shards, no collective -- shards never exchange data; hits are gathered on the host).
-// bench.py instead runs one process per GPU (torch.distributed launch) and uses the scan API on its own device.
+// Process model: one process may drive every visible MI355X.  crack_files (crack.cpp) runs a stager and a scanner
+// thread per device worker over ONE shared dictionary stream, cut into work items by guided self-scheduling
+// (dict_reader.hpp ItemQueue) -- no collective, workers never exchange data; hits are gathered on the host.
+// bench.py's scan workloads run one process per GPU (torch.distributed launch) on the scan API instead.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -361,30 +363,15 @@ static std::vector<int> active_devices(uint32_t mask = 0) {
     return v;
 }
 
-static int env_int(const char* name, int dflt, int lo, int hi) {
-    const char* e = getenv(name);
-    const int v = e && *e ? atoi(e) : dflt;
-    return v < lo ? lo : v > hi ? hi : v;
-}
-// Check-path scheduling knobs (A/B switches; the defaults are the measured best):
-//   DWPA_CHECK_PRIO    wave priority of the post-derive kernels (0)
-//   DWPA_KV3_PRIO      wave priority of the keyver-3 verify kernels (0)
-//   DWPA_TAIL_PRIO     priority the PBKDF2 tail raises itself to once the head has ended (2; 0 = stays at 0)
-//   DWPA_HEAD_FENCE    concurrent calls on one device launch their heads one after another (1)
-//   DWPA_VERIFY_FANOUT the head slots' keyver-3 verify runs on its own stream beside the other classes (1)
-//   DWPA_VERIFY_KV3_FIRST the keyver-3 launches are queued before the other classes (0)
-static int check_prio_knob() { static const int v = env_int("DWPA_CHECK_PRIO", 0, 0, 3); return v; }
-static int kv3_prio_knob() { static const int v = env_int("DWPA_KV3_PRIO", 0, 0, 3); return v; }
-static int tail_prio_knob() { static const int v = env_int("DWPA_TAIL_PRIO", 2, 0, 3); return v; }
-static bool head_fence_knob() { static const bool v = env_int("DWPA_HEAD_FENCE", 1, 0, 1) != 0; return v; }
-static bool verify_fanout_knob() { static const bool v = env_int("DWPA_VERIFY_FANOUT", 1, 0, 1) != 0; return v; }
-static bool verify_kv3_first_knob() { static const bool v = env_int("DWPA_VERIFY_KV3_FIRST", 0, 0, 1) != 0; return v; }
+// The priority the PBKDF2 tail raises itself to once the head has ended (pbkdf2_dev.hpp pbkdf2_lane_tail): above
+// the verify waves that share its SIMDs.  (The other scheduling choices of the check path -- post-derive and keyver-3
+// kernels at priority 0, head fence, keyver-3 fan-out, verify order -- are fixed at their measured best: DESIGN.md 4,
+// CHANGELOG.md.)
+constexpr uint32_t TAIL_PRIO = 2;
 
 static int device_stream(Device& d) {
     if (!d.stream) {
         HIPCHK(hipSetDevice(d.id));
-        HIPCHK(set_check_prio((uint32_t)check_prio_knob()));
-        HIPCHK(set_kv3_prio((uint32_t)kv3_prio_knob()));
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&d.side, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&d.side_done, hipEventDisableTiming));
@@ -608,15 +595,6 @@ struct DeriveStage {
     uint32_t split = 0;  // slots [0, split) read d.stream's PMKs; [split, n) d.tail's (== n: no tail)
 };
 
-// DWPA_CHECK_SPLIT=0 keeps every derive in one PBKDF2 launch (A/B of the head/tail split below).
-static bool check_split_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("DWPA_CHECK_SPLIT");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-
 // Head/tail split of one derive.  PBKDF2 is issue-bound, so a launch takes as long as its fullest SIMD: nu unique
 // PMKs at k.f waves per SIMD cost k + 1 whole wave times (~7 ms each at C5 size), the last one with 1 - f of the
 // chip idle.  The head (k whole waves per SIMD) runs at wave priority 3..1 (pbkdf2_dev.hpp PRIO); the tail
@@ -625,7 +603,7 @@ static bool check_split_enabled() {
 // up (the head's PRIO kernel; below that both kernels are lone-wave plain kernels) the split pays.
 static uint32_t head_pmks(uint32_t nu) {
     const uint32_t unit = pbkdf2_wave_unit();
-    if (!check_split_enabled() || !unit || nu < 2 * unit) return nu;
+    if (!unit || nu < 2 * unit) return nu;
     return nu / unit * unit;
 }
 
@@ -781,7 +759,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
                                 (const uint32_t*)d.uslot.p, nu, (uint32_t*)d.batch.mid.p, cap, s));
         HeadFence& f = *g_fence[d.id];
         std::lock_guard<std::mutex> fl(f.mu);
-        if (head_fence_knob() && f.last && f.last != d.head_end) HIPCHK(hipStreamWaitEvent(s, f.last, 0));
+        if (f.last && f.last != d.head_end) HIPCHK(hipStreamWaitEvent(s, f.last, 0));
         uint32_t* head_flag = (uint32_t*)d.batch.counters.p + 3;  // zeroed with the counters above
         uint32_t* raised = (uint32_t*)d.batch.counters.p + 4;     // likewise; read back by collect_hits
         d.stats.pmks += nu;
@@ -789,7 +767,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
             HIPCHK(hipEventRecord(d.prep_done, s));
             HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
             HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh,
-                                         head_flag, (uint32_t)tail_prio_knob(), raised, d.tail));
+                                         head_flag, TAIL_PRIO, raised, d.tail));
             d.stats.tail_pmks += nu - nh;
             d.stats.tail_waves += 2 * ((nu - nh + 63) / 64);  // two output-block lanes per PMK
         }
@@ -812,7 +790,8 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
     return 0;
 }
 
-// DWPA_FIRST_KEY_EXIT=0 verifies every key of a job even after an earlier key matched (A/B of the early exit).
+// DWPA_FIRST_KEY_EXIT=0 verifies every key of a job even after an earlier key matched: a test switch
+// (tests/test_gpu_parity.py::test_first_key_exit_across_chunks runs both ways; the results are the same).
 static bool first_key_exit_knob() {
     static const bool on = [] {
         const char* e = getenv("DWPA_FIRST_KEY_EXIT");
@@ -821,15 +800,9 @@ static bool first_key_exit_knob() {
     return on;
 }
 
-// Keys per attempt-parallel segment (DWPA_ATT_SEG_KEYS, 1..64, default 16) when the first-key early exit is on.
-static uint32_t att_seg_keys() {
-    static const uint32_t k = [] {
-        const char* e = getenv("DWPA_ATT_SEG_KEYS");
-        const int v = e ? atoi(e) : 16;
-        return (uint32_t)std::min(64, std::max(1, v));
-    }();
-    return k;
-}
+// Keys per attempt-parallel segment when the first-key early exit is on: a later segment of the same job can skip
+// itself once an earlier one matched.
+constexpr uint32_t ATT_SEG_KEYS = 16;
 
 // d.stream waits for everything queued on d.tail so far.
 static int join_tail(Device& d) {
@@ -852,7 +825,7 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
     // runs while the PBKDF2 tail holds some SIMDs ends only with the tail, so fewer launches in a row end sooner.
     std::vector<SegDev> bucket[8];
     auto bucket_vc = [](int k) { return k == 5 ? (uint32_t)(VC_KV1 | VC_KV2) : 1u << (k & 3); };
-    const uint32_t att_seg = first_key_exit_knob() ? att_seg_keys() : 64;
+    const uint32_t att_seg = first_key_exit_knob() ? ATT_SEG_KEYS : 64;
     for (uint32_t i = 0; i < n;) {
         uint32_t j = i;
         const uint32_t job = T.job[b + i];
@@ -924,14 +897,13 @@ static int queue_verify(Device& d, const SlotTable& T, size_t base, size_t b, si
     // the other classes on s, which then waits for them.  Verify waves that land on the SIMDs of the tail's lone
     // waves hold back only their own stream.  (A fourth stream of its own would share a hardware queue with the
     // tail's: a process gets GPU_MAX_HW_QUEUES = 4, one of them the null stream's.)
-    const bool fan = fanout && verify_fanout_knob() && (!bucket[3].empty() || !bucket[7].empty());
+    const bool fan = fanout && (!bucket[3].empty() || !bucket[7].empty());
     if (fan) {
         HIPCHK(hipEventRecord(d.vs_go, s));
         HIPCHK(hipStreamWaitEvent(d.side, d.vs_go, 0));
     }
     uint32_t* hitcnt = (uint32_t*)d.batch.counters.p + 1;
-    static const int kOrder[2][8] = {{0, 1, 2, 3, 4, 5, 6, 7}, {3, 7, 0, 1, 2, 4, 5, 6}};
-    for (int k : kOrder[verify_kv3_first_knob() ? 1 : 0]) {
+    for (int k = 0; k < 8; k++) {
         const uint32_t nb = (uint32_t)(bstart[k + 1] - bstart[k]), vc = bucket_vc(k);
         const SegDev* sg = (const SegDev*)segbuf.p + bstart[k];
         if (!nb) continue;

@@ -99,11 +99,8 @@ __global__ __launch_bounds__(256) void k_pbkdf2(const uint32_t* __restrict__ mid
 }
 
 // Lanes [live, count) of a padded launch (lone_pad below) repeat slot live-1's derivation and store nothing.
-// DWPA_LONE_WPE: the occupancy bound of this lone-wave kernel (A/B builds may lift it).
-#ifndef DWPA_LONE_WPE
-#define DWPA_LONE_WPE __attribute__((amdgpu_waves_per_eu(8, 8)))
-#endif
-__global__ __launch_bounds__(256) DWPA_LONE_WPE void k_pbkdf2_ms(
+// Occupancy bound 8 waves per SIMD (lifting it measured slower, CHANGELOG.md round 5).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_pbkdf2_ms(
     const uint32_t* __restrict__ mid, uint32_t cap, uint32_t count, const uint32_t* __restrict__ pool,
     const uint32_t* __restrict__ sref, uint32_t* __restrict__ pmk, uint32_t live) {
     const uint32_t blk = blockIdx.y;
@@ -146,21 +143,12 @@ __global__ void k_set_flag(uint32_t* flag) {
     if (threadIdx.x == 0) __hip_atomic_exchange(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave priority of the check path's post-derive kernels (DWPA_CHECK_PRIO, set per device by set_check_prio); the
-// keyver-3 class (latency-bound AES-CMAC, the longest verify) has its own (DWPA_KV3_PRIO, set_kv3_prio).
-__device__ uint32_t g_check_prio = 0;
-__device__ uint32_t g_kv3_prio = 0;
-__device__ __forceinline__ void check_prio() { set_wave_prio(g_check_prio); }
-template <uint32_t VC>
-__device__ __forceinline__ void check_prio_vc() { set_wave_prio(VC == VC_KV3 ? g_kv3_prio : g_check_prio); }
-
 // Slot PMKs from the derived unique (ESSID, key) PMKs or from caller-supplied PMKs:
 // src[i] = u -> upmk[.][u];  src[i] = GATHER_CALLER | c -> cpmk[c][0..7] (check_key_m22000's $pmk, common.php:178).
 __global__ __launch_bounds__(256) void k_gather_pmk(const uint32_t* __restrict__ upmk, uint32_t ucap,
                                                     const uint32_t* __restrict__ cpmk,
                                                     const uint32_t* __restrict__ src, uint32_t n,
                                                     uint32_t* __restrict__ pmk, uint32_t cap) {
-    check_prio();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t r = src[i];
@@ -296,16 +284,11 @@ __device__ __forceinline__ uint32_t att_nblk(const LineDev& L, const AttDev& at)
 // keyver 3: KDF-SHA256) -> KCK -> HMAC-MD5 (1), HMAC-SHA1 (2) or AES-128-CMAC (3) over the EAPOL frame.
 // KP (key-parallel): `at` is the same for every lane, so its PRF blocks come as KW blocks; otherwise (attempt-
 // parallel, lanes hold different attempts) they are patched per lane.  The EAPOL frame's blocks are KW blocks.
-// DWPA_KV3_RK_LDS=1 (with DWPA_KV3_WAVES=3): AES round keys expanded once per key into LDS instead of per CMAC
-// block.  Measured level (profiles/r02/kv3_rk_lds_ab): the compiler already hoists the loop-invariant key schedule
-// out of the CMAC loop into registers, so the LDS reads left are the state's T-table lookups (4.3 bank-conflict
-// cycles per ds_read); kept as a build switch for A/B.
-#ifndef DWPA_KV3_RK_LDS
-#define DWPA_KV3_RK_LDS 0
-#endif
+// (AES round keys in LDS, once per key, measured level: the compiler already hoists the loop-invariant key schedule
+// out of the CMAC loop, CHANGELOG.md round 2.)
 template <uint32_t VC, bool KP>
 __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __restrict__ pool, const EapolKey& K,
-                                          const AttDev& at, const uint32_t* te, uint32_t mic[4], uint4* rk = nullptr) {
+                                          const AttDev& at, const uint32_t* te, uint32_t mic[4]) {
     constexpr bool has1 = (VC & VC_KV1) != 0, has2 = (VC & VC_KV2) != 0, has3 = (VC & VC_KV3) != 0;
     if ((has1 || has2) && (!has3 || L.keyver != 3)) {
         uint32_t st[5], ptk[5];
@@ -348,13 +331,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
         sha256_compress(ptk, m);
         // AES-128-CMAC(KCK = PTK[0..15], EAPOL)  (common.php:72-112)
         uint32_t Lb[4] = {0, 0, 0, 0}, K1[4], K2[4];
-#if DWPA_KV3_RK_LDS
-        aes128_expand_lds(te, ptk, rk, blockDim.x);
-        aes128_encrypt_rk(te, ptk, rk, blockDim.x, Lb);
-#else
-        (void)rk;
         aes128_encrypt_te4(te, ptk, Lb);
-#endif
         cmac_dbl(Lb, K1);
         cmac_dbl(K1, K2);
         uint32_t c[4] = {0, 0, 0, 0};
@@ -367,11 +344,7 @@ __device__ __forceinline__ void eapol_mic(const LineDev& L, const uint32_t* __re
                 if (last) v ^= L.cmac_complete ? K1[k] : K2[k];
                 c[k] ^= v;
             }
-#if DWPA_KV3_RK_LDS
-            aes128_encrypt_rk(te, ptk, rk, blockDim.x, c);
-#else
             aes128_encrypt_te4(te, ptk, c);
-#endif
         }
         mic[0] = c[0]; mic[1] = c[1]; mic[2] = c[2]; mic[3] = c[3];
     }
@@ -407,31 +380,23 @@ __device__ __forceinline__ void report_hits(bool found, uint32_t lane, uint64_t 
     }
 }
 
-// The AES table image (crypto_dev.hpp: lane-sliced Te0, or Te0..Te3) into the workgroup's LDS, for kernels that
-// verify keyver 3; returns this lane's copy.
+// The AES table image (crypto_dev.hpp: lane-sliced Te0) into the workgroup's LDS, for kernels that verify keyver 3;
+// returns the table base (every lane picks its copy inside the lookups).
 template <uint32_t VC>
 __device__ __forceinline__ const uint32_t* aes_table_lds(uint32_t* te) {
     if constexpr ((VC & VC_KV3) != 0) {
-#if DWPA_KV3_AES == 1 || DWPA_KV3_AES == 3
-        // four copies of one entry per 16-byte store (words 4j..4j+3 all hold the same table's entry 4j >> 5)
+        // four copies of one entry per 16-byte store (words 4j..4j+3 all hold entry 4j >> 5)
         for (uint32_t j = threadIdx.x; j < AES_LDS_WORDS / 4; j += blockDim.x) {
             const uint32_t v = aes_lds_word(4 * j);
             reinterpret_cast<uint4*>(te)[j] = make_uint4(v, v, v, v);
         }
-#else
-        for (uint32_t k = threadIdx.x; k < AES_LDS_WORDS; k += blockDim.x) te[k] = aes_lds_word(k);
-#endif
         __syncthreads();
     }
-    return te + (DWPA_KV3_AES == 0 ? threadIdx.x % AES_SLICES : 0u);  // layouts 1/2 pick the lane's copy per lookup
+    return te;
 }
-// keyver-3 kernels with the four-table layout sliced (DWPA_KV3_AES=0, DWPA_KV3_SLICES > 1: 64 KiB of LDS at S = 16,
-// an A/B build) run 512-thread workgroups: two per CU, 4 waves per SIMD; the lane-sliced Te0 (32 KiB) and the plain
-// tables keep 256-thread workgroups, which also fit beside a concurrent call's PBKDF2 head.
-#ifndef DWPA_KV3_BLOCK
-#define DWPA_KV3_BLOCK (DWPA_KV3_AES == 0 && AES_SLICES > 1 ? 512 : 256)
-#endif
-constexpr uint32_t vc_block(uint32_t vc) { return (vc & VC_KV3) ? DWPA_KV3_BLOCK : 256; }
+// Every verify class runs 256-thread workgroups; the keyver-3 ones (32 KiB of LDS) also fit beside a concurrent
+// call's PBKDF2 head.
+constexpr uint32_t vc_block(uint32_t) { return 256; }
 
 // Key-parallel verification (client scans: many candidates, few attempts): one lane = one candidate slot, one
 // wave = up to 64 slots x one line; the line and every attempt are wave-uniform (scalar loads).
@@ -439,10 +404,7 @@ constexpr uint32_t vc_block(uint32_t vc) { return (vc & VC_KV3) ? DWPA_KV3_BLOCK
 // 9 VGPRs, which measured level with a 6-wave, spill-free build (profiles/r01/verify_waves_ab); keyver 3 runs at 4
 // waves (106 VGPRs, AES round keys computed on the fly; 2 and 6 waves level, 8 waves with 18 spilled VGPRs slower:
 // profiles/r02/c5_sched/kv3_waves).
-#ifndef DWPA_KV3_WAVES
-#define DWPA_KV3_WAVES 4
-#endif
-constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? DWPA_KV3_WAVES : 8; }
+constexpr uint32_t vc_waves(uint32_t vc) { return (vc & VC_KV3) ? 4 : 8; }
 
 template <uint32_t VC>
 __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc_waves(VC)))) void k_verify(
@@ -454,15 +416,8 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                 const LineDev* __restrict__ lines, const uint32_t* __restrict__ pool,
                                                 const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                 uint32_t* __restrict__ hitcnt, uint32_t hitcap) {
-    check_prio_vc<VC>();
     __shared__ __attribute__((aligned(16))) uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 4];
     const uint32_t* te = aes_table_lds<VC>(te_lds);
-#if DWPA_KV3_RK_LDS
-    __shared__ uint4 rk_lds[(VC & VC_KV3) ? 10 * vc_block(VC) : 1];
-    uint4* rk = rk_lds + threadIdx.x;
-#else
-    uint4* rk = nullptr;
-#endif
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t segi = blockIdx.x * (blockDim.x >> 6) + wave;
@@ -518,7 +473,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
             const AttDev* al = atts + L.list_off + list * L.natt;
             for (uint32_t a = 0; a < L.natt; a++) {
                 uint32_t mic[4];
-                eapol_mic<VC, true>(L, pool, K, al[a], te, mic, rk);
+                eapol_mic<VC, true>(L, pool, K, al[a], te, mic);
                 if (mine && !found && mic_match(L, mic)) {
                     found = true;
                     found_att = a;
@@ -535,7 +490,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
 // k_eapol_keys: lane = (segment, key) pair, computes everything of the check that depends on the PMK but not on
 // the attempt (HMAC key midstates, PRF prefix: EapolKey) once per pair into a SoA scratch array, word w of pair
 // (segment i, key k) at keys[w * kstride + segk * i + k] (segk = the most keys a segment holds, 1..64: the host cuts
-// attempt-parallel segments to DWPA_ATT_SEG_KEYS keys, so the scratch is sized for that, not for 64).
+// attempt-parallel segments to ATT_SEG_KEYS (16) keys, so the scratch is sized for that, not for 64).
 //
 // k_verify_att: the (key, attempt) items of a segment are laid out key-major and cut into waves of 64 lanes, so
 // every lane runs one attempt and a wave ends only where the segment does (segs[i].pad = the segment's first wave
@@ -553,7 +508,6 @@ __global__ __launch_bounds__(256) void k_eapol_keys(const uint32_t* __restrict__
                                                     const LineDev* __restrict__ lines,
                                                     const uint32_t* __restrict__ pool, uint32_t* __restrict__ keys,
                                                     uint32_t kstride, uint32_t segk) {
-    check_prio_vc<VC>();
     const uint32_t segi = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t k = threadIdx.x & 63;
     if (segi >= nsegs) return;
@@ -592,15 +546,8 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
                                                     const AttDev* __restrict__ atts, HitDev* __restrict__ hits,
                                                     uint32_t* __restrict__ hitcnt, uint32_t hitcap,
                                                     uint32_t* __restrict__ first_hit) {
-    check_prio_vc<VC>();
     __shared__ __attribute__((aligned(16))) uint32_t te_lds[(VC & VC_KV3) ? AES_LDS_WORDS : 4];
     const uint32_t* te = aes_table_lds<VC>(te_lds);  // (every wave of the block helps fill the table first)
-#if DWPA_KV3_RK_LDS
-    __shared__ uint4 rk_lds[(VC & VC_KV3) ? 10 * vc_block(VC) : 1];
-    uint4* rk = rk_lds + threadIdx.x;
-#else
-    uint4* rk = nullptr;
-#endif
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t gw = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (gw >= nwaves) return;
@@ -647,7 +594,7 @@ __global__ __launch_bounds__(vc_block(VC)) __attribute__((amdgpu_waves_per_eu(vc
     }
     const uint32_t sel = (uint32_t)min<uint64_t>(cand, (uint64_t)(L.nlists - 1));
     uint32_t mic[4];
-    eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic, rk);
+    eapol_mic<VC, false>(L, pool, K, atts[L.list_off + sel * L.natt + a], te, mic);
     const bool found = active && mic_match(L, mic);
     if (found && first_hit)
         __hip_atomic_fetch_min(first_hit + sg.line, (uint32_t)cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -695,22 +642,14 @@ hipError_t launch_pbkdf2_plain(const uint32_t* mid, uint32_t cap, uint32_t base,
 // nothing).  On gfx950 a wave whose EXEC mask is partial runs a dependent VALU chain 18 % slower alone on its SIMD
 // and 39 % slower with 8 such waves on the chip, at the same shader clock (tools/clock_idle.hip,
 // profiles/r04/small_call/clock_lanes.jsonl); a one-key server call took 9.6-11.8 ms against 8.3 ms for 202 keys.
-// Padded, it takes 8.4 ms.  DWPA_LONE_PAD = 0 (off) / 64 (default: whole waves) / 256 (whole workgroups) for A/B.
-static uint32_t lone_pad() {
-    static const uint32_t pad = [] {
-        const char* e = getenv("DWPA_LONE_PAD");
-        const int v = e ? atoi(e) : 64;
-        return (uint32_t)(v == 64 || v == 256 ? v : 0);
-    }();
-    return pad;
-}
+// Padded, it takes 8.4 ms.
+constexpr uint32_t LONE_PAD = 64;
 
 hipError_t launch_pbkdf2_ms_plain(const uint32_t* mid, uint32_t cap, uint32_t count, const uint32_t* pool,
                                   const uint32_t* sref, uint32_t* pmk, hipStream_t s) {
     count = min(count, cap);
     if (count == 0) return hipSuccess;
-    const uint32_t pad = lone_pad();
-    const uint32_t launch = pad ? (count + pad - 1) / pad * pad : count;
+    const uint32_t launch = (count + LONE_PAD - 1) / LONE_PAD * LONE_PAD;
     hipLaunchKernelGGL(k_pbkdf2_ms, dim3(cdiv(launch, 256), 2), dim3(256), 0, s, mid, cap, launch, pool, sref, pmk,
                        count);
     return hipGetLastError();
@@ -745,8 +684,6 @@ hipError_t launch_set_flag(uint32_t* flag, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t set_check_prio(uint32_t prio) { return hipMemcpyToSymbol(HIP_SYMBOL(g_check_prio), &prio, 4); }
-hipError_t set_kv3_prio(uint32_t prio) { return hipMemcpyToSymbol(HIP_SYMBOL(g_kv3_prio), &prio, 4); }
 
 hipError_t launch_set_pmk(uint32_t* pmk, uint32_t cap, uint32_t slot, const uint32_t w[8], hipStream_t s) {
     uint4 lo = make_uint4(w[0], w[1], w[2], w[3]), hi = make_uint4(w[4], w[5], w[6], w[7]);

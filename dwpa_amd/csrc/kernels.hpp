@@ -56,11 +56,6 @@ hipError_t launch_pbkdf2_ms_tail(const uint32_t* mid, uint32_t cap, uint32_t cou
                                  const uint32_t* sref, uint32_t* pmk, uint32_t* flag, uint32_t prio,
                                  uint32_t* raised, hipStream_t s);
 hipError_t launch_set_flag(uint32_t* flag, hipStream_t s);
-// Wave priority (0..3) of the check path's post-derive kernels (PMK gather, EAPOL key states, verifies) on the
-// current device; the hit copy-out always runs at 3.
-hipError_t set_check_prio(uint32_t prio);
-// Wave priority of the keyver-3 verify kernels (EAPOL key states, attempt- and key-parallel verify).
-hipError_t set_kv3_prio(uint32_t prio);
 constexpr uint32_t GATHER_CALLER = 0x80000000u;
 hipError_t launch_gather_pmk(const uint32_t* upmk, uint32_t ucap, const uint32_t* cpmk, const uint32_t* src,
                              uint32_t n, uint32_t* pmk, uint32_t cap, hipStream_t s);

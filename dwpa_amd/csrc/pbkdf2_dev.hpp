@@ -39,25 +39,6 @@ __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t
 #pragma unroll
     for (int k = 0; k < 5; k++) t[k] = u[k];
     if constexpr (!PRIO) {
-#if DWPA_PBKDF2_UNROLL2
-        // two iterations per loop trip (4094 = 2 x 2047), then the last one: the issue pass sees one block of 4
-        // compressions
-#pragma unroll 1
-        for (int it = 1; it < 4095; it += 2) {
-            sha1_84(MI, u, x);
-            sha1_84(MO, x, u);
-#pragma unroll
-            for (int k = 0; k < 5; k++) t[k] ^= u[k];
-            sha1_84(MI, u, x);
-            sha1_84(MO, x, u);
-#pragma unroll
-            for (int k = 0; k < 5; k++) t[k] ^= u[k];
-        }
-        sha1_84(MI, u, x);
-        sha1_84(MO, x, u);
-#pragma unroll
-        for (int k = 0; k < 5; k++) t[k] ^= u[k];
-#else
 #pragma unroll 1
         for (int it = 1; it < 4096; it++) {
             sha1_84(MI, u, x);
@@ -65,7 +46,6 @@ __device__ __forceinline__ void pbkdf2_lane(const uint32_t hi[5], const uint32_t
 #pragma unroll
             for (int k = 0; k < 5; k++) t[k] ^= u[k];
         }
-#endif
     } else {
         __builtin_amdgcn_s_setprio(3);
         int it = 1;

@@ -1,8 +1,9 @@
 // pbkdf2_module.cpp -- loads the issue-pass PBKDF2 code object (embedded at build time) on each device and launches
 // it.  Launches with at most one wave per SIMD (small server checks: C1) take the hipcc-scheduled k_pbkdf2 instead:
 // the issue pass's s_nops only pay when several waves share a SIMD, and a lone wave runs its stream 1.55x slower
-// with them (profiles/r01/partial_round/).  DWPA_PBKDF2_PLAIN=1 forces the plain kernel everywhere and
-// DWPA_PBKDF2_ISSUE=1 the issue-pass kernel everywhere (A/B; identical results).
+// with them (profiles/r01/partial_round/).  DWPA_PBKDF2_PLAIN=1 runs the plain kernel everywhere (a deployment's
+// fallback to the compiler's own schedule); DWPA_PBKDF2_ISSUE=1 the issue-pass kernel everywhere (the test suite's
+// switch to run the small parity cases on it).  The results are identical.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -42,25 +43,10 @@ static bool force_issue() {
 // there the waves of a SIMD otherwise finish one after another and the last runs alone.  Measured on MI355X
 // (profiles/r02/prio/): 6 waves/SIMD 43.0 -> 40.7 ms, 4 waves 29.4 -> 26.5 ms, the C5 call 58.0 -> 54.6 ms; level on
 // 16-round launches (C2 844.3 vs 844.3 ms), so multi-round launches keep the plain-priority kernel.
-// DWPA_PBKDF2_PRIO=0/1 forces it off/on (A/B).
-static bool use_prio(const Fns& fn, uint64_t pmks) {
-    static const int forced = [] {
-        const char* e = getenv("DWPA_PBKDF2_PRIO");
-        return e && *e ? (*e != '0' ? 1 : 0) : -1;
-    }();
-    if (forced >= 0) return forced == 1;
-    return 2 * pmks <= 8 * fn.level_lanes;
-}
+static bool use_prio(const Fns& fn, uint64_t pmks) { return 2 * pmks <= 8 * fn.level_lanes; }
 
-// Workgroup size of the issue-pass launches (DWPA_PBKDF2_WG = 64/128/256, default 256): partial-round experiments.
-static uint32_t wg_size() {
-    static const uint32_t wg = [] {
-        const char* e = getenv("DWPA_PBKDF2_WG");
-        const int v = e ? atoi(e) : 256;
-        return (uint32_t)((v == 64 || v == 128) ? v : 256);
-    }();
-    return wg;
-}
+// Workgroup size of the issue-pass grid launches (64 and 128 measured level or slower on partial rounds).
+constexpr uint32_t WG = 256;
 
 static hipError_t tuned_functions(Fns* fn) {
     int dev = 0;
@@ -94,15 +80,7 @@ static bool lone_waves(const Fns& fn, uint64_t pmks) { return !force_issue() && 
 
 // Multi-round scan launches (one ESSID, ESSID groups) run as work queues: one resident round of 8 waves per SIMD
 // taking 64-lane items from a counter, so a faster XCD takes more of them.  Measured (profiles/r02/queue/): C2
-// 4.898 -> 4.907 M PMK/s, C4 4.980 -> 4.996 M.  DWPA_PBKDF2_QUEUE=0 switches back to grid launches (A/B).
-static bool use_queue() {
-    static const bool q = [] {
-        const char* e = getenv("DWPA_PBKDF2_QUEUE");
-        return !(e && *e == '0');
-    }();
-    return q;
-}
-
+// 4.898 -> 4.907 M PMK/s, C4 4.980 -> 4.996 M.
 hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint32_t count, const uint32_t* counter,
                          const uint32_t* salt, uint32_t nsalt, uint32_t* pmk, hipStream_t s, uint32_t* work) {
     if (count == 0) return hipSuccess;
@@ -114,7 +92,7 @@ hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint3
     if (lone_waves(fn, std::min<uint64_t>(count, cap > base ? cap - base : 0)))
         return launch_pbkdf2_plain(mid, cap, base, count, counter, salt, nsalt, pmk, s);
     const uint64_t pmks = std::min<uint64_t>(count, cap > base ? cap - base : 0);
-    if (work && use_queue() && !use_prio(fn, pmks)) {
+    if (work && !use_prio(fn, pmks)) {
         // one resident round (8 waves per SIMD) that drains the item counter
         e = hipMemsetAsync(work, 0, 4, s);
         if (e != hipSuccess) return e;
@@ -125,7 +103,7 @@ hipError_t launch_pbkdf2(const uint32_t* mid, uint32_t cap, uint32_t base, uint3
     }
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&base, (void*)&count, (void*)&counter,
                     (void*)&salt, (void*)&nsalt, (void*)&pmk};
-    const uint32_t wg = wg_size();
+    const uint32_t wg = WG;
     return hipModuleLaunchKernel(use_prio(fn, std::min<uint64_t>(count, cap > base ? cap - base : 0)) ? fn.one_p : fn.one,
                                  (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args,
                                  nullptr);
@@ -140,7 +118,7 @@ hipError_t launch_pbkdf2_ms(const uint32_t* mid, uint32_t cap, uint32_t count, c
     if (e != hipSuccess) return e;
     if (lone_waves(fn, std::min(count, cap))) return launch_pbkdf2_ms_plain(mid, cap, count, pool, sref, pmk, s);
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&count, (void*)&pool, (void*)&sref, (void*)&pmk};
-    const uint32_t wg = wg_size();
+    const uint32_t wg = WG;
     return hipModuleLaunchKernel(use_prio(fn, std::min(count, cap)) ? fn.ms_p : fn.ms, (count + wg - 1) / wg, 2, 1, wg, 1, 1, 0, s, args,
                                  nullptr);
 }
@@ -157,7 +135,7 @@ hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* c
     const uint64_t lanes = (uint64_t)ngroups * cap;
     if (lanes > 0xffffffffull - 255) return hipErrorInvalidValue;
     if (lone_waves(fn, lanes)) return launch_pbkdf2_mg_plain(mid, cap, counter, ngroups, salt, gsalt, pmk, pstride, s);
-    if (work && use_queue() && !use_prio(fn, lanes)) {
+    if (work && !use_prio(fn, lanes)) {
         e = hipMemsetAsync(work, 0, 4, s);
         if (e != hipSuccess) return e;
         void* qargs[] = {(void*)&mid, (void*)&cap, (void*)&counter, (void*)&ngroups, (void*)&salt, (void*)&gsalt,
@@ -167,7 +145,7 @@ hipError_t launch_pbkdf2_mg(const uint32_t* mid, uint32_t cap, const uint32_t* c
     }
     void* args[] = {(void*)&mid, (void*)&cap, (void*)&counter, (void*)&ngroups, (void*)&salt, (void*)&gsalt,
                     (void*)&pmk, (void*)&pstride};
-    const uint32_t wg = wg_size();
+    const uint32_t wg = WG;
     return hipModuleLaunchKernel(use_prio(fn, lanes) ? fn.mg_p : fn.mg, (uint32_t)((lanes + wg - 1) / wg), 2, 1, wg, 1, 1, 0, s,
                                  args, nullptr);
 }

@@ -163,7 +163,7 @@ int dwpa_check_batch(const dwpa_job *jobs, size_t njobs, dwpa_result *out, int *
  * (ABI 4), its jobs, the non-null keys of usable lines (slots), the (ESSID, key) PMKs derived after deduplication (on
  * the host backend: by it; the tail fields below stay 0 there), how many of those the tail launch
  * derived (the remainder under one wave per SIMD, run beside the head at low wave priority), the tail's waves and
- * how many of them saw the head end and raised their priority (DWPA_TAIL_PRIO), the hits, and the call's wall time.
+ * how many of them saw the head end and raised their priority, the hits, and the call's wall time.
  * Returns 0, or DWPA_E_ARG before any check call in this thread. */
 typedef struct {
     uint32_t jobs;

@@ -6,7 +6,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/legs}
 mkdir -p $OUT
-LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat c2files c2files_warm c3files c3files_server c3files_server_full expand"}
+LEGS=${LEGS:-"peak c2 c4 c4strong c3 c5 c5k2 c1 c1lat host c2files c2files_node8 c3files c3files_server c3files_server_full expand"}
 for leg in $LEGS; do
   case $leg in
     peak)    OUT=$OUT/peak tools/regen_peak.sh > /dev/null ;;
@@ -20,10 +20,13 @@ for leg in $LEGS; do
     c5k2)    timeout -k 10 240 python3 bench.py --workload c5 --callers 2 --steps 20 --warmup 3 --no-cpu-baseline \
                > $OUT/c5k2.json 2> $OUT/c5k2.err ;;
     c1)      timeout -k 10 240 python3 bench.py --workload c1 --steps 20 --warmup 3 > $OUT/c1.json 2> $OUT/c1.err ;;
-    c2files) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c2files --steps 1 --warmup 0 \
+    host)    timeout -k 10 240 python3 tools/host_backend_bench.py > $OUT/host.json 2> $OUT/host.err ;;
+    # the client's node mode: one process over every visible device (--gpus = their count), dictionary + rule pass
+    c2files) timeout -k 10 600 python3 bench.py --workload c2files --gpus ${NODE_GPUS:-1} --steps 1 --warmup 1 \
                > $OUT/c2files.json 2> $OUT/c2files.err ;;
-    c2files_warm) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c2files --steps 1 --warmup 1 \
-               > $OUT/c2files_warm.json 2> $OUT/c2files_warm.err ;;
+    # its 8-worker rehearsal on one GPU (an 8-GPU node's worker count and shared feed, not its throughput)
+    c2files_node8) DWPA_CRACK_SHARDS_PER_DEVICE=8 timeout -k 10 600 python3 bench.py --workload c2files --steps 1 \
+               --warmup 1 > $OUT/c2files_node8.json 2> $OUT/c2files_node8.err ;;
     c3files) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --steps 2 --warmup 0 \
                > $OUT/c3files.json 2> $OUT/c3files.err ;;
     c3files_server) DWPA_TRACE=1 timeout -k 10 400 python3 bench.py --workload c3files --rules-set server --steps 2 \
