@@ -214,26 +214,30 @@ struct Derive {
     uint32_t group;
 };
 
-// PBKDF2 of every entry of `dv` into pmk[i] (big-endian words), over up to host_threads() threads: chunks of
-// PBKDF2_CHAINS / 2 keys handed out through an atomic counter, so uneven keys (a 64 KiB one) do not stall a part.
+// PBKDF2 of every entry of `dv` into pmk[i] (big-endian words), over up to host_threads() threads: chunks handed
+// out through an atomic counter, so uneven keys (a 64 KiB one) do not stall a part.  A chunk is the fastest path's
+// unit (16 keys with AVX-512) when there are enough keys for every thread of the pool to take one, else
+// PBKDF2_CHAINS / 2 keys (SHA-NI chains spread over the threads: the latency of a call of a few keys).
 void derive_all(const std::vector<Derive>& dv, const std::vector<std::vector<uint32_t>>& salt,
                 const std::vector<uint32_t>& nblk, std::vector<std::array<uint32_t, 8>>& pmk) {
-    const size_t per = PBKDF2_CHAINS / 2, nchunks = (dv.size() + per - 1) / per;
+    const size_t wide = pbkdf2_keys_per_unit(), small = PBKDF2_CHAINS / 2;
+    const size_t per = dv.size() >= wide * host_threads_for(SIZE_MAX, 1) ? wide : small;
+    const size_t nchunks = (dv.size() + per - 1) / per;
     pmk.resize(dv.size());
     std::atomic<size_t> next{0};
     host_parallel(host_threads_for(nchunks, 1), [&](size_t) {
-        uint32_t mid[PBKDF2_CHAINS / 2][10];
-        const uint32_t* sp[PBKDF2_CHAINS / 2];
-        uint32_t nb[PBKDF2_CHAINS / 2];
+        std::vector<std::array<uint32_t, 10>> mid(per);
+        std::vector<const uint32_t*> sp(per);
+        std::vector<uint32_t> nb(per);
         for (size_t c; (c = next.fetch_add(1, std::memory_order_relaxed)) < nchunks;) {
             const size_t i0 = c * per, n = std::min(per, dv.size() - i0);
             for (size_t k = 0; k < n; k++) {
                 const Derive& d = dv[i0 + k];
-                hmac_sha1_mid(d.key, d.len, mid[k], mid[k] + 5);
+                hmac_sha1_mid(d.key, d.len, mid[k].data(), mid[k].data() + 5);
                 sp[k] = salt[d.group].data();
                 nb[k] = nblk[d.group];
             }
-            pbkdf2_sha1(n, mid, sp, nb, (uint32_t(*)[8])pmk[i0].data());
+            pbkdf2_sha1(n, (const uint32_t(*)[10])mid.data(), sp.data(), nb.data(), (uint32_t(*)[8])pmk[i0].data());
         }
     });
 }

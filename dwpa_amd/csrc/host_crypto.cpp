@@ -1,9 +1,11 @@
 // host_crypto.cpp -- the host backend's SHA-1 / SHA-256 / MD5 / AES-128 and PBKDF2 (see host_crypto.hpp).
 //
 // Instruction-set paths: SHA-NI (sha1rnds4 / sha1nexte / sha1msg1/2, sha256rnds2 / sha256msg1/2) and AES-NI, in SSE
-// registers.  A SHA-1 compression under SHA-NI is a chain of 20 dependent sha1rnds4, so one PBKDF2 chain is bound by
-// their latency; pbkdf2_sha1 therefore steps PBKDF2_CHAINS independent chains (two output blocks of each key) in
-// lock step, and the out-of-order core overlaps them.  The scalar paths are the FIPS 180-4 / RFC 1321 / FIPS 197
+// registers, and AVX-512F for PBKDF2 over many keys.  A SHA-1 compression under SHA-NI is a chain of 20 dependent
+// sha1rnds4, so one PBKDF2 chain is bound by their latency; pbkdf2_sha1 steps PBKDF2_CHAINS independent chains (two
+// output blocks of each key) in lock step, and the out-of-order core overlaps them -- the path for a call of a few
+// keys.  With many keys, 16 chains share each 512-bit register (vprold rotates, vpternlogd round functions) and two
+// such groups run in lock step: the throughput path.  The scalar paths are the FIPS 180-4 / RFC 1321 / FIPS 197
 // definitions and serve CPUs without the extensions (and DWPA_HOST_SIMD=0).
 #include "host_crypto.hpp"
 
@@ -11,6 +13,8 @@
 #include <immintrin.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 namespace dwpa {
 namespace hostc {
@@ -201,6 +205,7 @@ static void aes128_encrypt_scalar(const Aes128Key& ks, const uint8_t in[16], uin
 // =========================================================================================================
 #define DWPA_SHA_TARGET __attribute__((target("sha,sse4.1,ssse3")))
 #define DWPA_AES_TARGET __attribute__((target("aes,sse4.1")))
+#define DWPA_AVX512_TARGET __attribute__((target("avx512f")))
 
 // N SHA-1 compressions in lock step.  State in SHA-NI form: abcd = {A, B, C, D} from the high lane down, e = {E, 0,
 // 0, 0}; message m[n][q] = words 4q..4q+3, the first in the high lane.  Round group g (4 rounds) takes e_g = E + W for
@@ -314,6 +319,124 @@ DWPA_AES_TARGET static void aes128_encrypt_ni(const Aes128Key& ks, const uint8_t
     _mm_storeu_si128((__m128i*)out, aes128_enc_ni((const __m128i*)ks.rk, _mm_loadu_si128((const __m128i*)in)));
 }
 
+// SHA-1 over 16 lanes per register (AVX-512F), G independent groups in lock step: st[g][k] += compress(st[g], w[g])
+// with w[g] the 16 message words of every lane (consumed by the in-place schedule).  vprold rotates, vpternlogd
+// computes Ch (0xCA), parity (0x96) and Maj (0xE8) in one op each; the loop over t unrolls, so the round function and
+// the schedule's start are resolved at compile time and constant message words fold.
+template <int G>
+DWPA_AVX512_TARGET __attribute__((always_inline)) static inline void sha1x16(__m512i (*st)[5], __m512i (*w)[16]) {
+    __m512i a[G], b[G], c[G], d[G], e[G];
+    for (int g = 0; g < G; g++) {
+        a[g] = st[g][0];
+        b[g] = st[g][1];
+        c[g] = st[g][2];
+        d[g] = st[g][3];
+        e[g] = st[g][4];
+    }
+#pragma unroll
+    for (int t = 0; t < 80; t++) {
+        const __m512i K = _mm512_set1_epi32((int)(t < 20 ? 0x5a827999u : t < 40 ? 0x6ed9eba1u : t < 60 ? 0x8f1bbcdcu
+                                                                                                   : 0xca62c1d6u));
+        for (int g = 0; g < G; g++) {
+            __m512i wt = w[g][t & 15];
+            if (t >= 16) {
+                wt = _mm512_rol_epi32(_mm512_xor_si512(_mm512_ternarylogic_epi32(w[g][(t - 3) & 15], w[g][(t - 8) & 15],
+                                                                                 w[g][(t - 14) & 15], 0x96),
+                                                       wt),
+                                      1);
+                w[g][t & 15] = wt;
+            }
+            const __m512i f = t < 20 ? _mm512_ternarylogic_epi32(b[g], c[g], d[g], 0xca)
+                            : (t < 40 || t >= 60) ? _mm512_ternarylogic_epi32(b[g], c[g], d[g], 0x96)
+                                                  : _mm512_ternarylogic_epi32(b[g], c[g], d[g], 0xe8);
+            const __m512i x = _mm512_add_epi32(_mm512_add_epi32(_mm512_rol_epi32(a[g], 5), f),
+                                               _mm512_add_epi32(e[g], _mm512_add_epi32(K, wt)));
+            e[g] = d[g];
+            d[g] = c[g];
+            c[g] = _mm512_rol_epi32(b[g], 30);
+            b[g] = a[g];
+            a[g] = x;
+        }
+    }
+    for (int g = 0; g < G; g++) {
+        st[g][0] = _mm512_add_epi32(st[g][0], a[g]);
+        st[g][1] = _mm512_add_epi32(st[g][1], b[g]);
+        st[g][2] = _mm512_add_epi32(st[g][2], c[g]);
+        st[g][3] = _mm512_add_epi32(st[g][3], d[g]);
+        st[g][4] = _mm512_add_epi32(st[g][4], e[g]);
+    }
+}
+
+// U_2..U_4096 of 16 G chains, lane l of group g = chain 16 g + l (the same message shape as pbkdf2_loop_ni).
+template <int G>
+DWPA_AVX512_TARGET static void pbkdf2_loop_avx512(const uint32_t* const* mid, uint32_t* const* t) {
+    __m512i ih[G][5], oh[G][5], u[G][5], T[G][5];
+    alignas(64) uint32_t lanes[16];
+    for (int g = 0; g < G; g++)
+        for (int k = 0; k < 5; k++) {
+            for (int l = 0; l < 16; l++) lanes[l] = mid[16 * g + l][k];
+            ih[g][k] = _mm512_load_si512(lanes);
+            for (int l = 0; l < 16; l++) lanes[l] = mid[16 * g + l][5 + k];
+            oh[g][k] = _mm512_load_si512(lanes);
+            for (int l = 0; l < 16; l++) lanes[l] = t[16 * g + l][k];
+            u[g][k] = T[g][k] = _mm512_load_si512(lanes);
+        }
+    const __m512i pad = _mm512_set1_epi32((int)0x80000000u), zero = _mm512_setzero_si512(),
+                  len = _mm512_set1_epi32((64 + 20) * 8);
+    for (int it = 1; it < 4096; it++) {
+        __m512i st[G][5], w[G][16];
+        for (int g = 0; g < G; g++) {
+            for (int k = 0; k < 5; k++) {
+                st[g][k] = ih[g][k];
+                w[g][k] = u[g][k];
+            }
+            w[g][5] = pad;
+            for (int k = 6; k < 15; k++) w[g][k] = zero;
+            w[g][15] = len;
+        }
+        sha1x16<G>(st, w);
+        for (int g = 0; g < G; g++) {
+            for (int k = 0; k < 5; k++) {
+                w[g][k] = st[g][k];
+                st[g][k] = oh[g][k];
+            }
+            w[g][5] = pad;
+            for (int k = 6; k < 15; k++) w[g][k] = zero;
+            w[g][15] = len;
+        }
+        sha1x16<G>(st, w);
+        for (int g = 0; g < G; g++)
+            for (int k = 0; k < 5; k++) {
+                u[g][k] = st[g][k];
+                T[g][k] = _mm512_xor_si512(T[g][k], st[g][k]);
+            }
+    }
+    for (int g = 0; g < G; g++)
+        for (int k = 0; k < 5; k++) {
+            _mm512_store_si512(lanes, T[g][k]);
+            for (int l = 0; l < 16; l++) t[16 * g + l][k] = lanes[l];
+        }
+}
+
+// One 16-lane compression of word-form states and blocks (the self-test's view of sha1x16).
+DWPA_AVX512_TARGET static void sha1x16_words(uint32_t st[16][5], const uint32_t w[16][16]) {
+    __m512i s[1][5], m[1][16];
+    alignas(64) uint32_t lanes[16];
+    for (int k = 0; k < 5; k++) {
+        for (int l = 0; l < 16; l++) lanes[l] = st[l][k];
+        s[0][k] = _mm512_load_si512(lanes);
+    }
+    for (int k = 0; k < 16; k++) {
+        for (int l = 0; l < 16; l++) lanes[l] = w[l][k];
+        m[0][k] = _mm512_load_si512(lanes);
+    }
+    sha1x16<1>(s, m);
+    for (int k = 0; k < 5; k++) {
+        _mm512_store_si512(lanes, s[0][k]);
+        for (int l = 0; l < 16; l++) st[l][k] = lanes[l];
+    }
+}
+
 // =========================================================================================================
 // dispatch + self-test
 // =========================================================================================================
@@ -337,6 +460,21 @@ static bool selftest(const Caps& k) {
             sha256_scalar(a, w);
             sha256_ni(b, w);
             if (memcmp(a, b, 32)) return false;
+        }
+        if (k.avx512) {
+            uint32_t s16[16][5], w16[16][16], ref[5];
+            for (int l = 0; l < 16; l++) {
+                for (int i = 0; i < 5; i++) s16[l][i] = rnd();
+                for (int i = 0; i < 16; i++) w16[l][i] = rnd();
+            }
+            uint32_t keep[16][5];
+            memcpy(keep, s16, sizeof keep);
+            sha1x16_words(s16, w16);
+            for (int l = 0; l < 16; l++) {
+                memcpy(ref, keep[l], 20);
+                sha1_scalar(ref, w16[l]);
+                if (memcmp(ref, s16[l], 20)) return false;
+            }
         }
         if (k.aes_ni) {
             uint8_t key[16], in[16], o1[16], o2[16];
@@ -365,13 +503,27 @@ static Caps detect() {
         sse41 = (c >> 19) & 1;
         k.aes_ni = ((c >> 25) & 1) && sse41;
     }
-    if (__get_cpuid_count(7, 0, &a, &b, &c, &d)) k.sha_ni = ((b >> 29) & 1) && sse41 && ssse3;
-    Caps one = k;
-    one.aes_ni = false;  // test each extension on its own, so one failing leaves the other usable
-    if (k.sha_ni && !selftest(one)) k.sha_ni = false;
-    one = k;
-    one.sha_ni = false;
-    if (k.aes_ni && !selftest(one)) k.aes_ni = false;
+    bool osxsave = false;
+    if (__get_cpuid(1, &a, &b, &c, &d)) osxsave = (c >> 27) & 1;
+    if (__get_cpuid_count(7, 0, &a, &b, &c, &d)) {
+        k.sha_ni = ((b >> 29) & 1) && sse41 && ssse3;
+        // AVX-512F, with the OS saving the opmask and all of the ZMM state (XCR0 bits 1, 2, 5, 6, 7)
+        if (((b >> 16) & 1) && osxsave) {
+            uint32_t lo, hi;
+            __asm__("xgetbv" : "=a"(lo), "=d"(hi) : "c"(0));
+            k.avx512 = (lo & 0xe6u) == 0xe6u;
+        }
+    }
+    // test each extension on its own, so one failing leaves the others usable
+    const Caps found = k;
+    for (int x = 0; x < 3; x++) {
+        Caps one;
+        bool* have = x == 0 ? &k.sha_ni : x == 1 ? &k.aes_ni : &k.avx512;
+        if (!*have) continue;
+        (x == 0 ? one.sha_ni : x == 1 ? one.aes_ni : one.avx512) = true;
+        if (!selftest(one)) *have = false;
+    }
+    (void)found;
     return k;
 }
 
@@ -548,27 +700,51 @@ DWPA_SHA_TARGET static void pbkdf2_loop_ni(const uint32_t* const* mid, uint32_t*
     }
 }
 
+size_t pbkdf2_keys_per_unit() { return caps().avx512 ? PBKDF2_WIDE / 2 : PBKDF2_CHAINS / 2; }
+
 void pbkdf2_sha1(size_t n, const uint32_t (*mid)[10], const uint32_t* const* salt, const uint32_t* nblk,
                  uint32_t (*pmk)[8]) {
-    const bool ni = caps().sha_ni;
-    constexpr int C = PBKDF2_CHAINS;
-    // chain 2i + b = output block b + 1 of key i; chains run C at a time
-    uint32_t T[C][5];
-    const uint32_t* cm[C];
-    uint32_t* ct[C];
-    for (size_t c0 = 0; c0 < 2 * n; c0 += C) {
-        const int nc = (int)((2 * n - c0) < (size_t)C ? 2 * n - c0 : C);
+    const Caps& k = caps();
+    // chain 2i + b = output block b + 1 of key i
+    uint32_t T[PBKDF2_WIDE][5];
+    const uint32_t* cm[PBKDF2_WIDE];
+    uint32_t* ct[PBKDF2_WIDE];
+    const size_t chains = 2 * n;
+    auto prep = [&](size_t c0, int nc) {
         for (int c = 0; c < nc; c++) {
             const size_t i = (c0 + c) >> 1;
-            const int b = (int)((c0 + c) & 1);
-            pbkdf2_u1(mid[i], salt[i], nblk[i], b, T[c]);
+            pbkdf2_u1(mid[i], salt[i], nblk[i], (int)((c0 + c) & 1), T[c]);
             cm[c] = mid[i];
             ct[c] = T[c];
         }
-        if (!ni) {
+    };
+    auto store = [&](size_t c0, int nc) {
+        for (int c = 0; c < nc; c++) {
+            const size_t i = (c0 + c) >> 1;
+            if ((c0 + c) & 1) memcpy(pmk[i] + 5, T[c], 12);  // T_2: the PMK's last 12 bytes
+            else memcpy(pmk[i], T[c], 20);
+        }
+    };
+    size_t c0 = 0;
+    if (k.avx512) {
+        for (; chains - c0 >= PBKDF2_WIDE; c0 += PBKDF2_WIDE) {
+            prep(c0, PBKDF2_WIDE);
+            pbkdf2_loop_avx512<PBKDF2_WIDE / 16>(cm, ct);
+            store(c0, PBKDF2_WIDE);
+        }
+        if (chains - c0 >= 16) {
+            prep(c0, 16);
+            pbkdf2_loop_avx512<1>(cm, ct);
+            store(c0, 16);
+            c0 += 16;
+        }
+    }
+    constexpr int C = PBKDF2_CHAINS;
+    for (; c0 < chains; c0 += C) {
+        const int nc = (int)std::min<size_t>(chains - c0, C);
+        prep(c0, nc);
+        if (!k.sha_ni) {
             for (int c = 0; c < nc; c++) pbkdf2_loop_scalar(cm[c], T[c]);
-        } else if (nc == C) {
-            pbkdf2_loop_ni<C>(cm, ct);
         } else {
             for (int c = nc; c < C; c++) {  // a partial last group: pad with copies of chain 0 (results dropped)
                 memcpy(T[c], T[0], 20);
@@ -578,11 +754,7 @@ void pbkdf2_sha1(size_t n, const uint32_t (*mid)[10], const uint32_t* const* sal
             if (nc <= 2) pbkdf2_loop_ni<2>(cm, ct);
             else pbkdf2_loop_ni<C>(cm, ct);
         }
-        for (int c = 0; c < nc; c++) {
-            const size_t i = (c0 + c) >> 1;
-            if ((c0 + c) & 1) memcpy(pmk[i] + 5, T[c], 12);  // T_2: the PMK's last 12 bytes
-            else memcpy(pmk[i], T[c], 20);
-        }
+        store(c0, nc);
     }
 }
 

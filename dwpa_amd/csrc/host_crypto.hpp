@@ -7,6 +7,8 @@
 // scalar path.  The choice is made once per process, after a known-answer self-test of the instruction-set path
 // against the scalar one; DWPA_HOST_SIMD=0 forces the scalar path.
 //
+// PBKDF2 has a third path, AVX-512F (16 lanes per register) for many keys at once.
+//
 // Conventions: SHA-1 / SHA-256 message words and states are big-endian words (the host integers of the bytes read
 // big-endian), MD5's little-endian words, as in the device tables (tables.hpp).
 #pragma once
@@ -17,10 +19,11 @@ namespace dwpa {
 namespace hostc {
 
 struct Caps {
-    bool sha_ni = false;  // SHA-1 and SHA-256 compressions, PBKDF2
+    bool sha_ni = false;  // SHA-1 and SHA-256 compressions, PBKDF2 of a few keys
     bool aes_ni = false;  // AES-128
+    bool avx512 = false;  // PBKDF2 of many keys: 16 chains per 512-bit register (AVX-512F, ZMM state enabled by the OS)
 };
-const Caps& caps();       // detected once (CPUID + self-test); DWPA_HOST_SIMD=0 clears both
+const Caps& caps();       // detected once (CPUID + self-test of each path); DWPA_HOST_SIMD=0 clears all
 
 extern const uint32_t SHA1_IV[5];
 extern const uint32_t SHA256_IV[8];
@@ -46,9 +49,13 @@ void hmac_sha1_mid(const uint8_t* key, size_t len, uint32_t ipad[5], uint32_t op
 
 // PBKDF2-HMAC-SHA1(key, salt, 4096, 32) for n keys.  mid[i] = the key's HMAC-SHA1 midstates (ipad h0..h4, opad
 // h0..h4); salt[i] = its salt blocks as build_salt_blocks (m22000_host.hpp) lays them out, [2][nblk[i]][16] words of
-// ESSID || INT(b) || padding; pmk[i] = the 8 big-endian words of the PMK.  The 4,095 dependent iterations of the
-// two output blocks of up to PBKDF2_CHAINS / 2 keys run interleaved, which is what hides the SHA-NI round latency.
+// ESSID || INT(b) || padding; pmk[i] = the 8 big-endian words of the PMK.  A chain is one output block of one key
+// (4,095 dependent iterations).  With AVX-512, groups of PBKDF2_WIDE chains (16 keys) run as 2 x 16 lanes; the rest
+// (and everything without AVX-512) as PBKDF2_CHAINS SHA-NI chains in lock step, which hides the round latency of one.
 constexpr int PBKDF2_CHAINS = 4;
+constexpr int PBKDF2_WIDE = 32;
+// Keys per call of pbkdf2_sha1 that keep its fastest path busy (the host pool's work unit).
+size_t pbkdf2_keys_per_unit();
 void pbkdf2_sha1(size_t n, const uint32_t (*mid)[10], const uint32_t* const* salt, const uint32_t* nblk,
                  uint32_t (*pmk)[8]);
 

