@@ -326,7 +326,12 @@ static int ensure_init() {
 // Host backend switches (host_check.cpp).  allow_cpu_fallback: dwpa_init's value when set (1 on, -1 off), else
 // DWPA_CPU_FALLBACK=1 from the environment; off by default, so a box without a device says DWPA_E_NODEV unless the
 // caller asked for the host backend.  host_max_pmks: calls of at most this many PMK-equivalents with at least one
-// PBKDF2 derive run on the host (dwpa_init's value, else DWPA_HOST_MAX_PMKS, else 24; <= 0 from either = never).
+// PBKDF2 derive run on the host (dwpa_init's value, else DWPA_HOST_MAX_PMKS, else HOST_PMKS_PER_THREAD per host
+// thread; <= 0 from either = never).  On the MI355X box's EPYC 9575F a host thread derives ~4,700 PMK/s (AVX-512),
+// so the default's 256 PMKs on 16 threads take ~3.4 ms against ~8.5 ms for the GPU's one lone-wave round
+// (profiles/r06/host_bench.json); one thread's 16 take ~3.5 ms.
+static size_t host_threads(size_t n, size_t min_per_thread);
+constexpr double HOST_PMKS_PER_THREAD = 16.0;
 static bool cpu_fallback_on() {
     int v;
     {
@@ -346,7 +351,7 @@ static double host_max_pmks() {
     if (v) return v < 0 ? 0.0 : (double)v;
     const char* e = getenv("DWPA_HOST_MAX_PMKS");
     if (e && *e) return std::max(0.0, atof(e));
-    return 24.0;
+    return HOST_PMKS_PER_THREAD * (double)host_threads(SIZE_MAX, 1);
 }
 // Device-side failures a call may retry on the host backend (allow_cpu_fallback): no device, a HIP error, a device or
 // pinned allocation that failed, a hit buffer that overflowed.

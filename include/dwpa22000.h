@@ -124,7 +124,8 @@ typedef struct {
                                   and at most this many PMK-equivalents (derives + nonce-correction verify work /
                                   16,388 compressions) runs on the host backend, a dwpa_pbkdf2_pmk call of at most this
                                   many keys too; -1 = never (every call on the device); 0 = DWPA_HOST_MAX_PMKS from
-                                  the environment (<= 0: never), else 24.  Until the process's first device call
+                                  the environment (<= 0: never), else 16 per host thread of the library's pool
+                                  (DWPA_HOST_THREADS, default 16: 256).  Until the process's first device call
                                   completes the threshold is 8x this: that call also starts the HIP runtime (0.2-0.7 s
                                   in a fresh PHP-FPM worker) */
     int32_t reserved[1];

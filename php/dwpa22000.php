@@ -256,6 +256,12 @@ function dwpa22000_warmup()
     $ffi = Dwpa22000::ffi();
     $n = $ffi->dwpa_device_count();
     if ($n > 0) {
+        // this one call on the GPU whatever its size (host_max_pmks -1), then the library's routing again (0)
+        $cfg = $ffi->new('dwpa_config');
+        $cfg->struct_size = FFI::sizeof($cfg);
+        $cfg->allow_cpu_fallback = Dwpa22000::CPU_FALLBACK;
+        $cfg->host_max_pmks = -1;
+        $ffi->dwpa_init(FFI::addr($cfg));
         $line = 'WPA*01*' . str_repeat('0', 32) . '*020000000001*020000000002*7761726d7570***';
         $keys = [];
         for ($i = 0; $i < 512; $i++) {
@@ -264,6 +270,8 @@ function dwpa22000_warmup()
         [$arr, $keep, $vals] = Dwpa22000::keys($keys);
         $res = $ffi->new('dwpa_result');
         $ffi->dwpa_check_m22000($line, strlen($line), $arr, count($vals), null, 128, FFI::addr($res));
+        $cfg->host_max_pmks = 0;
+        $ffi->dwpa_init(FFI::addr($cfg));
     }
     return max(0, $n);
 }

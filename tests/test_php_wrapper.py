@@ -114,8 +114,8 @@ def test_pmk_is_never_padded_or_truncated():
 def test_library_routes_and_falls_back_itself():
     """ABI 4: ffi() turns the library's host backend on for a server without a usable GPU (allow_cpu_fallback), and
     check_key_m22000_routed no longer needs the reference's function: it is the library's own routing (small calls on
-    the host backend, the rest on the GPU) under the name earlier deployments call.  dwpa22000_warmup() sends one call
-    big enough for the GPU even before the first device call (8 x the default 24 PMK-equivalents)."""
+    the host backend, the rest on the GPU) under the name earlier deployments call.  dwpa22000_warmup() sends its one
+    call to the GPU (host_max_pmks -1 for that call) and then restores the library's routing (0)."""
     src = _src()
     ffi = _function(src, "ffi")
     assert "$cfg->allow_cpu_fallback = self::CPU_FALLBACK;" in ffi and "$ffi->dwpa_init(FFI::addr($cfg));" in ffi
@@ -126,8 +126,9 @@ def test_library_routes_and_falls_back_itself():
     assert routed.strip() == "return check_key_m22000_gpu($hashline, $keys, $pmk, $nc);"
     assert "$warm" not in src and "COLD_MIN_KEYS" not in src
     warm = _function(src, "dwpa22000_warmup")
-    n = int(re.search(r"\$i < (\d+);", warm).group(1))
-    assert n > 8 * 24
+    off, on = warm.index("$cfg->host_max_pmks = -1;"), warm.index("$cfg->host_max_pmks = 0;")
+    call = warm.index("$ffi->dwpa_check_m22000(")
+    assert off < call < on and warm.count("$ffi->dwpa_init(FFI::addr($cfg));") == 2
     line = "WPA*01*" + "0" * 32 + "*020000000001*020000000002*7761726d7570***"
     assert "$line = 'WPA*01*' . str_repeat('0', 32) . '*020000000001*020000000002*7761726d7570***';" in warm
     import dwpa_amd

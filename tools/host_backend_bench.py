@@ -4,6 +4,10 @@ vs a PMKID / EAPOL keyver 2 / keyver 3 line at nc=128, caller-PMK checks), each 
 oracle (OpenSSL, one PHP request's core).  Every result is checked against the oracle.  Prints one JSON line.
 
     python tools/host_backend_bench.py [--reps N]
+
+PBKDF2 runs on SHA-NI (four chains in lock step) for a few keys per thread and on AVX-512 (32 chains = 16 keys per
+task) once a call has 32 chains per pool thread; the one-thread rows (a child with DWPA_HOST_THREADS=1) give each
+path's per-core rate.
 """
 import argparse
 import json
@@ -21,6 +25,7 @@ os.environ.setdefault("DWPA_HOST_MAX_PMKS", "1000000000")  # every call with a d
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--pbkdf2-only", action="store_true")
     args = ap.parse_args()
     import dwpa_amd
     from dwpa_amd import m22000 as M
@@ -45,12 +50,27 @@ def main():
                            & {"sha_ni", "aes", "avx2", "avx512f"}),
            "host_threads_cap": int(os.environ.get("DWPA_HOST_THREADS", "16"))}
     rows = []
-    for n in (1, 2, 16, 64, 256):
+    threads = max(1, min(out["host_threads_cap"], len(os.sched_getaffinity(0)), os.cpu_count() or 1))
+    wide = "avx512f" in out["flags"] and "sha_ni" in out["flags"]
+    sizes = (2, 32, 256) if args.pbkdf2_only else (1, 2, 16, 64, 256, 512, 1024, 4096)
+    for n in sizes:
         keys = [S.fast_psk(rng) for _ in range(n)]
         ms = med(lambda: dwpa_amd.pbkdf2_pmk(keys, essid), max(3, args.reps // (1 + n // 16)))
         ok = b"".join(dwpa_amd.pbkdf2_pmk(keys, essid)) == O.c_pbkdf2_many(keys, essid, threads=8)
-        rows.append({"call": f"dwpa_pbkdf2_pmk, {n} key(s)", "ms": round(ms, 3), "pmk_per_s": round(n / ms * 1e3),
-                     "same_result": ok})
+        rows.append({"call": f"dwpa_pbkdf2_pmk, {n} key(s)", "threads": threads, "ms": round(ms, 3),
+                     "pmk_per_s": round(n / ms * 1e3),
+                     "path": "avx512" if wide and 2 * n >= 32 * threads else "sha_ni" if "sha_ni" in out["flags"]
+                     else "scalar", "same_result": ok})
+    if args.pbkdf2_only:
+        out["rows"] = rows
+        print(json.dumps(out))
+        sys.exit(0 if all(r["same_result"] for r in rows) else 3)
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--pbkdf2-only", "--reps", str(args.reps)],
+                       env=dict(os.environ, DWPA_HOST_THREADS="1"), capture_output=True, text=True, timeout=300)
+    if r.returncode not in (0, 3):
+        raise SystemExit(f"one-thread child failed: {r.stderr[-2000:]}")
+    rows += json.loads(r.stdout)["rows"]
     psk = S.fast_psk(rng)
     pmk = S.pmk(psk, essid)
     lines = {"pmkid": S.pmkid_line(psk, essid, apm, sta),
