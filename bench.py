@@ -160,6 +160,9 @@ def parse():
     ap.add_argument("--cold-role", choices=["parent", "worker", "context"], default="parent",
                     help=argparse.SUPPRESS)  # c1cold: the child processes the parent starts
     ap.add_argument("--cold-id", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--cold-warmup", action="store_true",
+                    help="c1cold workers start the HIP runtime before their first call (dwpa22000_warmup()'s model) "
+                         "instead of the PHP wrapper's default (dwpa_init with the host backend allowed, no probe)")
     ap.add_argument("--cold-k", default="4,8,16",
                     help="c1cold: concurrent worker counts (each a fresh process; the box allows 16 GPU processes)")
     ap.add_argument("--rules-set", choices=["wpa", "server"], default="wpa",
@@ -1094,12 +1097,15 @@ def main_latency(args, world, rank, local):
                     S.eapol_line(psk, e2, a2, s2, an2, sn2, kv, 37 if hit else 0, "LE", rng=rng))
             pmk = S.pmk(psk, e2) if use_true else (zpmk if site.startswith("zero") else S.pmk(S.fast_psk(rng), e2))
             keys = [psk if key is None else key]
-            gpu_ms, got = timed(lambda: dwpa_amd.check_key_m22000(line, keys, pmk, nc), reps)
+            lib_ms, got, backend = routed(lambda: dwpa_amd.check_key_m22000(line, keys, pmk, nc), reps)
+            gpu_ms, got_dev = device_only(lambda: dwpa_amd.check_key_m22000(line, keys, pmk, nc), reps)
             cpu_ms, exp = timed(lambda: O.c_check_key_m22000(line, keys, pmk, nc), reps)
             rows.append({"call": f"{site}, {kind}, caller PMK, nc={nc}, {'hit' if hit else 'miss'}", "keys": 1,
                          "caller_pmk": True, "nc": nc, "hit": bool(got),
+                         "lib_ms_per_call": round(lib_ms, 3), "lib_backend": BACKENDS[backend],
                          "gpu_ms_per_call": round(gpu_ms, 3), "cpu_1core_ms_per_call": round(cpu_ms, 3),
-                         "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp and bool(got) == hit})
+                         "lib_over_cpu": round(lib_ms / cpu_ms, 3), "gpu_over_cpu": round(gpu_ms / cpu_ms, 3),
+                         "same_result": got == exp and got_dev == exp and bool(got) == hit})
     # one crack's propagation over 16 sibling nets as a single dwpa_check_batch (the batched snippet of INTEGRATION.md)
     jobs = []
     for i in range(16):
@@ -1109,15 +1115,19 @@ def main_latency(args, world, rank, local):
                 S.eapol_line(psk, e2, a2, s2, an2, sn2, 2 + (i % 2), (i % 5) - 2, "BE", rng=rng))
         jobs.append((line, [b""], S.pmk(psk if i % 3 else S.fast_psk(rng), e2), 258))
     batch = dwpa_amd.BatchJobs(jobs)
-    gpu_ms, _ = timed(lambda: batch.run(), reps)
+    lib_ms, _, backend = routed(lambda: batch.run(), reps)
+    got_lib = batch.results()
+    gpu_ms, _ = device_only(lambda: batch.run(), reps)
     got = batch.results()
     t0 = time.perf_counter()
     exp = [O.c_check_key_m22000(*j) for j in jobs]
     cpu_ms = (time.perf_counter() - t0) * 1e3
     rows.append({"call": "PMK propagation to 16 sibling nets (PMKID + EAPOL keyver 2/3, nc=258) in one "
                          "dwpa_check_batch vs 16 check_key_m22000 calls", "keys": 16, "caller_pmk": True, "nc": 258,
+                 "lib_ms_per_call": round(lib_ms, 3), "lib_backend": BACKENDS[backend],
                  "gpu_ms_per_call": round(gpu_ms, 3), "cpu_1core_ms_per_call": round(cpu_ms, 3),
-                 "gpu_over_cpu": round(gpu_ms / cpu_ms, 3), "same_result": got == exp})
+                 "lib_over_cpu": round(lib_ms / cpu_ms, 3), "gpu_over_cpu": round(gpu_ms / cpu_ms, 3),
+                 "same_result": got == exp and got_lib == exp})
     ok = all(r["same_result"] for r in rows)
     if rank == 0:
         emit({"metric": "ms per server check call (latency), m22000", "value": rows[0]["lib_ms_per_call"],
@@ -1203,7 +1213,11 @@ def cold_worker(args):
     if args.start_at:
         time.sleep(max(0.0, args.start_at - time.time()))
     t0 = time.perf_counter()
-    ndev = dwpa_amd.device_count()  # the HIP runtime's initialisation, split out of the first call
+    if args.cold_warmup:
+        ndev = dwpa_amd.device_count()  # the HIP runtime's initialisation, split out of the first call
+    else:
+        M.init(allow_cpu_fallback=1)  # what the PHP wrapper's ffi() does: the device is probed when a call needs it
+        ndev = None
     t_init = time.perf_counter() - t0
     rss["runtime_init"] = _rss()
     calls, errors = [], []
@@ -1211,13 +1225,15 @@ def cold_worker(args):
     def call(kind):
         line, keys = one if kind == "one" else many
         t = time.perf_counter()
+        backend = None
         try:
             r = dwpa_amd.check_key_m22000(line, keys)
             ok = r == (exp_one if kind == "one" else exp_many)
+            backend = M.check_stats()["backend"]
         except Exception as e:  # noqa: BLE001 -- an allocation or device failure is what K workers may hit
             errors.append(repr(e)[:200])
             ok = False
-        calls.append({"kind": kind, "ms": round((time.perf_counter() - t) * 1e3, 3), "ok": ok})
+        calls.append({"kind": kind, "ms": round((time.perf_counter() - t) * 1e3, 3), "ok": ok, "backend": backend})
     call("one")  # first call of the worker
     rss["first_call"] = _rss()
     call("one")  # second
@@ -1249,6 +1265,8 @@ def main_cold(args):
     def spawn(role, i, env_extra=None, start_at=None, steps=None):
         cmd = [sys.executable, os.path.abspath(__file__), "--workload", "c1cold", "--cold-role", role,
                "--cold-id", str(i), "--steps", str(steps if steps is not None else args.steps)]
+        if args.cold_warmup:
+            cmd.append("--cold-warmup")
         if start_at:
             cmd += ["--start-at", repr(start_at)]
         env = dict(os.environ, **(env_extra or {}))
@@ -1278,6 +1296,8 @@ def main_cold(args):
         rows["one_worker_at_a_time"].append({
             "ms_import_and_load": w["ms_import_and_load"], "ms_runtime_init": w["ms_runtime_init"],
             "ms_first_call": c[0]["ms"], "ms_second_call": c[1]["ms"], "rss_mib_by_stage": w["rss_mib"],
+            "backends": sorted({x["backend"] for x in c if x["backend"] is not None}),
+            "devices_probed": w["resources"]["devices"],
             "ms_one_key_warm_median": q([x["ms"] for x in c[2:] if x["kind"] == "one"], 0.5),
             "ms_202_keys_warm_median": q([x["ms"] for x in c[2:] if x["kind"] == "many"], 0.5),
             "library_device_mib": round(w["resources"]["device_bytes"] / mib, 1),
@@ -1309,6 +1329,8 @@ def main_cold(args):
             "ms_202_keys_median": q([c["ms"] for c in calls if c["kind"] == "many"], 0.5),
             "ms_202_keys_p95": q([c["ms"] for c in calls if c["kind"] == "many"], 0.95),
             "calls": len(calls), "failed_calls": sum(1 for c in calls if not c["ok"]),
+            "calls_by_backend": {str(b): sum(1 for c in calls if c["backend"] == b)
+                                 for b in sorted({c["backend"] for c in calls if c["backend"] is not None})},
             "errors": sorted({e for w in ws for e in w["errors"]})[:5],
             "library_device_mib_per_worker": round(statistics.median([w["resources"]["device_bytes"] for w in ws]) / mib, 1),
             "library_pinned_host_mib_per_worker": round(
@@ -1323,6 +1345,9 @@ def main_cold(args):
           "higher_is_better": False, "dtype": "u32", "data": "synthetic",
           "config": {"workload": "C1 cold: fresh worker processes (put_work.php:14 -> common.php:849,902), one key "
                                  "vs a PMKID line and 202 keys vs an EAPOL keyver-2 line at nc=128",
+                     "worker_start": ("HIP runtime started before the first call (dwpa22000_warmup model)"
+                                      if args.cold_warmup else "dwpa_init(allow_cpu_fallback=1), as the PHP "
+                                      "wrapper's ffi(): the device is probed by the first call that needs it"),
                      "parallelism": "processes"},
           "rows": rows, "concurrent": conc, "cpu_model": host_cpu()["cpu_model"], "hits_verified": ok})
     if not ok:

@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <deque>
 #include <exception>
@@ -289,7 +290,7 @@ static int calls_per_device() {
     return k;
 }
 
-static int init_locked(const dwpa_config* cfg) {
+static int init_locked(const dwpa_config* cfg, bool probe = true) {
     if (cfg) {
         g_mask = cfg->device_mask;
         g_batch = cfg->batch;
@@ -297,7 +298,7 @@ static int init_locked(const dwpa_config* cfg) {
         if (DWPA_CFG_HAS(cfg, allow_cpu_fallback)) g_cpu_fallback = cfg->allow_cpu_fallback;
         if (DWPA_CFG_HAS(cfg, host_max_pmks)) g_host_max = cfg->host_max_pmks;
     }
-    if (g_init) return 0;
+    if (g_init || !probe) return 0;
     if (g_nodev) return DWPA_E_NODEV;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -326,12 +327,12 @@ static int ensure_init() {
 // Host backend switches (host_check.cpp).  allow_cpu_fallback: dwpa_init's value when set (1 on, -1 off), else
 // DWPA_CPU_FALLBACK=1 from the environment; off by default, so a box without a device says DWPA_E_NODEV unless the
 // caller asked for the host backend.  host_max_pmks: calls of at most this many PMK-equivalents with at least one
-// PBKDF2 derive run on the host (dwpa_init's value, else DWPA_HOST_MAX_PMKS, else HOST_PMKS_PER_THREAD per host
-// thread; <= 0 from either = never).  On the MI355X box's EPYC 9575F a host thread derives ~4,700 PMK/s (AVX-512),
-// so the default's 256 PMKs on 16 threads take ~3.4 ms against ~8.5 ms for the GPU's one lone-wave round
-// (profiles/r06/host_bench.json); one thread's 16 take ~3.5 ms.
+// PBKDF2 derive run on the host (dwpa_init's value, else DWPA_HOST_MAX_PMKS, else what the host pool derives in
+// HOST_BUDGET_S on this CPU, at least HOST_MIN_PMKS; <= 0 from either = never).  The budget is a quarter of the GPU's
+// one lone-wave PBKDF2 round (~8.2 ms): on the MI355X box's EPYC 9575F a host thread derives ~14,400 PMK/s on
+// AVX-512, so the default is ~460 PMKs on 16 threads (profiles/r06/).
 static size_t host_threads(size_t n, size_t min_per_thread);
-constexpr double HOST_PMKS_PER_THREAD = 16.0;
+constexpr double HOST_BUDGET_S = 0.002, HOST_MIN_PMKS = 8.0;
 static bool cpu_fallback_on() {
     int v;
     {
@@ -351,7 +352,8 @@ static double host_max_pmks() {
     if (v) return v < 0 ? 0.0 : (double)v;
     const char* e = getenv("DWPA_HOST_MAX_PMKS");
     if (e && *e) return std::max(0.0, atof(e));
-    return HOST_PMKS_PER_THREAD * (double)host_threads(SIZE_MAX, 1);
+    static const double dflt = std::max(HOST_MIN_PMKS, std::floor(host_pmks_in(HOST_BUDGET_S, host_threads(SIZE_MAX, 1))));
+    return dflt;
 }
 // Device-side failures a call may retry on the host backend (allow_cpu_fallback): no device, a HIP error, a device or
 // pinned allocation that failed, a hit buffer that overflowed.
@@ -1649,13 +1651,16 @@ int dwpa_init(const dwpa_config* cfg) {
             return DWPA_E_ARG;
         if (DWPA_CFG_HAS(cfg, allow_cpu_fallback) && (cfg->allow_cpu_fallback < -1 || cfg->allow_cpu_fallback > 1))
             return DWPA_E_ARG;
-        int rc;
         {
             std::lock_guard<std::mutex> lk(g_mu);
-            rc = init_locked(cfg);
+            init_locked(cfg, false);
         }
-        // no device: the library still answers check and PBKDF2 calls when the host backend may take them
-        return rc == DWPA_E_NODEV && cpu_fallback_on() ? 0 : rc;
+        // With the host backend allowed the library answers check and PBKDF2 calls with or without a device, so the
+        // device is probed at the first call that needs it: a PHP-FPM worker whose calls all stay on the host backend
+        // never starts the HIP runtime (0.1-0.2 s and ~60 MiB of RSS, more once queues exist).
+        if (cpu_fallback_on()) return 0;
+        std::lock_guard<std::mutex> lk(g_mu);
+        return init_locked(nullptr);
     });
 }
 

@@ -67,6 +67,8 @@ struct HostCost {
 HostCost host_cost(const dwpa_job* jobs, size_t njobs);
 int host_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs, dwpa_check_stats& stats);
 int host_pbkdf2(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out);
+// PMKs the host backend derives in `seconds` on this CPU over `threads` threads (its measured per-chunk costs).
+double host_pmks_in(double seconds, size_t threads);
 
 // Pinned host memory (hipHostMalloc) counted in dwpa_resource_stats.pinned_host_bytes; free with the same size.
 int pinned_alloc(void** p, size_t bytes);

@@ -214,14 +214,25 @@ struct Derive {
     uint32_t group;
 };
 
-// PBKDF2 of every entry of `dv` into pmk[i] (big-endian words), over up to host_threads() threads: chunks handed
-// out through an atomic counter, so uneven keys (a 64 KiB one) do not stall a part.  A chunk is the fastest path's
-// unit (16 keys with AVX-512) when there are enough keys for every thread of the pool to take one, else
-// PBKDF2_CHAINS / 2 keys (SHA-NI chains spread over the threads: the latency of a call of a few keys).
+// Keys per chunk for n derives over `threads` threads: the chunk size whose estimated makespan (rounds of chunks over
+// the threads x one chunk's measured cost) is least -- 1 or 2 keys on SHA-NI chains for a few keys per thread
+// (latency), 8 or 16 keys on AVX-512 once there are enough for the threads (throughput).
+size_t derive_chunk(size_t n, size_t threads) {
+    const Pbkdf2Costs& c = pbkdf2_costs();
+    size_t per = 1;
+    auto span = [&](size_t k, double cost) { return (double)(((n + k - 1) / k + threads - 1) / threads) * cost; };
+    double best = span(1, c.ni1);
+    if (span(2, c.ni) < best) best = span(2, c.ni), per = 2;
+    if (c.avx1 > 0 && span(8, c.avx1) < best) best = span(8, c.avx1), per = 8;
+    if (c.avx2 > 0 && span(16, c.avx2) < best) best = span(16, c.avx2), per = 16;
+    return per;
+}
+
+// PBKDF2 of every entry of `dv` into pmk[i] (big-endian words), over up to host_threads() threads: chunks of
+// derive_chunk() keys handed out through an atomic counter, so uneven keys (a 64 KiB one) do not stall a part.
 void derive_all(const std::vector<Derive>& dv, const std::vector<std::vector<uint32_t>>& salt,
                 const std::vector<uint32_t>& nblk, std::vector<std::array<uint32_t, 8>>& pmk) {
-    const size_t wide = pbkdf2_keys_per_unit(), small = PBKDF2_CHAINS / 2;
-    const size_t per = dv.size() >= wide * host_threads_for(SIZE_MAX, 1) ? wide : small;
+    const size_t per = derive_chunk(dv.size(), host_threads_for(SIZE_MAX, 1));
     const size_t nchunks = (dv.size() + per - 1) / per;
     pmk.resize(dv.size());
     std::atomic<size_t> next{0};
@@ -416,6 +427,15 @@ int host_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* 
         }
     }
     return 0;
+}
+
+double host_pmks_in(double seconds, size_t threads) {
+    const Pbkdf2Costs& c = pbkdf2_costs();
+    double rate = c.ni1 > 0 ? 1.0 / c.ni1 : 0.0;  // keys per second per thread on the best path
+    if (c.ni > 0) rate = std::max(rate, 2.0 / c.ni);
+    if (c.avx1 > 0) rate = std::max(rate, 8.0 / c.avx1);
+    if (c.avx2 > 0) rate = std::max(rate, 16.0 / c.avx2);
+    return rate * seconds * (double)threads;
 }
 
 int host_pbkdf2(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out) {

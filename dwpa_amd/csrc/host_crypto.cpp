@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 
 namespace dwpa {
 namespace hostc {
@@ -369,7 +370,7 @@ DWPA_AVX512_TARGET __attribute__((always_inline)) static inline void sha1x16(__m
 
 // U_2..U_4096 of 16 G chains, lane l of group g = chain 16 g + l (the same message shape as pbkdf2_loop_ni).
 template <int G>
-DWPA_AVX512_TARGET static void pbkdf2_loop_avx512(const uint32_t* const* mid, uint32_t* const* t) {
+DWPA_AVX512_TARGET static void pbkdf2_loop_avx512(const uint32_t* const* mid, uint32_t* const* t, int iters = 4096) {
     __m512i ih[G][5], oh[G][5], u[G][5], T[G][5];
     alignas(64) uint32_t lanes[16];
     for (int g = 0; g < G; g++)
@@ -383,7 +384,7 @@ DWPA_AVX512_TARGET static void pbkdf2_loop_avx512(const uint32_t* const* mid, ui
         }
     const __m512i pad = _mm512_set1_epi32((int)0x80000000u), zero = _mm512_setzero_si512(),
                   len = _mm512_set1_epi32((64 + 20) * 8);
-    for (int it = 1; it < 4096; it++) {
+    for (int it = 1; it < iters; it++) {
         __m512i st[G][5], w[G][16];
         for (int g = 0; g < G; g++) {
             for (int k = 0; k < 5; k++) {
@@ -631,10 +632,10 @@ static void pbkdf2_u1(const uint32_t mid[10], const uint32_t* salt, uint32_t nbl
 }
 
 // U_2..U_4096 of one chain, scalar: inner and outer compressions of the 20-byte U with fixed padding.
-static void pbkdf2_loop_scalar(const uint32_t mid[10], uint32_t t[5]) {
+static void pbkdf2_loop_scalar(const uint32_t mid[10], uint32_t t[5], int iters = 4096) {
     uint32_t u[5], w[16], st[5];
     memcpy(u, t, 20);
-    for (int it = 1; it < 4096; it++) {
+    for (int it = 1; it < iters; it++) {
         memcpy(w, u, 20);
         w[5] = 0x80000000u;
         for (int k = 6; k < 15; k++) w[k] = 0;
@@ -651,7 +652,7 @@ static void pbkdf2_loop_scalar(const uint32_t mid[10], uint32_t t[5]) {
 // The same for N chains in SHA-NI form.  Message block of both compressions: U (5 words), 0x80000000, zeros, the
 // bit length 672 -- so W0..W3 = the previous digest's abcd as is, W4 = its e lane, W5 = the padding bit.
 template <int N>
-DWPA_SHA_TARGET static void pbkdf2_loop_ni(const uint32_t* const* mid, uint32_t* const* t) {
+DWPA_SHA_TARGET static void pbkdf2_loop_ni(const uint32_t* const* mid, uint32_t* const* t, int iters = 4096) {
     __m128i ia[N], ie[N], oa[N], oe[N], ua[N], ue[N], ta[N], te[N];
     const __m128i pad = _mm_set_epi32(0, (int)0x80000000u, 0, 0), zero = _mm_setzero_si128(),
                   len = _mm_set_epi32(0, 0, 0, (64 + 20) * 8);
@@ -664,7 +665,7 @@ DWPA_SHA_TARGET static void pbkdf2_loop_ni(const uint32_t* const* mid, uint32_t*
         ta[n] = ua[n] = _mm_set_epi32((int)t[n][0], (int)t[n][1], (int)t[n][2], (int)t[n][3]);
         te[n] = ue[n] = _mm_set_epi32((int)t[n][4], 0, 0, 0);
     }
-    for (int it = 1; it < 4096; it++) {
+    for (int it = 1; it < iters; it++) {
         __m128i a[N], e[N], m[N][4];
         for (int n = 0; n < N; n++) {
             a[n] = ia[n];
@@ -700,7 +701,52 @@ DWPA_SHA_TARGET static void pbkdf2_loop_ni(const uint32_t* const* mid, uint32_t*
     }
 }
 
-size_t pbkdf2_keys_per_unit() { return caps().avx512 ? PBKDF2_WIDE / 2 : PBKDF2_CHAINS / 2; }
+// Each path timed over 64 iterations on this CPU (best of 3), scaled to 4,095.  Zen 5 (the MI355X box's EPYC 9575F)
+// runs 16 keys on AVX-512 in ~2.9x the time of 2 keys on SHA-NI; other CPUs differ, so derive_all's chunk size is
+// chosen from these figures rather than from a fixed rule.
+static Pbkdf2Costs measure_costs() {
+    Pbkdf2Costs c;
+    uint32_t mids[PBKDF2_WIDE][10], T[PBKDF2_WIDE][5];
+    const uint32_t* cm[PBKDF2_WIDE];
+    uint32_t* ct[PBKDF2_WIDE];
+    for (int i = 0; i < PBKDF2_WIDE; i++) {
+        for (int k = 0; k < 10; k++) mids[i][k] = 0x9e3779b9u * (uint32_t)(10 * i + k + 1);
+        cm[i] = mids[i];
+        ct[i] = T[i];
+    }
+    constexpr int IT = 65;
+    auto best = [&](auto&& run) {
+        double b = 1e30;
+        for (int rep = 0; rep < 3; rep++) {
+            for (int i = 0; i < PBKDF2_WIDE; i++) memset(T[i], 0, 20);
+            const auto t0 = std::chrono::steady_clock::now();
+            run();
+            b = std::min(b, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        }
+        return b * 4095.0 / (IT - 1);
+    };
+    const Caps& k = caps();
+    if (k.sha_ni) {
+        c.ni1 = best([&] { pbkdf2_loop_ni<2>(cm, ct, IT); });
+        c.ni = best([&] { pbkdf2_loop_ni<PBKDF2_CHAINS>(cm, ct, IT); });
+    } else {
+        c.ni1 = best([&] {
+            for (int i = 0; i < 2; i++) pbkdf2_loop_scalar(cm[i], ct[i], IT);
+        });
+        c.ni = 2 * c.ni1;
+    }
+    if (k.avx512) {
+        c.avx1 = best([&] { pbkdf2_loop_avx512<1>(cm, ct, IT); });
+        c.avx2 = best([&] { pbkdf2_loop_avx512<2>(cm, ct, IT); });
+    }
+    return c;
+}
+
+const Pbkdf2Costs& pbkdf2_costs() {
+    static const Pbkdf2Costs c = measure_costs();
+    return c;
+}
+
 
 void pbkdf2_sha1(size_t n, const uint32_t (*mid)[10], const uint32_t* const* salt, const uint32_t* nblk,
                  uint32_t (*pmk)[8]) {

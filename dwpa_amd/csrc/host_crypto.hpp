@@ -54,8 +54,13 @@ void hmac_sha1_mid(const uint8_t* key, size_t len, uint32_t ipad[5], uint32_t op
 // (and everything without AVX-512) as PBKDF2_CHAINS SHA-NI chains in lock step, which hides the round latency of one.
 constexpr int PBKDF2_CHAINS = 4;
 constexpr int PBKDF2_WIDE = 32;
-// Keys per call of pbkdf2_sha1 that keep its fastest path busy (the host pool's work unit).
-size_t pbkdf2_keys_per_unit();
+// Seconds one thread takes for one pbkdf2_sha1 call of 1 key (ni1: two SHA-NI chains, or scalar without SHA-NI),
+// 2 keys (ni: four chains in lock step), 8 keys (avx1: one AVX-512 group of 16 chains) and 16 keys (avx2: two groups
+// in lock step); 0 = path absent.  Measured once per process on this CPU.
+struct Pbkdf2Costs {
+    double ni1 = 0, ni = 0, avx1 = 0, avx2 = 0;
+};
+const Pbkdf2Costs& pbkdf2_costs();
 void pbkdf2_sha1(size_t n, const uint32_t (*mid)[10], const uint32_t* const* salt, const uint32_t* nblk,
                  uint32_t (*pmk)[8]);
 

@@ -29,7 +29,7 @@ def init(device_mask: int = 0, batch: int = 0, rule_mode: int = L.DWPA_RULES_DEF
          host_max_pmks: int = 0) -> int:
     """dwpa_init: the process's device selection, check batch, rule-file mode and host backend switches
     (allow_cpu_fallback 1/-1/0 = on/off/DWPA_CPU_FALLBACK; host_max_pmks n/-1/0 = small-call threshold/never/
-    DWPA_HOST_MAX_PMKS or 16 per host thread).  Returns 0 or raises (DWPA_E_NODEV without a device unless the
+    DWPA_HOST_MAX_PMKS or the PMKs the host pool derives in 2 ms).  Returns 0 or raises (DWPA_E_NODEV without a device unless the
     fallback is on)."""
     cfg = L.Config(ctypes.sizeof(L.Config), int(device_mask), int(batch), 0, int(rule_mode), int(allow_cpu_fallback),
                    int(host_max_pmks))

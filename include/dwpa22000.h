@@ -119,13 +119,16 @@ typedef struct {
     int32_t allow_cpu_fallback; /* ABI 4 (was reserved[1]), dwpa_init only: 1 = without a usable device, or after a
                                   device call failed (DWPA_E_NODEV / _HIP / _NOMEM / _OVERFLOW), check and PBKDF2
                                   calls run on the host backend; -1 = never; 0 = DWPA_CPU_FALLBACK=1 from the
-                                  environment, else never.  With it on, dwpa_init returns 0 on a box without a device */
+                                  environment, else never.  With it on, dwpa_init returns 0 without probing for a
+                                  device: the first call that needs one probes (a process whose calls all stay on the
+                                  host backend never starts the HIP runtime) */
     int32_t host_max_pmks;     /* ABI 4 (was reserved[2]), dwpa_init only: a check call with at least one PBKDF2 derive
                                   and at most this many PMK-equivalents (derives + nonce-correction verify work /
                                   16,388 compressions) runs on the host backend, a dwpa_pbkdf2_pmk call of at most this
                                   many keys too; -1 = never (every call on the device); 0 = DWPA_HOST_MAX_PMKS from
-                                  the environment (<= 0: never), else 16 per host thread of the library's pool
-                                  (DWPA_HOST_THREADS, default 16: 256).  Until the process's first device call
+                                  the environment (<= 0: never), else the PMKs the library's host pool derives in
+                                  2 ms on this CPU (measured at first use; ~460 on 16 threads of an EPYC 9575F, at
+                                  least 8).  Until the process's first device call
                                   completes the threshold is 8x this: that call also starts the HIP runtime (0.2-0.7 s
                                   in a fresh PHP-FPM worker) */
     int32_t reserved[1];

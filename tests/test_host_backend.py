@@ -250,8 +250,8 @@ def test_scalar_primitives_subprocess():
 @pytest.mark.skipif(_gpu_present(), reason="a GPU is visible: the no-device path is not reachable")
 def test_routing_without_a_device(monkeypatch):
     """No device here.  allow_cpu_fallback off and host_max_pmks -1: every compute call fails loudly (DWPA_E_NODEV).
-    The default threshold: a small call (one key) is answered by the host backend (backend 1), a large one (above
-    8 x 16 PMK-equivalents per host thread before any device call) is DWPA_E_NODEV.  allow_cpu_fallback on: dwpa_init returns 0 and the large
+    The default threshold: a small call (one key) is answered by the host backend (backend 1); with host_max_pmks 50
+    a call of 500 keys (above 8 x 50 before any device call) is DWPA_E_NODEV.  allow_cpu_fallback on: dwpa_init returns 0 and the large
     call is answered too (backend 2).  Caller-PMK calls (no derive) need the fallback."""
     monkeypatch.delenv("DWPA_CPU_FALLBACK", raising=False)
     monkeypatch.delenv("DWPA_HOST_MAX_PMKS", raising=False)
@@ -266,7 +266,7 @@ def test_routing_without_a_device(monkeypatch):
     psk = S.random_psk(rng)
     line = S.eapol_line(psk, essid, ap, sta, an, sn, 2, 3, "LE", rng=rng)
     small = (line, [psk], False, 128)
-    nlarge = 8 * 16 * min(16, os.cpu_count() or 1) + 100  # host_threads(): DWPA_HOST_THREADS (16) and the machine
+    nlarge = 500
     large = (line, [S.fast_psk(rng) for _ in range(nlarge - 1)] + [psk], False, 128)
     caller = (line, [b""], S.pmk(psk, essid), 128)
     exp = {k: O.c_check_key_m22000(*j) for k, j in (("small", small), ("large", large), ("caller", caller))}
@@ -284,11 +284,12 @@ def test_routing_without_a_device(monkeypatch):
         assert dwpa_amd.check_key_m22000(*small) == exp["small"]
         assert M.check_stats()["backend"] == L.DWPA_BACKEND_HOST_SMALL
         assert dwpa_amd.pbkdf2_pmk([psk], essid)[0] == S.pmk(psk, essid)
+        assert init(-1, 50) == L.DWPA_E_NODEV
         with pytest.raises(L.DwpaError):
             dwpa_amd.check_key_m22000(*large)
         with pytest.raises(L.DwpaError):
             dwpa_amd.check_key_m22000(*caller)
-        assert init(1, 0) == 0
+        assert init(1, 50) == 0
         assert dwpa_amd.check_key_m22000(*large) == exp["large"]
         st = M.check_stats()
         assert st["backend"] == L.DWPA_BACKEND_HOST_FALLBACK and st["pmks"] == nlarge and st["hits"] == 1

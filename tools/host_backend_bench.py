@@ -5,9 +5,9 @@ oracle (OpenSSL, one PHP request's core).  Every result is checked against the o
 
     python tools/host_backend_bench.py [--reps N]
 
-PBKDF2 runs on SHA-NI (four chains in lock step) for a few keys per thread and on AVX-512 (32 chains = 16 keys per
-task) once a call has 32 chains per pool thread; the one-thread rows (a child with DWPA_HOST_THREADS=1) give each
-path's per-core rate.
+PBKDF2 runs in chunks of 2 keys on SHA-NI chains, or 8 / 16 keys on AVX-512, whichever the library's measured
+per-chunk costs say finishes the call first (host_check.cpp derive_chunk); the one-thread rows (a child with
+DWPA_HOST_THREADS=1) give the per-core rates: 2 keys = SHA-NI, 32 and 256 keys = AVX-512 where present.
 """
 import argparse
 import json
@@ -51,16 +51,13 @@ def main():
            "host_threads_cap": int(os.environ.get("DWPA_HOST_THREADS", "16"))}
     rows = []
     threads = max(1, min(out["host_threads_cap"], len(os.sched_getaffinity(0)), os.cpu_count() or 1))
-    wide = "avx512f" in out["flags"] and "sha_ni" in out["flags"]
     sizes = (2, 32, 256) if args.pbkdf2_only else (1, 2, 16, 64, 256, 512, 1024, 4096)
     for n in sizes:
         keys = [S.fast_psk(rng) for _ in range(n)]
         ms = med(lambda: dwpa_amd.pbkdf2_pmk(keys, essid), max(3, args.reps // (1 + n // 16)))
         ok = b"".join(dwpa_amd.pbkdf2_pmk(keys, essid)) == O.c_pbkdf2_many(keys, essid, threads=8)
         rows.append({"call": f"dwpa_pbkdf2_pmk, {n} key(s)", "threads": threads, "ms": round(ms, 3),
-                     "pmk_per_s": round(n / ms * 1e3),
-                     "path": "avx512" if wide and 2 * n >= 32 * threads else "sha_ni" if "sha_ni" in out["flags"]
-                     else "scalar", "same_result": ok})
+                     "pmk_per_s": round(n / ms * 1e3), "same_result": ok})
     if args.pbkdf2_only:
         out["rows"] = rows
         print(json.dumps(out))

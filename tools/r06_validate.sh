@@ -13,7 +13,7 @@ if [ "${SUITE:-1}" = 1 ]; then
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
 fi
 if [ "${PROF:-1}" = 1 ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench -- python3 bench.py --steps 8 --warmup 2 \
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 8 --warmup 2 \
     > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 fi
 OUT=$OUT/legs LEGS=${LEGS:-"c1lat host c5 c5k2 c1 c4 c2files_node8"} tools/bench_legs.sh
