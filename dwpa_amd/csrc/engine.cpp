@@ -12,8 +12,8 @@
 #include <string.h>
 
 #include <algorithm>
-#include <cmath>
 #include <atomic>
+#include <cmath>
 #include <deque>
 #include <exception>
 #include <map>
@@ -595,12 +595,46 @@ static int upload_span(DevBuf& b, const Span<T>& v, hipStream_t s) {
     return 0;
 }
 
+// A host thread deriving the PBKDF2 remainder of a check call on the host backend while the head runs on the GPU
+// (derive_slots); joined by finish_derive, or at the latest when the stage goes out of scope.
+struct HostTailJob {
+    std::thread t;
+    int rc = 0;
+    ~HostTailJob() {
+        if (t.joinable()) t.join();
+    }
+};
+
 // Host staging of one derive step in the device's pinned arena; valid until the stream is synchronised.
 struct DeriveStage {
     Span<uint64_t> ids;
     Span<uint32_t> src, sref, spool, cpmk, uslot;
     uint32_t split = 0;  // slots [0, split) read d.stream's PMKs; [split, n) d.tail's (== n: no tail)
+    uint32_t n = 0, nh = 0, nu = 0;
+    bool host_tail = false;  // unique PMKs [nh, nu) come from the host (htail, SoA rows of nu - nh words)
+    Span<uint32_t> htail;
+    HostTailJob job;
 };
+
+// DWPA_HOST_TAIL=0 keeps the check path's PBKDF2 remainder on the GPU (a test switch: the suite runs both).
+static bool host_tail_knob() {
+    static const bool on = [] {
+        const char* e = getenv("DWPA_HOST_TAIL");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
+// The PBKDF2 remainder below one wave per SIMD (the tail) goes to the host backend when the host derives it well
+// within the head's time: the head then fills whole waves on every SIMD and no lone tail wave outlasts it.  A head
+// wave time is ~6.5-7 ms (C2 6.50 ms, the C5 head 7.03 ms per wave per SIMD, CHANGELOG.md round 4/5); the host gets
+// 3/4 of the head's estimated time, so the GPU never waits for it on a host with the measured speed.
+constexpr double HEAD_WAVE_S = 6.5e-3, HOST_TAIL_SHARE = 0.75;
+static bool host_tail_fits(uint32_t nt, uint32_t nh) {
+    if (!host_tail_knob() || !nt) return false;
+    const double head_s = (double)nh / (double)std::max<uint32_t>(1, pbkdf2_wave_unit()) * HEAD_WAVE_S;
+    return (double)nt <= host_pmks_in(HOST_TAIL_SHARE * head_s, host_threads(SIZE_MAX, 1));
+}
 
 // Head/tail split of one derive.  PBKDF2 is issue-bound, so a launch takes as long as its fullest SIMD: nu unique
 // PMKs at k.f waves per SIMD cost k + 1 whole wave times (~7 ms each at C5 size), the last one with 1 - f of the
@@ -631,7 +665,7 @@ static int upload_slot_keys(Device& d, const SlotTable& T) {
 // until that kernel ends.
 static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const std::vector<const uint8_t*>& job_pmk,
                         const std::vector<uint32_t>& runs, const std::vector<const std::string*>& run_essid,
-                        bool upload_keys, DeriveStage& st) {
+                        bool upload_keys, DeriveStage& st, bool allow_host_tail = false) {
     PhaseTrace tr;
     hipStream_t s = d.stream;
     const uint32_t n = (uint32_t)(e - b);
@@ -640,8 +674,8 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
     const size_t nruns = runs.size() - 1;
     for (size_t r = 0; r < nruns; r++)  // count word + [2][nblk][16], nblk = SHA-1 blocks of ESSID || INT(i) || pad
         saltwords += 1 + 32 * ((run_essid[r]->size() + 4 + 9 + 63) / 64);
-    // pinned staging, sized by upper bounds: <= n unique keys, <= n caller PMKs
-    RCHK(d.stage.reset(12 * (size_t)n + 8 * (size_t)n + 4 * saltwords + 32 * (size_t)n + 8 * 64));
+    // pinned staging, sized by upper bounds: <= n unique keys, <= n caller PMKs, <= n host-derived PMKs
+    RCHK(d.stage.reset(12 * (size_t)n + 8 * (size_t)n + 4 * saltwords + 64 * (size_t)n + 9 * 64));
     st.src = take<uint32_t>(d.stage, n);
     st.ids = take<uint64_t>(d.stage, n);
     // Runs are deduplicated independently (one small open-addressing table per run keeps it cache-resident), on
@@ -739,7 +773,45 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
     // read head PMKs (or caller PMKs) and the slots after it wait for the tail
     const uint32_t nh = head_pmks(nu);
     st.split = n;
-    if (nh < nu)
+    st.n = n;
+    st.nh = nh;
+    st.nu = nu;
+    if (allow_host_tail && nh < nu && host_tail_fits(nu - nh, nh)) {
+        // the remainder on the host backend, beside the head: its keys' bytes (T), salt blocks (spool) and SoA rows
+        // in pinned memory, uploaded by finish_derive once the thread is done
+        const uint32_t nt = nu - nh;
+        st.htail = take<uint32_t>(d.stage, 8 * (size_t)nt);
+        if (d.stage.used > d.stage.cap) return DWPA_E_ARG;
+        const uint8_t* kb = T.kbytes;
+        const uint64_t* ko = T.koff;
+        const uint32_t* kl = T.klen;
+        const uint32_t* us = st.uslot.data() + nh;
+        const uint32_t* sr = st.sref.data() + nh;
+        const uint32_t* sp = st.spool.data();
+        uint32_t* out = st.htail.data();
+        HostTailJob& job = st.job;
+        try {
+            job.t = std::thread([=, &job] {
+                job.rc = guarded([&]() -> int {
+                    std::vector<const uint8_t*> key(nt);
+                    std::vector<uint32_t> len(nt), nblk(nt);
+                    std::vector<const uint32_t*> salt(nt);
+                    for (uint32_t u = 0; u < nt; u++) {
+                        key[u] = kb + ko[us[u]];
+                        len[u] = kl[us[u]];
+                        nblk[u] = sp[sr[u]];
+                        salt[u] = sp + sr[u] + 1;
+                    }
+                    host_derive_soa(nt, key.data(), len.data(), salt.data(), nblk.data(), out, nt);
+                    return 0;
+                });
+            });
+            st.host_tail = true;
+        } catch (...) {  // no thread: the GPU derives the remainder as a tail, as without the host backend
+            st.host_tail = false;
+        }
+    }
+    if (nh < nu && !st.host_tail)
         for (uint32_t i = 0; i < n; i++)
             if (!(st.src[i] & GATHER_CALLER) && st.src[i] >= nh) {
                 st.split = i;
@@ -770,7 +842,8 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
         uint32_t* head_flag = (uint32_t*)d.batch.counters.p + 3;  // zeroed with the counters above
         uint32_t* raised = (uint32_t*)d.batch.counters.p + 4;     // likewise; read back by collect_hits
         d.stats.pmks += nu;
-        if (nh < nu) {  // the tail first, beside the head (priority 0 until the head has ended: pbkdf2_lane_tail)
+        if (st.host_tail) d.stats.tail_pmks += nu - nh;
+        if (nh < nu && !st.host_tail) {  // the tail first, beside the head (priority 0 until the head has ended)
             HIPCHK(hipEventRecord(d.prep_done, s));
             HIPCHK(hipStreamWaitEvent(d.tail, d.prep_done, 0));
             HIPCHK(launch_pbkdf2_ms_tail(mid + nh, cap, nu - nh, (const uint32_t*)d.salt.p, sref + nh, upmk + nh,
@@ -779,10 +852,11 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
             d.stats.tail_waves += 2 * ((nu - nh + 63) / 64);  // two output-block lanes per PMK
         }
         HIPCHK(launch_pbkdf2_ms(mid, cap, nh, (const uint32_t*)d.salt.p, sref, upmk, s));
-        if (nh < nu) HIPCHK(launch_set_flag(head_flag, s));
+        if (nh < nu && !st.host_tail) HIPCHK(launch_set_flag(head_flag, s));
         HIPCHK(hipEventRecord(d.head_end, s));
         f.last = d.head_end;
     }
+    if (st.host_tail) return 0;  // finish_derive gathers once the host's PMKs are up
     // SoA rows keep their stride (cap), so a sub-range is the same launch on offset base pointers
     const uint32_t sp = st.split;
     if (sp)
@@ -794,6 +868,27 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
         HIPCHK(launch_gather_pmk(upmk, cap, (const uint32_t*)d.cpmk.p, (const uint32_t*)d.src.p + sp, n - sp,
                                  (uint32_t*)d.batch.pmk.p + sp, cap, d.tail));
     }
+    return 0;
+}
+
+// The end of a derive whose remainder the host backend computes (derive_slots): wait for the host thread, upload its
+// PMKs next to the head's, then gather every slot.  The host thread ran while the GPU derived the head, so the upload
+// is normally queued well before the head ends.  Should the thread have failed (an allocation), the GPU derives the
+// remainder after the head instead.
+static int finish_derive(Device& d, DeriveStage& st) {
+    if (!st.host_tail) return 0;
+    if (st.job.t.joinable()) st.job.t.join();
+    const uint32_t cap = d.batch.cap, nh = st.nh, nt = st.nu - st.nh;
+    uint32_t* upmk = (uint32_t*)d.upmk.p;
+    if (st.job.rc == 0) {
+        HIPCHK(hipMemcpy2DAsync(upmk + nh, (size_t)cap * 4, st.htail.data(), (size_t)nt * 4, (size_t)nt * 4, 8,
+                                hipMemcpyHostToDevice, d.stream));
+    } else {
+        HIPCHK(launch_pbkdf2_ms((const uint32_t*)d.batch.mid.p + nh, cap, nt, (const uint32_t*)d.salt.p,
+                                (const uint32_t*)d.sref.p + nh, upmk + nh, d.stream));
+    }
+    HIPCHK(launch_gather_pmk(upmk, cap, (const uint32_t*)d.cpmk.p, (const uint32_t*)d.src.p, st.n,
+                             (uint32_t*)d.batch.pmk.p, cap, d.stream));
     return 0;
 }
 
@@ -1215,11 +1310,12 @@ static int check_batch_body(Device& d, const dwpa_job* jobs, size_t njobs, dwpa_
         }
         runs.push_back((uint32_t)(e - b));
         DeriveStage st;
-        RCHK(derive_slots(d, T, b, e, cs.job_pmk, runs, run_essid, false, st));
+        RCHK(derive_slots(d, T, b, e, cs.job_pmk, runs, run_essid, false, st, true));
         if (b == 0) {
             for (uint32_t j : cs.order) job_line[j] = tb.add_line(cs.parsed[j], jobs[j].nc, DWPA_NC_PHP, 0);
             tr.mark("tables (overlapped)");
         }
+        RCHK(finish_derive(d, st));
         // the tail slots' verify first: its segment upload goes up the side stream ahead of the head's keyver-3
         // verify, which that stream then runs (fan-out)
         RCHK(queue_verify(d, T, b, b + st.split, e, job_line, tb, b == 0, d.tail, d.segs_tail, d.keys_tail, false));

@@ -69,6 +69,10 @@ int host_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* 
 int host_pbkdf2(const dwpa_bytes* keys, size_t nkeys, const uint8_t* essid, size_t essid_len, uint8_t* out);
 // PMKs the host backend derives in `seconds` on this CPU over `threads` threads (its measured per-chunk costs).
 double host_pmks_in(double seconds, size_t threads);
+// PBKDF2 of n keys on the host backend into SoA rows: pmk[w * stride + i] = big-endian word w of key i's PMK; key i
+// salted with salt[i] (build_salt_blocks layout, nblk[i] blocks).  The device check path's remainder helper.
+void host_derive_soa(size_t n, const uint8_t* const* key, const uint32_t* len, const uint32_t* const* salt,
+                     const uint32_t* nblk, uint32_t* pmk, size_t stride);
 
 // Pinned host memory (hipHostMalloc) counted in dwpa_resource_stats.pinned_host_bytes; free with the same size.
 int pinned_alloc(void** p, size_t bytes);

@@ -228,29 +228,46 @@ size_t derive_chunk(size_t n, size_t threads) {
     return per;
 }
 
-// PBKDF2 of every entry of `dv` into pmk[i] (big-endian words), over up to host_threads() threads: chunks of
-// derive_chunk() keys handed out through an atomic counter, so uneven keys (a 64 KiB one) do not stall a part.
-void derive_all(const std::vector<Derive>& dv, const std::vector<std::vector<uint32_t>>& salt,
-                const std::vector<uint32_t>& nblk, std::vector<std::array<uint32_t, 8>>& pmk) {
-    const size_t per = derive_chunk(dv.size(), host_threads_for(SIZE_MAX, 1));
-    const size_t nchunks = (dv.size() + per - 1) / per;
-    pmk.resize(dv.size());
+// PBKDF2 of n keys over up to host_threads() threads: chunks of derive_chunk() keys handed out through an atomic
+// counter, so uneven keys (a 64 KiB one) do not stall a part.  get(i, key, len, salt, nblk) describes key i (salt in
+// build_salt_blocks layout), put(i, pmk) takes its PMK (8 big-endian words).
+template <class Get, class Put>
+void derive_each(size_t nkeys, Get get, Put put) {
+    const size_t per = derive_chunk(nkeys, host_threads_for(SIZE_MAX, 1));
+    const size_t nchunks = (nkeys + per - 1) / per;
     std::atomic<size_t> next{0};
     host_parallel(host_threads_for(nchunks, 1), [&](size_t) {
         std::vector<std::array<uint32_t, 10>> mid(per);
+        std::vector<std::array<uint32_t, 8>> out(per);
         std::vector<const uint32_t*> sp(per);
         std::vector<uint32_t> nb(per);
         for (size_t c; (c = next.fetch_add(1, std::memory_order_relaxed)) < nchunks;) {
-            const size_t i0 = c * per, n = std::min(per, dv.size() - i0);
+            const size_t i0 = c * per, n = std::min(per, nkeys - i0);
             for (size_t k = 0; k < n; k++) {
-                const Derive& d = dv[i0 + k];
-                hmac_sha1_mid(d.key, d.len, mid[k].data(), mid[k].data() + 5);
-                sp[k] = salt[d.group].data();
-                nb[k] = nblk[d.group];
+                const uint8_t* key;
+                size_t len;
+                get(i0 + k, key, len, sp[k], nb[k]);
+                hmac_sha1_mid(key, len, mid[k].data(), mid[k].data() + 5);
             }
-            pbkdf2_sha1(n, (const uint32_t(*)[10])mid.data(), sp.data(), nb.data(), (uint32_t(*)[8])pmk[i0].data());
+            pbkdf2_sha1(n, (const uint32_t(*)[10])mid.data(), sp.data(), nb.data(), (uint32_t(*)[8])out.data());
+            for (size_t k = 0; k < n; k++) put(i0 + k, out[k].data());
         }
     });
+}
+
+// PBKDF2 of every entry of `dv` into pmk[i] (big-endian words).
+void derive_all(const std::vector<Derive>& dv, const std::vector<std::vector<uint32_t>>& salt,
+                const std::vector<uint32_t>& nblk, std::vector<std::array<uint32_t, 8>>& pmk) {
+    pmk.resize(dv.size());
+    derive_each(
+        dv.size(),
+        [&](size_t i, const uint8_t*& key, size_t& len, const uint32_t*& sp, uint32_t& nb) {
+            key = dv[i].key;
+            len = dv[i].len;
+            sp = salt[dv[i].group].data();
+            nb = nblk[dv[i].group];
+        },
+        [&](size_t i, const uint32_t* w) { memcpy(pmk[i].data(), w, 32); });
 }
 
 void pmk_bytes_out(const uint32_t w[8], uint8_t out[32]) {
@@ -427,6 +444,21 @@ int host_check_batch(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* 
         }
     }
     return 0;
+}
+
+void host_derive_soa(size_t n, const uint8_t* const* key, const uint32_t* len, const uint32_t* const* salt,
+                     const uint32_t* nblk, uint32_t* pmk, size_t stride) {
+    derive_each(
+        n,
+        [&](size_t i, const uint8_t*& k, size_t& l, const uint32_t*& sp, uint32_t& nb) {
+            k = key[i];
+            l = len[i];
+            sp = salt[i];
+            nb = nblk[i];
+        },
+        [&](size_t i, const uint32_t* w) {
+            for (int k = 0; k < 8; k++) pmk[(size_t)k * stride + i] = w[k];
+        });
 }
 
 double host_pmks_in(double seconds, size_t threads) {

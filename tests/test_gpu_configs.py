@@ -113,6 +113,39 @@ def test_batch_head_tail_split():
         assert O.c_check_key_m22000(line, [keys[w]], False, nc) == g
 
 
+def test_batch_host_tail():
+    """A derive of 6 whole waves per SIMD plus a small remainder: the remainder (the tail) is derived on the host
+    backend while the head runs (the box's EPYC derives it in well under the head's time), so no
+    device tail wave runs.  Hits planted in head PMKs, in host-derived PMKs, and in later jobs re-using both."""
+    import random
+    rng = random.Random(92)
+    n_per = 50000  # 4 ESSIDs x 50,000 = 200,000 = 6 x 32,768 + 3,392 (MI355X: 256 CUs x 4 SIMDs x 64 / 2)
+    nets = [S.random_net(rng, essid_len=9 + e) for e in range(4)]
+    keyset = [[b"h%d-%06d-" % (e, i) + S.fast_psk(rng, 8, 20) for i in range(n_per)] for e in range(4)]
+    jobs, want = [], []
+    for e, (essid, ap, sta, an, sn) in enumerate(nets):
+        keys = keyset[e]
+        hit = [10, 25000, 40000, 49990][e]  # ESSID 3's key is one of the last derived: a host-tail PMK
+        line = (S.pmkid_line(keys[hit], essid, ap, sta) if e % 2 else
+                S.eapol_line(keys[hit], essid, ap, sta, an, sn, 3 if e else 2, -4, "BE", rng=rng))
+        jobs.append((line, keys, False, 8))
+        want.append(hit)
+    essid, ap, sta, an, sn = nets[3]
+    for src in (7, 49995):  # later jobs re-using a head PMK and a host-tail PMK
+        keys = [b"again-%05d-" % i + S.fast_psk(rng, 8, 12) for i in range(100)]
+        keys[60] = keyset[3][src]
+        jobs.append((S.eapol_line(keyset[3][src], essid, ap, sta, an, sn, 1, 2, "LE", rng=rng), keys, False, 8))
+        want.append(60)
+    got = dwpa_amd.check_batch(jobs)
+    st = dwpa_amd.check_stats()
+    for job, g, w in zip(jobs, got, want):
+        line, keys, _, nc = job
+        assert g and g[0] == keys[w], (line[:30], g)
+        assert O.c_check_key_m22000(line, [keys[w]], False, nc) == g
+    assert st["pmks"] == 4 * n_per + 200 - 2 and st["tail_pmks"] == 4 * n_per + 200 - 2 - 6 * 32768
+    assert st["tail_waves"] == 0, st  # the remainder came from the host backend
+
+
 def test_batch_fanout_dedup_and_mixed_salt_lengths():
     """put_work shape (common.php:879-902): one submitted key checked against every net of an ESSID, plus PMK
     re-use jobs (:919) -- the engine derives each (ESSID, key) once.  ESSIDs of 1..60 bytes put 1- and 2-block
