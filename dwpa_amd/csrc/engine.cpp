@@ -1408,7 +1408,8 @@ static int pbkdf2_device(const dwpa_bytes* keys, size_t nkeys, const uint8_t* es
     for (size_t b = 0; b < nkeys; b += chunk) {
         const size_t e = std::min(nkeys, b + chunk);
         DeriveStage st;
-        RCHK(derive_slots(d, T, b, e, jp, {0u, (uint32_t)(e - b)}, {&es}, b == 0, st));
+        RCHK(derive_slots(d, T, b, e, jp, {0u, (uint32_t)(e - b)}, {&es}, b == 0, st, true));
+        RCHK(finish_derive(d, st));
         RCHK(join_tail(d));
         std::vector<uint32_t> w((size_t)PMK_WORDS * d.batch.cap);
         HIPCHK(hipMemcpyAsync(w.data(), d.batch.pmk.p, w.size() * 4, hipMemcpyDeviceToHost, d.stream));

@@ -256,20 +256,22 @@ def test_pbkdf2_pmk_duplicate_keys():
     assert got == [O.c_pbkdf2(k, essid) for k in keys]
 
 
-def test_pbkdf2_pmk_head_tail_split():
-    """dwpa_pbkdf2_pmk over 70,000 keys (> 2 waves per SIMD: the head/tail split of the derive, joined before the PMKs
-    are copied out), with duplicates and the empty key: every PMK in its input position, a sample of 300 spread over
-    head and tail against the oracle and every duplicate equal to its first copy."""
+@pytest.mark.parametrize("nkeys", [70000, 66800])
+def test_pbkdf2_pmk_head_tail_split(nkeys):
+    """dwpa_pbkdf2_pmk over > 2 waves per SIMD of keys (the head/tail split of the derive, joined before the PMKs are
+    copied out), with duplicates and the empty key: every PMK in its input position, a sample of 300 spread over head
+    and tail against the oracle and every duplicate equal to its first copy.  70,000 keys leave a ~4,400-PMK tail for
+    the GPU; 66,800 a ~1,200-PMK one, which the host backend derives beside the head."""
     import random
     rng = random.Random(97)
-    keys = [b"p%06d-" % i + S.fast_psk(rng, 4, 30) for i in range(70000)]
-    for i in range(0, 70000, 997):
+    keys = [b"p%06d-" % i + S.fast_psk(rng, 4, 30) for i in range(nkeys)]
+    for i in range(0, nkeys, 997):
         keys[i] = keys[i // 2]  # duplicates of earlier keys (head and tail positions)
     keys[12345] = b""
     essid = b"split-essid"
     got = dwpa_amd.pbkdf2_pmk(keys, essid)
     assert len(got) == len(keys)
-    idx = sorted(set(rng.sample(range(len(keys)), 300)) | {0, 12345, 69999, 65535, 65536})
+    idx = sorted(set(rng.sample(range(len(keys)), 300)) | {0, 12345, nkeys - 1, 65535, 65536})
     with ThreadPoolExecutor(THREADS) as ex:
         exp = list(ex.map(lambda i: O.c_pbkdf2(keys[i], essid), idx))
     assert [got[i] for i in idx] == exp
