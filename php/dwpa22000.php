@@ -238,19 +238,21 @@ function check_keys_m22000_gpu_batch($jobs)
     return $res;
 }
 
-/* Since ABI 4 the library routes by call shape itself (one key, or a handful: its host backend on this server's
- * cores, well under PHP's 1.1 ms per key; more keys and caller-PMK checks of EAPOL lines: the GPU), and a worker's
- * first GPU call is taken only by a call big enough to amortise the runtime start-up (the threshold is 8x higher
- * until then, INTEGRATION.md section 2).  check_key_m22000_routed stays as the name earlier deployments call. */
+/* Since ABI 4 the library routes by call shape itself: a call whose PBKDF2 work the host backend finishes in about
+ * 2 ms on this server's cores (one key: 0.24 ms, against PHP's 1.1 ms) runs there, the rest and every caller-PMK
+ * check on the GPU.  A worker that has not made a GPU call yet keeps calls of up to 8x that on the host and does not
+ * start the HIP runtime until a call needs it (INTEGRATION.md section 2).  check_key_m22000_routed stays as the name
+ * earlier deployments call. */
 function check_key_m22000_routed($hashline, $keys, $pmk = False, $nc = 128)
 {
     return check_key_m22000_gpu($hashline, $keys, $pmk, $nc);
 }
 
-/* Optional, for pools that keep their workers (pm = static, pm.max_requests = 0): pay the GPU start-up in this worker
- * now -- the runtime, the code objects and the call context, through one 512-key check of a fixed PMKID line (a
- * miss; big enough to go to the GPU) -- e.g. from an auto_prepend_file on the worker's first request.  Returns the
- * number of usable gfx950 devices (0: none -- every check then runs on the library's host backend). */
+/* Optional, for pools whose workers make large calls (pm = static, pm.max_requests = 0): pay the GPU start-up in this
+ * worker now -- the runtime, the code objects and the call context, through one 512-key check of a fixed PMKID line
+ * (a miss) forced onto the GPU -- e.g. from an auto_prepend_file on the worker's first request.  Workers that only
+ * make put_work's small calls need no warm-up: the host backend answers them.  Returns the number of usable gfx950
+ * devices (0: none -- every check then runs on the library's host backend). */
 function dwpa22000_warmup()
 {
     $ffi = Dwpa22000::ffi();
