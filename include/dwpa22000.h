@@ -165,9 +165,10 @@ int dwpa_check_m22000(const char *line, size_t line_len, const dwpa_bytes *keys,
 int dwpa_check_batch(const dwpa_job *jobs, size_t njobs, dwpa_result *out, int *rcs);
 /* What the calling thread's last dwpa_check_m22000 / dwpa_check_batch call did (ABI 3): which backend answered it
  * (ABI 4), its jobs, the non-null keys of usable lines (slots), the (ESSID, key) PMKs derived after deduplication (on
- * the host backend: by it; the tail fields below stay 0 there), how many of those the tail launch
- * derived (the remainder under one wave per SIMD, run beside the head at low wave priority), the tail's waves and
- * how many of them saw the head end and raised their priority, the hits, and the call's wall time.
+ * the host backend: by it; the tail fields below stay 0 there), how many of those formed the device call's tail
+ * (the remainder under one wave per SIMD: derived by the host backend beside the head when it fits the head's time,
+ * tail_waves 0; else by a tail launch beside the head at low wave priority), the tail launch's waves and how many of
+ * them saw the head end and raised their priority, the hits, and the call's wall time.
  * Returns 0, or DWPA_E_ARG before any check call in this thread. */
 typedef struct {
     uint32_t jobs;
