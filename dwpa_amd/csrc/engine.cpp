@@ -616,7 +616,7 @@ struct DeriveStage {
     HostTailJob job;
 };
 
-// DWPA_HOST_TAIL=0 keeps the check path's PBKDF2 remainder on the GPU (a test switch: the suite runs both).
+// DWPA_HOST_TAIL=0 keeps the check path's PBKDF2 remainder on the GPU (a test switch: test_batch_host_tail_switch_off).
 static bool host_tail_knob() {
     static const bool on = [] {
         const char* e = getenv("DWPA_HOST_TAIL");

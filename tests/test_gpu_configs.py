@@ -143,7 +143,24 @@ def test_batch_host_tail():
         assert g and g[0] == keys[w], (line[:30], g)
         assert O.c_check_key_m22000(line, [keys[w]], False, nc) == g
     assert st["pmks"] == 4 * n_per + 200 - 2 and st["tail_pmks"] == 4 * n_per + 200 - 2 - 6 * 32768
-    assert st["tail_waves"] == 0, st  # the remainder came from the host backend
+    if os.environ.get("DWPA_HOST_TAIL") == "0":
+        assert st["tail_waves"] > 0, st  # the switch keeps the remainder on the GPU
+    else:
+        assert st["tail_waves"] == 0, st  # the remainder came from the host backend
+
+
+def test_batch_host_tail_switch_off():
+    """The same batch with DWPA_HOST_TAIL=0 (read once per process, so in a child): the remainder runs as GPU tail
+    waves and every result is the same."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_gpu_configs.py") + "::test_batch_host_tail"],
+                       cwd=root, env=dict(os.environ, DWPA_HOST_TAIL="0"), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "1 passed" in r.stdout
 
 
 def test_batch_fanout_dedup_and_mixed_salt_lengths():
