@@ -41,9 +41,11 @@ def job_args(j):
 def _device_path_for_gpu_tests(request, monkeypatch):
     """GPU tests measure the device path: the library's small-call routing to its host backend (ABI 4,
     dwpa_config.host_max_pmks) is off for them, so a one-key parity check runs the HIP kernels, not the CPU.  Tests
-    marked host_routing exercise the routing and set it themselves."""
+    marked host_routing exercise the routing and set it themselves.  DWPA_TEST_HOST_BACKEND=1 turns it around: every
+    check call with a derive goes to the host backend (to run a GPU test's jobs through it on the GPU box's CPU)."""
     if request.node.get_closest_marker("gpu") and not request.node.get_closest_marker("host_routing"):
-        monkeypatch.setenv("DWPA_HOST_MAX_PMKS", "-1")
+        host = os.environ.get("DWPA_TEST_HOST_BACKEND") == "1"
+        monkeypatch.setenv("DWPA_HOST_MAX_PMKS", "1000000000" if host else "-1")
         monkeypatch.delenv("DWPA_CPU_FALLBACK", raising=False)
     yield
 

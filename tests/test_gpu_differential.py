@@ -12,7 +12,8 @@ the same batches:
 
 Jobs run as check_batch calls of 1..400 jobs, plus single calls for a sample.  The size is
 DWPA_DIFF_JOBS (default 1,500, ~20 s on one MI355X); round 5 ran it once at 60,000 jobs
-(profiles/r05/differential/)."""
+(profiles/r05/differential/), round 6 at 30,000 on the device and 30,000 on the host backend
+(DWPA_TEST_HOST_BACKEND=1, tests/conftest.py; profiles/r06/differential/)."""
 import os
 import random
 from concurrent.futures import ThreadPoolExecutor
@@ -75,6 +76,8 @@ def test_differential_mixed_jobs():
     for j in range(0, n, 97):
         assert dwpa_amd.check_key_m22000(*jobs[j]) == exp[j], j
     hits = sum(1 for e in exp if e)
+    backend = {0: "device", 1: "host backend", 2: "host fallback"}[dwpa_amd.check_stats()["backend"]]
     print(f"differential: {n} jobs, {hits} hits, "
-          f"{sum(1 for e in exp if e and e[1] not in (None, 0))} with a nonce correction, 0 mismatches")
+          f"{sum(1 for e in exp if e and e[1] not in (None, 0))} with a nonce correction, 0 mismatches "
+          f"(last call on the {backend})")
     assert hits > n // 4
