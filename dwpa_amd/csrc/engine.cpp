@@ -231,6 +231,7 @@ struct Device {
     hipEvent_t vs_go = nullptr, vs_done = nullptr;  // check path: fan-out of the keyver-3 verify onto `side`
     hipEvent_t head_done = nullptr, tail_done = nullptr, prep_done = nullptr;
     hipEvent_t head_end = nullptr;  // check path: this context's last PBKDF2 head (the device's head fence)
+    double tail_share = 0.75;     // check path: share of the head's time the host tail may take (host_tail_fits)
     PinnedArena stage;            // check path: host staging of the derive uploads
     MappedHost hits_host;         // check path: hit count + hits written by k_hits_out
     TableBuilder tb;              // check path: line and attempt tables of the current call (capacity kept)
@@ -628,12 +629,16 @@ static bool host_tail_knob() {
 // The PBKDF2 remainder below one wave per SIMD (the tail) goes to the host backend when the host derives it well
 // within the head's time: the head then fills whole waves on every SIMD and no lone tail wave outlasts it.  A head
 // wave time is ~6.5-7 ms (C2 6.50 ms, the C5 head 7.03 ms per wave per SIMD, CHANGELOG.md round 4/5); the host gets
-// 3/4 of the head's estimated time, so the GPU never waits for it on a host with the measured speed.
+// a share of the head's estimated time (d.tail_share, at most 3/4), so the GPU does not wait for it on a host with
+// the measured speed.  A host busier than measured (other workers on the same cores) is caught by finish_derive: a
+// tail that came after the head halves the share, and every later tail brings it back by a quarter.
 constexpr double HEAD_WAVE_S = 6.5e-3, HOST_TAIL_SHARE = 0.75;
-static bool host_tail_fits(uint32_t nt, uint32_t nh) {
+static bool host_tail_fits(Device& d, uint32_t nt, uint32_t nh) {
     if (!host_tail_knob() || !nt) return false;
     const double head_s = (double)nh / (double)std::max<uint32_t>(1, pbkdf2_wave_unit()) * HEAD_WAVE_S;
-    return (double)nt <= host_pmks_in(HOST_TAIL_SHARE * head_s, host_threads(SIZE_MAX, 1));
+    const double share = d.tail_share;
+    d.tail_share = std::min(HOST_TAIL_SHARE, d.tail_share * 1.25);
+    return (double)nt <= host_pmks_in(share * head_s, host_threads(SIZE_MAX, 1));
 }
 
 // Head/tail split of one derive.  PBKDF2 is issue-bound, so a launch takes as long as its fullest SIMD: nu unique
@@ -776,7 +781,7 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
     st.n = n;
     st.nh = nh;
     st.nu = nu;
-    if (allow_host_tail && nh < nu && host_tail_fits(nu - nh, nh)) {
+    if (allow_host_tail && nh < nu && host_tail_fits(d, nu - nh, nh)) {
         // the remainder on the host backend, beside the head: its keys' bytes (T), salt blocks (spool) and SoA rows
         // in pinned memory, uploaded by finish_derive once the thread is done
         const uint32_t nt = nu - nh;
@@ -878,6 +883,11 @@ static int derive_slots(Device& d, const SlotTable& T, size_t b, size_t e, const
 static int finish_derive(Device& d, DeriveStage& st) {
     if (!st.host_tail) return 0;
     if (st.job.t.joinable()) st.job.t.join();
+    // the head had already ended: the GPU waited for the host, so give later tails less of the head's time
+    if (hipEventQuery(d.head_end) == hipSuccess) {
+        d.tail_share = std::max(0.05, d.tail_share * 0.5);
+        if (PhaseTrace().on) fprintf(stderr, "[dwpa] host tail after the head: share now %.3f\n", d.tail_share);
+    }
     const uint32_t cap = d.batch.cap, nh = st.nh, nt = st.nu - st.nh;
     uint32_t* upmk = (uint32_t*)d.upmk.p;
     if (st.job.rc == 0) {
