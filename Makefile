@@ -67,7 +67,7 @@ clean:
 
 tools: tools/bin/valu_peak tools/bin/pbkdf2_lab tools/bin/valu_lat tools/bin/valu_peak64 tools/bin/inflate_bench \
        tools/bin/inflate_check tools/bin/item_queue_check tools/bin/rules_fuzz_asan tools/bin/clock_idle \
-       tools/bin/inflate_check_tsan tools/bin/tail_placement tools/bin/parse_fuzz_asan tools/bin/host_check_fuzz_asan tools/bin/vgpr_bank
+       tools/bin/inflate_check_tsan tools/bin/tail_placement tools/bin/parse_fuzz_asan tools/bin/host_check_fuzz_asan tools/bin/host_pbkdf2_paths tools/bin/vgpr_bank
 
 tools/bin/valu_lat: tools/valu_lat.hip
 	@mkdir -p tools/bin
@@ -118,6 +118,11 @@ tools/bin/host_check_fuzz_asan: tools/host_check_fuzz.cpp $(SRC)/host_check.cpp 
 	@mkdir -p tools/bin
 	$(HIPCC) -O1 -g -std=c++17 -Iinclude -I$(SRC) -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
 	    -o $@ tools/host_check_fuzz.cpp $(SRC)/host_check.cpp $(SRC)/host_crypto.cpp $(SRC)/m22000_host.cpp -lpthread
+
+# one thread's time per call of each host PBKDF2 loop (SHA-NI 1/2/4 chains, AVX-512 1/2/3 registers, scalar)
+tools/bin/host_pbkdf2_paths: tools/host_pbkdf2_paths.cpp $(SRC)/host_crypto.cpp $(SRC)/host_crypto.hpp
+	@mkdir -p tools/bin
+	$(HIPCC) -O3 -std=c++17 -Iinclude -I$(SRC) -o $@ tools/host_pbkdf2_paths.cpp
 
 tools/bin/clock_idle: tools/clock_idle.hip
 	@mkdir -p tools/bin
