@@ -1140,16 +1140,21 @@ static int check_batch_device(const dwpa_job* jobs, size_t njobs, dwpa_result* o
     return rc;
 }
 
-// Routing: a small call (at least one PBKDF2 derive, at most host_max_pmks PMK-equivalents) runs on the host without
-// touching the device; every other call on the device, and on the host after a device-side failure when
-// allow_cpu_fallback is on.
+// Routing: a small call runs on the host without touching the device -- one with PBKDF2 derives and at most
+// host_max_pmks PMK-equivalents, or one without derives (caller-PMK checks, common.php:592,606,919) whose verify work
+// the host does in tens of microseconds (HOST_VERIFY_MAX compressions: a PMKID check, or an EAPOL window of a few
+// dozen attempts; a GPU call costs ~0.1 ms however little it does) -- both 8x larger before the process's first device
+// call; every other call on the device, and on the host after a device-side failure when allow_cpu_fallback is on.
+// host_max_pmks <= 0 turns both off.
+constexpr double HOST_VERIFY_MAX = 1000.0;
 static int check_batch_impl(const dwpa_job* jobs, size_t njobs, dwpa_result* out, int* rcs) {
     const auto t0 = std::chrono::steady_clock::now();
     g_check_stats = dwpa_check_stats{};
     g_have_check_stats = true;
     const HostCost hc = host_cost(jobs, njobs);
-    const double thr = host_max_pmks() * (g_device_warm.load(std::memory_order_relaxed) ? 1.0 : COLD_FACTOR);
-    if (hc.derives && hc.pmk_equiv <= thr)
+    const double cold = g_device_warm.load(std::memory_order_relaxed) ? 1.0 : COLD_FACTOR;
+    const double thr = host_max_pmks() * cold;
+    if (thr > 0 && (hc.derives ? hc.pmk_equiv <= thr : hc.pmk_equiv * 16388.0 <= HOST_VERIFY_MAX * cold))
         return check_batch_host(jobs, njobs, out, rcs, DWPA_BACKEND_HOST_SMALL, t0);
     const int rc = check_batch_device(jobs, njobs, out, rcs, t0);
     if (host_retry_code(rc) && cpu_fallback_on())

@@ -101,7 +101,8 @@ def test_pbkdf2_host_equals_device():
 
 
 def test_default_routing():
-    """One key: the host backend.  Thousands of keys: the device, cold or warm (8 x the default budget is far below)."""
+    """One key: the host backend.  Thousands of keys: the device, cold or warm (8 x the default budget is far below).
+    Caller-PMK checks: a PMKID line's one HMAC on the host, a 521-attempt EAPOL window on the (warm) device."""
     rng = random.Random(8)
     essid, ap, sta, an, sn = S.random_net(rng)
     psk = S.fast_psk(rng)
@@ -111,6 +112,16 @@ def test_default_routing():
     assert M.check_stats()["backend"] == L.DWPA_BACKEND_HOST_SMALL
     keys = [S.fast_psk(rng) for _ in range(40000)] + [psk]
     assert dwpa_amd.check_key_m22000(line, keys) == [psk, 5, "BE", S.pmk(psk, essid)]
+    assert M.check_stats()["backend"] == L.DWPA_BACKEND_DEVICE
+    # caller-PMK checks (common.php:592,606,919): a PMKID line's one HMAC on the host, a 521-attempt EAPOL window
+    # (the device is warm now) on the GPU
+    pline = S.pmkid_line(psk, essid, ap, sta)
+    pmk = S.pmk(psk, essid)
+    r = dwpa_amd.check_key_m22000(pline, [b""], pmk, 258)
+    assert r == O.c_check_key_m22000(pline, [b""], pmk, 258) and r
+    assert M.check_stats()["backend"] == L.DWPA_BACKEND_HOST_SMALL
+    r = dwpa_amd.check_key_m22000(line, [b""], pmk, 258)
+    assert r == O.c_check_key_m22000(line, [b""], pmk, 258) and r
     assert M.check_stats()["backend"] == L.DWPA_BACKEND_DEVICE
 
 

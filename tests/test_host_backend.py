@@ -252,7 +252,8 @@ def test_routing_without_a_device(monkeypatch):
     """No device here.  allow_cpu_fallback off and host_max_pmks -1: every compute call fails loudly (DWPA_E_NODEV).
     The default threshold: a small call (one key) is answered by the host backend (backend 1); with host_max_pmks 50
     a call of 500 keys (above 8 x 50 before any device call) is DWPA_E_NODEV.  allow_cpu_fallback on: dwpa_init returns 0 and the large
-    call is answered too (backend 2).  Caller-PMK calls (no derive) need the fallback."""
+    call is answered too (backend 2).  Caller-PMK calls (no derive) are host calls when their verify work is tiny, and
+    need the fallback above that."""
     monkeypatch.delenv("DWPA_CPU_FALLBACK", raising=False)
     monkeypatch.delenv("DWPA_HOST_MAX_PMKS", raising=False)
     lib = L.load()
@@ -268,8 +269,10 @@ def test_routing_without_a_device(monkeypatch):
     small = (line, [psk], False, 128)
     nlarge = 500
     large = (line, [S.fast_psk(rng) for _ in range(nlarge - 1)] + [psk], False, 128)
-    caller = (line, [b""], S.pmk(psk, essid), 128)
-    exp = {k: O.c_check_key_m22000(*j) for k, j in (("small", small), ("large", large), ("caller", caller))}
+    caller = (line, [b""], S.pmk(psk, essid), 2000)  # 4,001 attempts: above the cold host budget for caller-PMK checks
+    small_caller = (line, [b""], S.pmk(psk, essid), 8)  # 17 attempts: answered by the host backend
+    exp = {k: O.c_check_key_m22000(*j) for k, j in (("small", small), ("large", large), ("caller", caller),
+                                                     ("small_caller", small_caller))}
     assert all(exp.values())
     try:
         assert init(-1, -1) == L.DWPA_E_NODEV
@@ -284,6 +287,8 @@ def test_routing_without_a_device(monkeypatch):
         assert dwpa_amd.check_key_m22000(*small) == exp["small"]
         assert M.check_stats()["backend"] == L.DWPA_BACKEND_HOST_SMALL
         assert dwpa_amd.pbkdf2_pmk([psk], essid)[0] == S.pmk(psk, essid)
+        assert dwpa_amd.check_key_m22000(*small_caller) == exp["small_caller"]
+        assert M.check_stats()["backend"] == L.DWPA_BACKEND_HOST_SMALL
         assert init(-1, 50) == L.DWPA_E_NODEV
         with pytest.raises(L.DwpaError):
             dwpa_amd.check_key_m22000(*large)
