@@ -43,17 +43,17 @@ PEAK_COMPRESSIONS = SIMDS * CLOCK_HZ * 64 / C_MIN_CYCLES
 # over that workload's bench command (FETCH_SIZE doubled as MI355X_MICROARCH.md "HBM [CDNA4]" prescribes, plus
 # WRITE_SIZE; per-launch medians divided by the PMKs of the launch).  PMC counters cannot be read inside a timed
 # run, so the bench scales the measured per-PMK figure to its launches.
-#   c2/c4: k_pbkdf2_gfx950_q (the work-queue kernel multi-round scans run), profiles/r05/pmc_final (round 5's last
-#          code, the two full 16,777,216-PMK launches): FETCH 358,833,216 B x 2 = 42.8 B/PMK (a slot range's two
-#          output-block items are taken back to back, so the second read of each 40-byte key midstate is an L2 hit)
-#          + WRITE 553,910,272 B = 33.0 B/PMK (round 4, profiles/r04/traffic_c2: FETCH 356,765,120 B; round 3:
-#          359,755,264 B; round 2, profiles/r02/traffic_q: 365,219,648 B; the same WRITE)
+#   c2/c4: k_pbkdf2_gfx950_q (the work-queue kernel multi-round scans run), profiles/r06/pmc (round 6's last code,
+#          tools/profile_traffic.sh, median of the full 16,777,216-PMK launches): FETCH 360,959,040 B x 2 = 43.0 B/PMK
+#          (a slot range's two output-block items are taken back to back, so the second read of each 40-byte key
+#          midstate is an L2 hit) + WRITE 553,910,272 B = 33.0 B/PMK (round 5, profiles/r05/pmc_final: FETCH
+#          358,833,216 B; round 4: 356,765,120 B; round 2: 365,219,648 B; the same WRITE)
 #   c3:    k_pbkdf2_gfx950_mg_q + k_verify<PMKID> + k_verify<keyver 2> per dwpa_scan_run (the roofline's events
 #          bracket all three), profiles/r02/traffic_q3: 463.9 + 446.6 + 1,093.9 MB for 13,445,190 PMKs
-TRAFFIC_BYTES_PER_PMK = {"c2": (2 * 358833216 + 553910272) / 16777216, "c4": (2 * 358833216 + 553910272) / 16777216,
+TRAFFIC_BYTES_PER_PMK = {"c2": (2 * 360959040 + 553910272) / 16777216, "c4": (2 * 360959040 + 553910272) / 16777216,
                          "c3": (463.935e6 + 446.650e6 + 1093.884e6) / 13445190}
-TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950_q, profiles/r05/pmc_final",
-                  "c4": "k_pbkdf2_gfx950_q per PMK as measured on c2, profiles/r05/pmc_final",
+TRAFFIC_SOURCE = {"c2": "k_pbkdf2_gfx950_q, profiles/r06/pmc",
+                  "c4": "k_pbkdf2_gfx950_q per PMK as measured on c2, profiles/r06/pmc",
                   "c3": "k_pbkdf2_gfx950_mg_q + k_verify, profiles/r02/traffic_q3"}
 # Algorithmic bytes per PMK: PBKDF2 reads the 40-byte key midstate once and writes the 32-byte PMK (c2/c4, the
 # kernel the roofline names).  c3's events also bracket the verify, which reads each PMK (32 B) and candidate id
