@@ -1,7 +1,6 @@
 """CPU: the library's host logic (parsing with PHP semantics, attempt-list construction, rule parsing) against
 the oracle and the golden fixtures -- no device needed."""
 import ctypes
-import struct
 
 import pytest
 
