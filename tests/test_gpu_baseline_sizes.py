@@ -11,7 +11,8 @@ O.c_check_key_m22000 (the restatement of check_key_m22000, common.php:157-307).
 * C2 -- a 100M-word dictionary resident in HBM against EAPOL keyver-2 lines of one ESSID in hashcat nonce mode
   (--nonce-error-corrections=8, help_crack.py:773), as the client runs it (~22 s).
 * C3 -- one dwpa_scan_run over 1,024 ESSIDs of a word x rule batch amplified on the GPU (every group of the work
-  unit in one PBKDF2 launch); the expected hits come from the rule oracle (oracle/rules.py).
+  unit in one PBKDF2 launch); the expected hits come from the rule oracle (oracle/rules.py).  And C3's base size:
+  10,000 words x the rule set over 8 ESSIDs in 4,096-word batches (~11.8 M PMKs).
 """
 import random
 
@@ -163,3 +164,64 @@ def test_c3_scan_run_1024_essids_rules():
     for h in hits:
         _check_hit(lines[h["line"]], valid[h["cand"]], line_essid[h["line"]], h, 8)
     sc.close()
+
+
+def test_c3_full_base_dictionary_rules():
+    """SURVEY.md 8(d) C3's base size: 10,000 words x the WPA rule set (~1.48 M candidates per ESSID, 8..63 filter on
+    the GPU) against 8 ESSIDs of 2 lines each, in dwpa_scan_run batches of 4,096 words x every rule (the last batch
+    partial), ~11.8 M PMKs.  PSKs are planted at (word, rule) positions across the keyspace -- the first and last
+    word, both sides of the batch boundaries, the last rule -- each from the rule oracle's expansion of that one word;
+    every planted (line, candidate) must be reported, and every reported hit must be the line's PSK by the oracle
+    (another rule may produce the same string: such duplicates are genuine) with the oracle's PMK and correction."""
+    rng = random.Random(105)
+    rules = wpa_rules()
+    parsed = [p for p in (R.parse(x) for x in rules) if p]
+    nr = len(parsed)
+    assert nr == len(rules)
+    nw, per = 10000, 4096
+    words = [S.random_psk(rng, 6, 12) for _ in range(nw)]
+    spots = [(0, 0), (nw - 1, nr - 1), (per - 1, 3), (per, nr // 2), (2 * per - 1, nr - 1), (2 * per, 1),
+             (rng.randrange(nw), rng.randrange(nr)), (rng.randrange(nw), rng.randrange(nr))]
+    plants = []
+    for w, r in spots:  # the next rule of the word whose candidate passes the 8..63 filter
+        for k in range(nr):
+            c = R.apply(parsed[(r + k) % nr], words[w])
+            if c is not None and 8 <= len(c) <= 63:
+                plants.append((w, (r + k) % nr, c))
+                break
+    assert len(plants) == len(spots)
+    lines, line_essid, want = [], [], set()
+    for e in range(8):
+        essid = b"c3-%d-" % e + bytes(rng.choice(b"abcdef") for _ in range(rng.randint(1, 12)))
+        _, ap, sta, an, sn = S.random_net(rng)
+        for k in range(2):
+            i = 2 * e + k
+            if i < len(plants):
+                w, r, psk = plants[i]
+                want.add((len(lines), w * nr + r))
+            else:
+                psk = b"not-in-keyspace-%d" % i
+            if (e + k) % 2 == 0:
+                lines.append(S.pmkid_line(psk, essid, rng.randbytes(6), sta))
+            else:
+                lines.append(S.eapol_line(psk, essid, ap, sta, an, sn, 1 + (e % 3), rng.randint(-4, 4),
+                                          rng.choice(["LE", "BE"]), rng=rng))
+            line_essid.append(essid)
+    d = Dictionary.from_words(words)
+    sc = dwpa_amd.Scan(lines, nc=8, nc_mode=0, batch=(per * nr + 63) // 64 * 64)
+    assert sc.groups == 8
+    assert sc.set_rules("\n".join(rules)) == nr
+    hits = []
+    for w0 in range(0, nw, per):
+        sc.load_rules(d.off.ptr, d.data.ptr, w0, min(per, nw - w0))
+        sc.run()
+        hits += sc.hits()
+    sc.close()
+    got = {(h["line"], h["cand"]) for h in hits}
+    assert want <= got, sorted(want - got)
+    psk_of = {li: (plants[li][2] if li < len(plants) else None) for li in range(len(lines))}
+    for h in hits:
+        w, r = divmod(h["cand"], nr)
+        cand = R.apply(parsed[r], words[w])
+        assert cand == psk_of[h["line"]], (h, cand)
+        _check_hit(lines[h["line"]], cand, line_essid[h["line"]], h, 8)
