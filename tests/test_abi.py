@@ -147,3 +147,21 @@ def test_python_nc_outside_int32_is_refused():
         assert e.value.code == L.DWPA_E_ARG
         with pytest.raises(L.DwpaError):
             dwpa_amd.check_batch([(pmkid, [b"aaaa1234"], False, nc)])
+
+
+def test_plain_c_client(tmp_path):
+    """The header is plain C99 (what PHP FFI::cdef and any C caller consume): tools/abi_c_client.c compiles against it
+    with -Wall -Wextra -Werror, links libdwpa22000.so and checks the reference's challenge (help_crack.py:692-699) with
+    dwpa_check_m22000 and dwpa_check_batch, the host backend allowed (no GPU here: it answers)."""
+    import subprocess
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "abi_c_client"
+    lib = os.path.join(ROOT, "dwpa_amd", "lib")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tools", "abi_c_client.c"), "-L", lib, "-ldwpa22000",
+                    "-Wl,-rpath," + lib, "-o", str(exe)], check=True)
+    env = dict(os.environ, DWPA_HOST_MAX_PMKS="1000000000")
+    r = subprocess.run([str(exe)] + [l.decode() for l in S.CHALLENGE_LINES], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "line 1: rc 1 key_index 1 nc_valid 1 nc 4 endian 2" in r.stdout and "batch: both hit" in r.stdout
