@@ -84,6 +84,17 @@ def main():
             rows.append({"call": f"check_key_m22000, {kind}, {label}", "ms": round(ms, 3),
                          "oracle_openssl_1core_ms": round(cpu, 3), "backend": backend,
                          "same_result": got == O.c_check_key_m22000(*job)})
+    # a GPU-less server's bulk call: a C5-shaped batch (PMKID + keyver 1/2/3, nc=128, 202 keys per job), all on the
+    # host backend (DWPA_HOST_MAX_PMKS above: every call with a derive is a host call), every result vs the oracle
+    jobs, _ = S.c5_plan(seed=9, per_kind=25, essids=20, zero_pmk=1)
+    nkeys = sum(len(j[1]) for j in jobs)
+    ms = med(lambda: dwpa_amd.check_batch(jobs), 3)
+    got = dwpa_amd.check_batch(jobs)
+    backend = M.check_stats()["backend"]
+    exp = [O.c_check_key_m22000(*j) for j in jobs]
+    rows.append({"call": f"check_batch, C5-shaped {len(jobs)} jobs x 202 keys, nc=128 (a GPU-less server's bulk call)",
+                 "keys": nkeys, "ms": round(ms, 1), "pmk_per_s": round(nkeys / ms * 1e3), "backend": backend,
+                 "same_result": got == exp})
     out["rows"] = rows
     out["all_same"] = all(r["same_result"] for r in rows)
     print(json.dumps(out))
