@@ -1,6 +1,7 @@
 // engine.cpp -- libdwpa22000.so: device contexts, the server-side check path (routed to the host backend in
-// host_check.cpp for small calls, and without a device when allowed), the device-resident scan API and the C-ABI
-// exports declared in include/dwpa22000.h.
+// host_check.cpp for small calls, and without a device when allowed; a device call derives its PBKDF2 remainder on
+// the host beside the GPU head when that fits), the device-resident scan API and the C-ABI exports declared in
+// include/dwpa22000.h.
 //
 // Process model: one process may drive every visible MI355X.  crack_files (crack.cpp) runs a stager and a scanner
 // thread per device worker over ONE shared dictionary stream, cut into work items by guided self-scheduling
