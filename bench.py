@@ -615,7 +615,10 @@ def main():
         sc.verify(0, hs)
         return cnt
 
-    for s, (_, b) in enumerate(weak_units(rank, 0, args.warmup, w.nbatches)):
+    # the batch order is rotated so that the first timed step scans the planted batch: every timed window, however
+    # short, holds at least one scan whose hits verify_timed_hits checks against the plant
+    rot = (getattr(w, "plant_batch", 0) - args.warmup) % w.nbatches
+    for s, (_, b) in enumerate(weak_units(rank, 0, args.warmup, w.nbatches, rot)):
         step(b, s % P)
     sync_all()
     for k in range(P):
@@ -628,7 +631,7 @@ def main():
     t0 = time.perf_counter()
     done = 0
     counts = []
-    for s, (_, b) in enumerate(weak_units(rank, args.warmup, args.steps, w.nbatches)):
+    for s, (_, b) in enumerate(weak_units(rank, args.warmup, args.steps, w.nbatches, rot)):
         counts.append(step(b, s % P, kev[s]))
         done += counts[-1]
     sync_all()
@@ -650,7 +653,8 @@ def main():
     for k in range(P):
         timed_hits += w.scans[k].hits(streams[k].handle)
     timed_ok, hits_check = verify_timed_hits(w, timed_hits,
-                                             [b for _, b in weak_units(rank, args.warmup, args.steps, w.nbatches)])
+                                             [b for _, b in weak_units(rank, args.warmup, args.steps, w.nbatches,
+                                                                       rot)])
     step(w.plant_batch, 0)
     plant_ok = bool(w.check(w.scans[0].hits(streams[0].handle)))
     hits_check["plant_rescan_ok"] = plant_ok

@@ -10,9 +10,9 @@ region, the max elapsed time and the total PMK count.
 from __future__ import annotations
 
 
-def weak_units(rank: int, first_step: int, steps: int, nbatches: int):
-    """(shard, batch) scanned by `rank` at each step: its own shard, step s -> batch s mod nbatches."""
-    return [(rank, s % nbatches) for s in range(first_step, first_step + steps)]
+def weak_units(rank: int, first_step: int, steps: int, nbatches: int, offset: int = 0):
+    """(shard, batch) scanned by `rank` at each step: its own shard, step s -> batch (s + offset) mod nbatches."""
+    return [(rank, (s + offset) % nbatches) for s in range(first_step, first_step + steps)]
 
 
 def contiguous_shard(n: int, k: int, g: int):
