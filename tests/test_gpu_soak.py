@@ -40,7 +40,7 @@ def _calls(seed):
     nets = [S.random_net(rng) for _ in range(6)]
     seq = []
     for r in range(16):
-        shape = "big" if r in (3, 11) else rng.choice(["one", "one", "batch", "batch", "mid"])
+        shape = "big" if r in (3, 11) else "bigt" if r == 7 else rng.choice(["one", "one", "batch", "batch", "mid"])
         if shape == "one":
             seq.append(("one", [_job(rng, nets, rng.randint(0, 20), rng.choice([0, 8, 128]),
                                      caller=rng.random() < 0.3)]))
@@ -49,8 +49,10 @@ def _calls(seed):
                                        caller=rng.random() < 0.2) for _ in range(rng.randint(1, 24))]))
         elif shape == "mid":
             seq.append(("batch", [_job(rng, nets, rng.randint(50, 100), 128) for _ in range(rng.randint(4, 8))]))
-        else:  # > 2 waves per SIMD of unique keys: the check path's head/tail split; the planted key early
+        elif shape == "big":  # > 2 waves per SIMD of unique keys: the head/tail split, a tail the GPU derives
             seq.append(("batch", [_job(rng, nets, 36000, 8, plant_at=rng.randrange(600)) for _ in range(2)]))
+        else:  # a head of 2 waves per SIMD and a small remainder: the tail derived on the host beside the head
+            seq.append(("batch", [_job(rng, nets, 33000, 8, plant_at=rng.randrange(600)) for _ in range(2)]))
     return seq
 
 
@@ -75,6 +77,19 @@ def _expected(job, got):
 
 
 def test_many_calls_of_every_shape_from_three_threads():
+    _soak()
+
+
+@pytest.mark.host_routing
+def test_many_calls_with_the_library_routing_from_three_threads():
+    """The same lifetime with the library's own routing: small calls on the host backend, the rest
+    on the device with host-derived tails, three threads sharing the host pool and the call contexts."""
+    from dwpa_amd import m22000 as M
+    M.init()
+    _soak()
+
+
+def _soak():
     seqs = [_calls(1000 + t) for t in range(3)]
     results = [None] * 3
 
