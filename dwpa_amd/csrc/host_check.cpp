@@ -116,6 +116,64 @@ void mic_md5(const uint32_t kck_be[4], const uint32_t* blocks, uint32_t nblk, ui
     md5_compress(mic, w);
 }
 
+// Keyver 1/2 attempts at[0..3] (equal block counts) against the line: the first of them whose MIC matches (0..3) or
+// -1.  The PRF, the PTK's outer hash and the keyver 2 MIC run as four SHA-1 chains in lock step; keyver 1's HMAC-MD5
+// per attempt.
+int64_t verify_att4(const LineDev& L, const AttDev* at, const uint32_t* pool, const uint32_t pre[5],
+                    const uint32_t op[5]) {
+    uint32_t st[4][5], w[4][16];
+    const uint32_t* wp[4] = {w[0], w[1], w[2], w[3]};
+    for (int n = 0; n < 4; n++) memcpy(st[n], pre, 20);
+    for (uint32_t b = 0; b < at[0].nblk; b++) {
+        for (int n = 0; n < 4; n++) att_block(L, at[n], pool, b, w[n]);
+        sha1_compress_x4(st, wp);
+    }
+    uint32_t ptk[4][5];
+    for (int n = 0; n < 4; n++) {
+        memcpy(w[n], st[n], 20);
+        w[n][5] = 0x80000000u;
+        for (int t = 6; t < 15; t++) w[n][t] = 0;
+        w[n][15] = (64 + 20) * 8;
+        memcpy(ptk[n], op, 20);
+    }
+    sha1_compress_x4(ptk, wp);
+    uint32_t mic[4][5];
+    if (L.keyver == 2) {  // HMAC-SHA1(KCK, EAPOL) (common.php:268), as mic_sha1
+        uint32_t ko[4][16], mo[4][5];
+        for (int n = 0; n < 4; n++)
+            for (int t = 0; t < 16; t++) {
+                const uint32_t v = t < 4 ? ptk[n][t] : 0;
+                w[n][t] = v ^ 0x36363636u;
+                ko[n][t] = v ^ 0x5c5c5c5cu;
+            }
+        for (int n = 0; n < 4; n++) memcpy(mic[n], SHA1_IV, 20);
+        sha1_compress_x4(mic, wp);
+        for (uint32_t b = 0; b < L.mic_nblk; b++) {
+            const uint32_t* blk = pool + L.mic_off + 16 * (size_t)b;
+            const uint32_t* bp[4] = {blk, blk, blk, blk};
+            sha1_compress_x4(mic, bp);
+        }
+        const uint32_t* kop[4] = {ko[0], ko[1], ko[2], ko[3]};
+        for (int n = 0; n < 4; n++) memcpy(mo[n], SHA1_IV, 20);
+        sha1_compress_x4(mo, kop);
+        for (int n = 0; n < 4; n++) {
+            memcpy(w[n], mic[n], 20);
+            w[n][5] = 0x80000000u;
+            for (int t = 6; t < 15; t++) w[n][t] = 0;
+            w[n][15] = (64 + 20) * 8;
+        }
+        sha1_compress_x4(mo, wp);
+        for (int n = 0; n < 4; n++)
+            if (memcmp(mo[n], L.target, 16) == 0) return n;
+        return -1;
+    }
+    for (int n = 0; n < 4; n++) {  // keyver 1: HMAC-MD5(KCK, EAPOL) (common.php:264)
+        mic_md5(ptk[n], pool + L.mic_off, L.mic_nblk, mic[n]);
+        if (memcmp(mic[n], L.target, 16) == 0) return n;
+    }
+    return -1;
+}
+
 // The first attempt of the line's list for key ordinal `ord` under which `pmk` verifies, or -1 (PMKID lines: 0 / -1).
 int64_t verify_pmk(const TableBuilder& tb, uint32_t li, uint32_t ord, const uint32_t pmk[8]) {
     const LineDev& L = tb.lines[li];
@@ -141,7 +199,14 @@ int64_t verify_pmk(const TableBuilder& tb, uint32_t li, uint32_t ord, const uint
         pmk_mid_sha1(pmk, ip, op);
         memcpy(pre, ip, 20);
         for (uint32_t b = 0; b < L.pre_nblk; b++) sha1_compress(pre, pool + L.pre_off + 16 * (size_t)b);
-        for (uint32_t a = 0; a < L.natt; a++) {
+        uint32_t a = 0;
+        // four attempts at a time, their SHA-1 compressions in lock step (a miss walks every attempt of the window)
+        for (; a + 4 <= L.natt; a += 4) {
+            if (at[a].nblk != at[a + 1].nblk || at[a].nblk != at[a + 2].nblk || at[a].nblk != at[a + 3].nblk) break;
+            const int64_t r = verify_att4(L, at + a, pool, pre, op);
+            if (r >= 0) return a + r;
+        }
+        for (; a < L.natt; a++) {
             uint32_t st[5], ptk[5], mic[5];
             memcpy(st, pre, 20);
             for (uint32_t b = 0; b < at[a].nblk; b++) {

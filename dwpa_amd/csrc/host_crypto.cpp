@@ -257,6 +257,25 @@ DWPA_SHA_TARGET static void sha1_ni(uint32_t st[5], const uint32_t w[16]) {
     st[4] = (uint32_t)_mm_extract_epi32(e[0], 3);
 }
 
+// Four independent compressions in lock step (the verify's nonce-correction attempts, host_check.cpp).
+DWPA_SHA_TARGET static void sha1_ni_x4(uint32_t (*st)[5], const uint32_t* const* w) {
+    __m128i abcd[4], e[4], m[4][4];
+    for (int n = 0; n < 4; n++) {
+        abcd[n] = _mm_set_epi32((int)st[n][0], (int)st[n][1], (int)st[n][2], (int)st[n][3]);
+        e[n] = _mm_set_epi32((int)st[n][4], 0, 0, 0);
+        for (int q = 0; q < 4; q++)
+            m[n][q] = _mm_set_epi32((int)w[n][4 * q], (int)w[n][4 * q + 1], (int)w[n][4 * q + 2], (int)w[n][4 * q + 3]);
+    }
+    sha1ni_x<4>(abcd, e, m);
+    for (int n = 0; n < 4; n++) {
+        st[n][0] = (uint32_t)_mm_extract_epi32(abcd[n], 3);
+        st[n][1] = (uint32_t)_mm_extract_epi32(abcd[n], 2);
+        st[n][2] = (uint32_t)_mm_extract_epi32(abcd[n], 1);
+        st[n][3] = (uint32_t)_mm_extract_epi32(abcd[n], 0);
+        st[n][4] = (uint32_t)_mm_extract_epi32(e[n], 3);
+    }
+}
+
 // SHA-256: state as {A, B, E, F} and {C, D, G, H} from the high lane down; message words W_4q.. with W_4q in the low
 // lane.  sha256rnds2 runs two rounds on the low two lanes of W + K; block q >= 4 of the schedule is
 // msg2(msg1(W_{q-4}, W_{q-3}) + alignr(W_{q-1}, W_{q-2}, 4), W_{q-1}).
@@ -536,6 +555,13 @@ const Caps& caps() {
 void sha1_compress(uint32_t st[5], const uint32_t w[16]) {
     if (caps().sha_ni) sha1_ni(st, w);
     else sha1_scalar(st, w);
+}
+void sha1_compress_x4(uint32_t (*st)[5], const uint32_t* const* w) {
+    if (caps().sha_ni) {
+        sha1_ni_x4(st, w);
+    } else {
+        for (int n = 0; n < 4; n++) sha1_scalar(st[n], w[n]);
+    }
 }
 void sha256_compress(uint32_t st[8], const uint32_t w[16]) {
     if (caps().sha_ni) sha256_ni(st, w);

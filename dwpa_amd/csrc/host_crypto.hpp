@@ -30,6 +30,8 @@ extern const uint32_t SHA256_IV[8];
 extern const uint32_t MD5_IV[4];
 
 void sha1_compress(uint32_t st[5], const uint32_t w[16]);
+// Four independent SHA-1 compressions in lock step (SHA-NI hides one compression's round latency behind the others).
+void sha1_compress_x4(uint32_t (*st)[5], const uint32_t* const* w);
 void sha256_compress(uint32_t st[8], const uint32_t w[16]);
 void md5_compress(uint32_t st[4], const uint32_t w[16]);
 // Whole-message SHA-1 (HMAC keys longer than one block are hashed first, RFC 2104).
